@@ -1,0 +1,299 @@
+#!/usr/bin/env python3
+"""bench.py — LLA-MPC model-bank tick on MI355X (BASELINE.json metric).
+
+One *step* = one LLA-MPC control tick of the hot path over the whole bank:
+look-back (score every model on the newest transition, slide the W-window, argmin +
+top-K) + look-ahead (H-step RK4 rollout + MPC cost of every (model, candidate)) +
+selection, i.e. ``llampc_plan_device`` (3 kernels).  With --gpus N > 1 each rank owns a
+contiguous shard of N_per_gpu models (weak scaling; config 4 = 8 x 10^4) and every tick
+adds ONE RCCL all-gather of the 1.5 KB shard record plus the on-device merge.
+
+Workload (BASELINE.json configs[1]): ETHZ track, N_models = 10^4 per GPU, H = 20, C = 1
+candidate, W = 10, K = 10, Ts = 0.02, gradual friction change.  Tick inputs are
+synthetic-but-physical: states from the device RK6 plant (Dynamic.sim_continuous)
+driven by the recorded ETHZ controls (tests/golden/dyn_slice.npz) under the gradual
+friction decay D <- D(1 - 1/2600) per tick (rt.py:125-130), xref from ConstantSpeed on the
+packaged ETHZ raceline library.  All tick inputs are resident in HBM before timing.
+
+value = (N_total * C * H + N_total) / (ms_per_step / 1e3)  [model-rollout-steps / s].
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "lla-mpc_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector spec
+FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation (excl. transcendentals)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n-per-gpu", type=int, default=10000)
+    ap.add_argument("--H", type=int, default=20)
+    ap.add_argument("--C", type=int, default=1)
+    ap.add_argument("--W", type=int, default=10)
+    ap.add_argument("--K", type=int, default=10)
+    ap.add_argument("--track", default="ETHZ", choices=["ETHZ", "ETHZMobil"])
+    ap.add_argument("--ticks", type=int, default=64, help="distinct resident tick inputs")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C=64 and latency extras")
+    ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    return ap.parse_args()
+
+
+def make_ticks(args, T, seed=0):
+    """T ticks of (x_prev, u_prev, x_now, uprev, xref, U) for the gradual-friction scenario."""
+    from llampc.models import Dynamic
+    from llampc.mpc import CandidateGenerator, ConstantSpeed
+    from llampc.params import ORCA
+    from llampc.tracks import ETHZ, ETHZMobil
+    d = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))
+    u_rec = d["inputs"]
+    p = ORCA()
+    plant = Dynamic(**p, device=torch_device_index())
+    x = d["states"][:, 0].copy()
+    track = ETHZ() if args.track == "ETHZ" else ETHZMobil()
+    gen = CandidateGenerator(args.C, args.H, seed=2)
+    H, Ts = args.H, 0.02
+    k0 = 100                                    # ticks into the decay
+    Df, Dr = p["Df"] * (1 - 1 / 2600.) ** k0, p["Dr"] * (1 - 1 / 2600.) ** k0
+    packs, projidx = [], 0
+    for t in range(T + 1):
+        u = u_rec[:, t % u_rec.shape[1]]
+        plant.Df, plant.Dr = Df, Dr
+        xn, _ = plant.sim_continuous(x, u.reshape(2, 1), [0, Ts])
+        x_next = xn[:, -1]
+        if t >= 1:
+            mu = (Df + Dr) / (9.81 * p["mass"])
+            xref, projidx, _ = ConstantSpeed(x_next[:2], x_next[3], track, H, Ts, projidx, curr_mu=mu, scale=0.9)
+            U = gen(None, u)
+            packs.append(np.concatenate([x, u, x_next, u, xref.ravel(), U.ravel()]))
+        x = x_next
+        Df -= Df / 2600.
+        Dr -= Dr / 2600.
+    return np.stack(packs[:T])
+
+
+_DEV = [0]
+
+
+def torch_device_index():
+    return _DEV[0]
+
+
+def cpu_baseline(args, seconds):
+    """The oracle (NumPy restatement of the reference path, one core) on the same
+    workload shape: look-back + window/argmin/argsort + H-step RK4 rollout + cost."""
+    from llampc.mpc import generate_bank
+    from oracle import llampc_oracle as O
+    ticks = make_ticks(args, 4)
+    N, H, C = args.n_per_gpu, args.H, args.C
+    bank = generate_bank(N, seed=0)
+    p = O.orca_params()
+    shared = {k: p[k] for k in ("lf", "lr", "mass", "Iz", "Cm1", "Cm2", "Cr0", "Cr2")}
+    win = O.LookbackWindow(N, args.W, args.K)
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+
+    def one(i):
+        pk = ticks[i % len(ticks)]
+        xref = pk[16:16 + 2 * (H + 1)].reshape(2, H + 1)
+        U = pk[16 + 2 * (H + 1):].reshape(C, H, 2)
+        O.plan_cpu(shared, bank, win, pk[0:6], pk[6:8], pk[8:14], U, xref, pk[14:16], 0.02, Q, R, P)
+
+    one(0)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        one(reps + 1)
+        reps += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and reps >= 2) or reps >= 1000:
+            break
+    per = el / reps
+    return {"value": (N * C * H + N) / per, "unit": "model-rollout-steps/s", "cores": 1, "kind": "port",
+            "ms_per_step": per * 1e3,
+            "sample": f"{reps} plan() ticks of the oracle NumPy restatement (oracle/llampc_oracle.py "
+                      f"plan_cpu = reference evaluate_models_vectorized + rt.py window logic + H x "
+                      f"_integrate_batch + nmpc.py cost) at N={N}, H={H}, C={C} on 1 host core "
+                      f"({os.cpu_count()} visible), {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    _DEV[0] = local
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    from llampc import _native as nat
+    from llampc.mpc import generate_bank
+    from llampc.mpc.sharded import ShardedBank
+
+    N_local, H, C, K, W = args.n_per_gpu, args.H, args.C, args.K, args.W
+    N_total = N_local * world
+    T = max(args.ticks, 1)
+    ticks = make_ticks(args, T)
+    dev = torch.device("cuda", local)
+    packs = torch.from_numpy(ticks).to(dev)                 # resident tick inputs [T, L]
+    bank_global = generate_bank(N_total, seed=0 if args.track == "ETHZ" else 1)
+    sb = ShardedBank(bank_global, rank, world, local, W=W)
+    stream = torch.cuda.current_stream(dev)
+    pins = [sb.make_plan_in(packs[i], C, H, K=K, current_model=0) for i in range(T)]
+    lib = nat.load()
+
+    def step(i):
+        sb.launch(pins[i % T], stream)
+
+    for i in range(args.warmup):
+        step(i)
+    if not args.no_timing:
+        nat.check(lib.llampc_bank_timing(sb.bank.handle, 1, args.steps + 8))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms = el / args.steps * 1e3
+
+    avg = (ctypes.c_double * 3)()
+    cnt = (ctypes.c_int64 * 3)()
+    if not args.no_timing:
+        nat.check(lib.llampc_bank_timing_read(sb.bank.handle, avg, cnt))
+        nat.check(lib.llampc_bank_timing(sb.bank.handle, 0, 1))
+    la_ms, lb_ms, sel_ms = avg[1], avg[0], avg[2]
+
+    merged = sb.fetch(stream)          # result of the last tick (all ranks identical)
+
+    extra = {}
+    if not args.no_extra and rank == 0:
+        extra = extras(args, sb, stream, world)
+
+    if rank == 0:
+        steps_per_tick = N_total * C * H + N_total
+        value = steps_per_tick / (ms / 1e3)
+        # algorithmic HBM bytes of one look-ahead launch (the dominant kernel): params 48 B
+        # + per-model result 12 B per model, candidates 16*C*H, xref 16*(H+1), x0/uprev 64
+        la_bytes = N_local * (48 + 12) + 16 * C * H + 16 * (H + 1) + 64
+        achieved = la_bytes / (la_ms * 1e-3) / 1e9 if la_ms > 0 else None
+        traffic = pmc_traffic(args)
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                "kernel": "lookahead_kernel<RK4>", "kernel_avg_us": la_ms * 1e3,
+                "bytes_per_launch": la_bytes,
+                "note": "binding resource is fp64 VALU/latency, not HBM (see valu)"}
+        valu_gf = N_local * C * H * FLOPS_PER_MODEL_STEP / (la_ms * 1e-3) / 1e9 if la_ms > 0 else None
+        line = {
+            "metric": "model-rollouts/sec (N_models x H steps) per control tick; wall-clock per plan() call",
+            "value": value, "unit": "model-rollout-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (RK6-plant states under gradual friction decay, recorded ETHZ controls, "
+                    "ConstantSpeed xref; seeded Pacejka bank)",
+            "config": {"workload": f"{args.track} LLA-MPC tick: look-back W={W} K={K} + look-ahead H={H} "
+                                   f"C={C}, gradual friction", "N_models_total": N_total,
+                       "N_models_per_gpu": N_local, "H": H, "C": C, "W": W, "K": K, "Ts": 0.02,
+                       "track": args.track, "parallelism": f"bank-shard x{world}" + (" + 1 RCCL all-gather/tick" if world > 1 else "")},
+            "roofline": roof,
+            "valu": {"bound": "fp64-valu", "achieved_gflops": valu_gf, "peak_tflops": FP64_VALU_PEAK_TFLOPS,
+                     "frac": valu_gf / (FP64_VALU_PEAK_TFLOPS * 1e3) if valu_gf else None,
+                     "flops_per_model_step": FLOPS_PER_MODEL_STEP,
+                     "note": "plain flops only; the 29 fp64 transcendentals per RK4 step are excluded"},
+            "kernel_us": {"lookback": lb_ms * 1e3, "lookahead": la_ms * 1e3, "select": sel_ms * 1e3,
+                          "events": list(cnt)},
+            "result_check": {"sel_model": merged.best_model, "window_full": merged.window_full,
+                             "sel_cand": merged.best_cand, "n_nonfinite": merged.n_nonfinite},
+            "cpu_baseline": None,
+        }
+        line.update(extra)
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    sb.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def extras(args, sb, stream, world):
+    """Rank-0 extras: C=64 throughput on the same bank, and synchronous per-tick latency
+    through the host-pointer API (PCIe-inclusive; never the headline value)."""
+    import torch
+    out = {}
+    H = args.H
+    a2 = argparse.Namespace(**vars(args))
+    a2.C = 64
+    t64 = make_ticks(a2, 8)
+    p64 = torch.from_numpy(t64).to(torch.device("cuda", sb.device))
+    pins = [sb.make_plan_in(p64[i], 64, H, K=args.K) for i in range(8)]
+    for i in range(5):
+        sb.launch(pins[i % 8], stream)
+    torch.cuda.synchronize()
+    n = 50
+    t0 = time.perf_counter()
+    for i in range(n):
+        sb.launch(pins[i % 8], stream)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / n * 1e3
+    Nt = args.n_per_gpu * world
+    out["C64"] = {"ms_per_step": ms, "value": (Nt * 64 * H + Nt) / (ms / 1e3)}
+    if world == 1:
+        pk = make_ticks(args, 1)[0]
+        C = args.C
+        xref = pk[16:16 + 2 * (H + 1)].reshape(2, H + 1)
+        U = pk[16 + 2 * (H + 1):].reshape(C, H, 2)
+        lat = []
+        for i in range(220):
+            t0 = time.perf_counter()
+            sb.bank.plan_raw(pk[0:6], pk[6:8], pk[8:14], U, xref, pk[14:16], K=args.K)
+            lat.append(time.perf_counter() - t0)
+        lat = np.array(lat[20:]) * 1e6
+        out["sync_plan_latency_us"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
+                                       "note": "host-pointer llampc_plan incl. H2D/D2H + stream sync"}
+    return out
+
+
+def pmc_traffic(args):
+    """HBM bytes per look-ahead launch from a committed rocprofv3 --pmc summary (None if
+    absent for this config): profiles/pmc_lookahead.json written by tools/pmc_summary.py."""
+    path = os.path.join(REPO, "profiles", "pmc_lookahead.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    key = f"{args.track}_N{args.n_per_gpu}_H{args.H}_C{args.C}"
+    v = d.get(key)
+    return None if v is None else v.get("hbm_bytes_per_launch")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,217 @@
+/*
+ * llampc.h — C ABI of the MI355X-native LLA-MPC model-bank engine (libllampc_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path (tianhao-stan-wu/LLA-MPC; all
+ * citations relative to the reference root).  Plain pointers and sizes only; every
+ * array is row-major fp64 unless stated.  All calls return 0 on success or a negative
+ * LLAMPC_E_* code; llampc_last_error() gives the thread's last message.
+ *
+ *  ABI entry point                 replaces (reference)
+ *  ------------------------------  -----------------------------------------------------
+ *  llampc_bank_create/destroy      the N-object MODEL_BANK + params_pass tuple
+ *                                  (llampc/mpc/run_nmpc_orca_llampc_rt.py:161-179) and the
+ *                                  error_windows ring (rt.py:83-84)
+ *  llampc_lookback                 evaluate_models_vectorized (llampc/mpc/evaluate_models_
+ *                                  vectorized.py:4-24) + the inline error / window / argmin
+ *                                  / argsort[:K] block (rt.py:347-366)
+ *  llampc_lookahead                H x Model._integrate_batch (llampc/models/model.py:32-40)
+ *                                  per (model, candidate) + the NLP objective
+ *                                  (llampc/mpc/nmpc.py:44-111) + argmin
+ *  llampc_plan / llampc_plan_device one LLA-MPC tick: rt.py:300-366 (look-back on the
+ *                                  newest transition, selection, look-ahead from x_t)
+ *  llampc_merge / _device          (new) cross-shard merge of per-GPU plan results
+ *  llampc_dynamics_batch           Dynamic.calc_forces_batch (llampc/models/dynamic.py:
+ *                                  117-154), Dynamic._diffequation_batch (:98-115)
+ *  llampc_integrate_batch          Model._integrate_batch (model.py:32-40, RK4),
+ *                                  Model._integrate/odeintRK6 (model.py:18-30,
+ *                                  llampc/utils/rk6.py:13-28) and the NLP Euler form
+ *                                  (nmpc.py:58-60 with Dynamic.casadi, dynamic.py:195-226)
+ */
+#ifndef LLAMPC_H_
+#define LLAMPC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LLAMPC_ABI_VERSION 1
+#define LLAMPC_KMAX 32          /* max top-K (rt.py:69 uses K=10) */
+#define LLAMPC_WMAX 128         /* max look-back window (rt.py:67 uses W=10) */
+
+enum llampc_status {
+  LLAMPC_OK = 0,
+  LLAMPC_E_ARG = -1,        /* bad argument / shape                       */
+  LLAMPC_E_HIP = -2,        /* HIP runtime error                          */
+  LLAMPC_E_NODEV = -3,      /* no HIP device                              */
+  LLAMPC_E_STATE = -4,      /* call not valid in the handle's state       */
+  LLAMPC_E_OOM = -5         /* device allocation failed                   */
+};
+
+/* Integrators.  RK4 = odeintRK4_batch (rk6.py:50-68) on the |vx| dynamics
+ * (dynamic.py:98-154); EULER_NLP = the NLP transcription x+Ts*f (nmpc.py:58-60) on
+ * Dynamic.casadi (vmin clamp, atan2(.,vx); dynamic.py:195-226); RK6 = odeintRK6
+ * (rk6.py:13-28), the plant integrator (dynamic.py:59-74). */
+enum llampc_integrator { LLAMPC_RK4 = 0, LLAMPC_EULER_NLP = 1, LLAMPC_RK6 = 2 };
+
+/* argmin NaN policy for the look-back selection: NAN_FIRST reproduces np.argmin
+ * (first NaN wins, rt.py:359); NAN_IGNORE treats NaN as +inf.  top-K always orders
+ * NaN last (np.argsort, rt.py:360).  The look-ahead argmin always treats NaN as +inf. */
+enum llampc_nan_policy { LLAMPC_NAN_FIRST = 0, LLAMPC_NAN_IGNORE = 1 };
+
+/* llampc_dynamics_batch ops */
+enum llampc_dyn_op { LLAMPC_OP_FORCES = 0, LLAMPC_OP_DERIV = 1 };
+
+/* Shared (per-bank) vehicle constants (llampc/params/orca.py:13-27). */
+typedef struct llampc_vehicle {
+  double lf, lr, mass, Iz;
+  double Cm1, Cm2, Cr0, Cr2;
+  int32_t input_acc;   /* 1: Frx = mass*u0 (dynamic.py:139-142)                    */
+  int32_t approx;      /* 1: linear tires Ffy=2*Cf*af (dynamic.py:126-136); params */
+                       /*    rows Cf/Cr are then cornering stiffnesses             */
+} llampc_vehicle;
+
+/* Look-ahead objective (nmpc.py:44-111) and candidate feasibility (nmpc.py:102-105). */
+typedef struct llampc_cost {
+  double Q[4];         /* 2x2 row-major tracking weight   (rt.py:60 diag(1,1))      */
+  double R[4];         /* 2x2 row-major input-rate weight (rt.py:62 diag(5e-3,1))   */
+  double P[4];         /* 2x2 row-major terminal weight   (rt.py:61 diag(0,0))      */
+  double umin[2], umax[2];   /* input bounds (orca.py:31-35)                        */
+  double rate_max[2];  /* |u_k - u_{k-1}| <= rate_max*Ts; <0 disables (orca.py:35)  */
+  int32_t enforce_bounds;    /* 1: infeasible candidates cost +inf                  */
+  int32_t reserved;
+} llampc_cost;
+
+/* One tick's inputs.  Pointers are HOST pointers for llampc_plan and DEVICE pointers
+ * for llampc_plan_device. */
+typedef struct llampc_plan_in {
+  const double* x_prev;   /* [6]  x_{t-1}                                          */
+  const double* u_prev;   /* [2]  u_{t-1}                                          */
+  const double* x_now;    /* [6]  x_t (look-back target, look-ahead start)          */
+  const double* U;        /* [C][H][2] candidate control sequences                 */
+  const double* xref;     /* [2][H+1] reference (planner.py:12-67 output)          */
+  const double* uprev;    /* [2]  last applied input for du_0 (nmpc.py:65-66)      */
+  int32_t C, H;
+  int32_t K;              /* top-K size, <= LLAMPC_KMAX                            */
+  int32_t integrator;     /* look-ahead integrator                                 */
+  int32_t do_lookback;    /* 0: skip the look-back (first tick, rt.py:347)         */
+  int32_t do_lookahead;   /* 0: skip the look-ahead                                */
+  int32_t nan_policy;
+  int32_t reserved;
+  int64_t current_model;  /* global index used while the window fills (rt.py:264)  */
+  double Ts;
+  llampc_cost cost;
+} llampc_plan_in;
+
+/* One tick's result (fixed size: also the cross-GPU payload, see llampc_merge). */
+typedef struct llampc_plan_out {
+  int32_t window_count;   /* transitions in the window, <= W (rt.py:354)           */
+  int32_t window_full;    /* window_count >= W: selection valid (rt.py:357)        */
+  int32_t K;
+  int32_t sel_owned;      /* this shard owns sel_model                             */
+  int64_t lb_best;        /* argmin of the window mean (rt.py:359), -1 if not full */
+  double  lb_best_val;
+  int64_t sel_model;      /* full ? lb_best : current_model                        */
+  int32_t sel_cand;       /* argmin_c cost[sel_model, c]  ("chosen control")       */
+  int32_t n_nonfinite;    /* look-ahead rollouts whose cost is not finite          */
+  double  sel_cost;
+  int64_t la_best_model;  /* argmin over all (model, candidate) costs              */
+  int32_t la_best_cand;
+  int32_t reserved;
+  double  la_best_cost;
+  int64_t topk[LLAMPC_KMAX];      /* argsort(window mean)[:K] (rt.py:360), -1 pad  */
+  double  topk_val[LLAMPC_KMAX];
+  double  topk_Df[LLAMPC_KMAX];   /* bank Df/Dr of the top-K (rt.py:336-338)      */
+  double  topk_Dr[LLAMPC_KMAX];
+  int32_t topk_cand[LLAMPC_KMAX]; /* look-ahead best candidate of each top-K model */
+  double  topk_cost[LLAMPC_KMAX];
+} llampc_plan_out;
+
+typedef struct llampc_bank llampc_bank;
+
+/* ---- library ---------------------------------------------------------------- */
+int32_t     llampc_abi_version(void);
+const char* llampc_last_error(void);
+int         llampc_device_count(int32_t* count);
+
+/* ---- bank handle -------------------------------------------------------------- */
+/* params: [6][n] rows (Bf, Cf, Df, Br, Cr, Dr) = rt.py:179 params_pass order.
+ * global_offset: global index of this shard's first model (multi-GPU).  W: window. */
+int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
+                       const llampc_vehicle* veh, int32_t W, int32_t device,
+                       llampc_bank** out);
+int llampc_bank_destroy(llampc_bank* bank);
+int llampc_bank_info(const llampc_bank* bank, int64_t* n, int64_t* global_offset,
+                     int32_t* W, int32_t* window_count, int32_t* device);
+int llampc_bank_reset(llampc_bank* bank);                 /* empty the window       */
+/* ring: [n][W] oldest -> newest (the rt.py error_windows layout, zeros if unfilled) */
+int llampc_bank_window(llampc_bank* bank, double* ring, int32_t* window_count);
+/* stream the bank launches on (hipStream_t as void*); NULL = its own stream */
+int llampc_bank_set_stream(llampc_bank* bank, void* stream);
+
+/* Per-kernel HIP-event timing of the bank's launches, on the stream they run on (for the
+ * benchmark's roofline).  enable=1 arms `max_launches` event pairs per kernel; each
+ * launch of {look-back, look-ahead, select} is bracketed by hipEventRecord. */
+int llampc_bank_timing(llampc_bank* bank, int32_t enable, int32_t max_launches);
+/* Synchronises, returns avg_ms[3] and count[3] for {look-back, look-ahead, select} since
+ * the last read, and re-arms the counters. */
+int llampc_bank_timing_read(llampc_bank* bank, double* avg_ms, int64_t* count);
+
+/* ---- look-back (host pointers) -------------------------------------------------- */
+/* err_out [n] (rt.py:349 errors), wmean_out [n] (rt.py:358 avg_errors, valid when the
+ * window is full), topk/topk_val [K] may each be NULL. */
+int llampc_lookback(llampc_bank* bank, const double* x_prev, const double* u_prev,
+                    const double* x_now, double Ts, int32_t K, int32_t nan_policy,
+                    double* err_out, double* wmean_out, int64_t* best, int64_t* topk,
+                    double* topk_val, int32_t* window_count);
+
+/* ---- look-ahead (host pointers) ------------------------------------------------- */
+/* cost_out [n][C] and best_cand_out [n] may be NULL. */
+int llampc_lookahead(llampc_bank* bank, const double* x0, const double* U, int32_t C,
+                     int32_t H, const double* xref, const double* uprev,
+                     const llampc_cost* cost, double Ts, int32_t integrator,
+                     double* cost_out, int32_t* best_cand_out, int64_t* best_model,
+                     int32_t* best_cand, double* best_cost);
+
+/* ---- fused tick ------------------------------------------------------------------ */
+/* Host pointers; blocking.  err_out [n], wmean_out [n], cost_out [n][C] may be NULL. */
+int llampc_plan(llampc_bank* bank, const llampc_plan_in* in, llampc_plan_out* out,
+                double* err_out, double* wmean_out, double* cost_out);
+/* Device pointers in `in`; d_out is a device llampc_plan_out; asynchronous on
+ * `stream` (hipStream_t, NULL = the bank's stream).  d_err/d_wmean/d_cost: device
+ * arrays or NULL. */
+int llampc_plan_device(llampc_bank* bank, const llampc_plan_in* in, void* d_out,
+                       double* d_err, double* d_wmean, double* d_cost, void* stream);
+
+/* ---- multi-GPU merge ----------------------------------------------------------- */
+/* Merge G shard results (shards ordered by global_offset) into one, deterministic:
+ * lowest value, ties -> lowest global index, NaN first for lb_best under NAN_FIRST.
+ * Host version runs the same merge code as the device version. */
+int llampc_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_policy,
+                 llampc_plan_out* merged);
+int llampc_merge_device(const void* d_parts, int32_t G, int32_t nan_policy, void* d_merged,
+                        int32_t device, void* stream);
+
+/* ---- raw batched dynamics (Dynamic API parity) ---------------------------------- */
+/* x [n][6], u [n][2]; params [6][P] with P == 1 (one model broadcast) or P == n.
+ * OP_FORCES -> out [5][n] = (Ffy, Frx, Fry, alphaf, alphar)   (dynamic.py:117-154)
+ * OP_DERIV  -> out [n][6]                                      (dynamic.py:98-115)
+ * device_ptrs: 0 = host arrays (blocking), 1 = device arrays (async on stream). */
+int llampc_dynamics_batch(int32_t op, const double* x, const double* u,
+                          const double* params, int64_t P, const llampc_vehicle* veh,
+                          int64_t n, double* out, int32_t device, int32_t device_ptrs,
+                          void* stream);
+/* S successive integration steps per lane: x0 [n][6]; u [n][S][2] (u_stride_lane =
+ * S*2) or [S][2] broadcast (u_stride_lane = 0); h [S] step sizes; traj_out
+ * [S+1][n][6] (full trajectory) or [n][6] (final state only, when final_only=1). */
+int llampc_integrate_batch(const double* x0, const double* u, int64_t u_stride_lane,
+                           const double* h, int32_t S, const double* params, int64_t P,
+                           const llampc_vehicle* veh, int64_t n, int32_t integrator,
+                           double* traj_out, int32_t final_only, int32_t device,
+                           int32_t device_ptrs, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LLAMPC_H_ */

@@ -1,0 +1,757 @@
+// capi.hip — extern "C" boundary (include/llampc.h): the device-resident model-bank
+// handle, host<->device staging and the per-tick launch sequence.
+//
+// A bank owns, on its device: params SoA [6][n] (48 B/model, read coalesced by lane),
+// the look-back ring [W][n] (slot-major, so each tick writes one contiguous row — the
+// reference's np.roll copy of N*W doubles per tick, rt.py:352, is gone), per-block
+// reduction partials, the per-model look-ahead result, and pinned host staging so one
+// tick = 1 H2D copy + 3 kernels + 1 D2H copy on one stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "merge.hpp"
+
+using namespace llampc;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(LLAMPC_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),    \
+                  __FILE__, __LINE__);                                                    \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+VehK make_veh(const llampc_vehicle& v) {
+  VehK k;
+  k.lf = v.lf;
+  k.lr = v.lr;
+  k.mass = v.mass;
+  k.inv_mass = 1 / v.mass;  // the reference's `1/self.mass` scalar (dynamic.py:111-112)
+  k.inv_Iz = 1 / v.Iz;      // `1/self.Iz` (dynamic.py:113)
+  k.Cm1 = v.Cm1;
+  k.Cm2 = v.Cm2;
+  k.Cr0 = v.Cr0;
+  k.Cr2 = v.Cr2;
+  k.input_acc = v.input_acc;
+  k.approx = v.approx;
+  return k;
+}
+
+CostK make_cost(const llampc_cost& c, double Ts) {
+  CostK k;
+  for (int i = 0; i < 4; ++i) {
+    k.Q[i] = c.Q[i];
+    k.R[i] = c.R[i];
+    k.P[i] = c.P[i];
+  }
+  for (int i = 0; i < 2; ++i) {
+    k.umin[i] = c.umin[i];
+    k.umax[i] = c.umax[i];
+    k.dmax[i] = c.rate_max[i] < 0 ? -1.0 : c.rate_max[i] * Ts;   // nmpc.py:104-105
+  }
+  k.enforce = c.enforce_bounds;
+  k.pad = 0;
+  return k;
+}
+
+template <class T>
+int dev_alloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+  if (e != hipSuccess)
+    return fail(LLAMPC_E_OOM, "hipMalloc(%zu B) failed: %s", count * sizeof(T), hipGetErrorString(e));
+  return LLAMPC_OK;
+}
+
+}  // namespace
+
+struct llampc_bank {
+  int device = 0;
+  int64_t n = 0, goff = 0;
+  int32_t W = 0, count = 0, slot = 0;
+  VehK veh{};
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  double* d_params = nullptr;
+  double* d_ring = nullptr;
+  double* d_am_val = nullptr;
+  int64_t* d_am_idx = nullptr;
+  double* d_tk_val = nullptr;
+  int64_t* d_tk_idx = nullptr;
+  double* d_pv = nullptr;
+  int64_t* d_pidx = nullptr;
+  int32_t* d_pnf = nullptr;
+  int32_t* d_best_cand = nullptr;
+  double* d_best_cost = nullptr;
+  double* h_in = nullptr;          // pinned input pack
+  double* d_in = nullptr;
+  size_t in_cap = 0;               // doubles
+  llampc_plan_out* h_out = nullptr;
+  llampc_plan_out* d_out = nullptr;
+  double* d_err = nullptr;         // [n]
+  double* d_wmean = nullptr;       // [n]
+  double* d_cost = nullptr;        // [n*C]
+  size_t cost_cap = 0;
+  std::mutex mu;
+  // optional per-kernel event timing: [kernel][2*i] start, [kernel][2*i+1] stop
+  std::vector<hipEvent_t> ev[3];
+  size_t ev_used[3] = {0, 0, 0};
+  bool timing = false;
+};
+
+namespace {
+
+int ensure_in(llampc_bank* b, size_t doubles) {
+  if (doubles <= b->in_cap) return LLAMPC_OK;
+  if (b->h_in) (void)hipHostFree(b->h_in);
+  if (b->d_in) (void)hipFree(b->d_in);
+  b->h_in = nullptr;
+  b->d_in = nullptr;
+  b->in_cap = 0;
+  size_t cap = std::max<size_t>(doubles, 1024);
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&b->h_in), cap * sizeof(double), hipHostMallocDefault));
+  int rc = dev_alloc(&b->d_in, cap);
+  if (rc) return rc;
+  b->in_cap = cap;
+  return LLAMPC_OK;
+}
+
+int ensure_cost(llampc_bank* b, size_t count) {
+  if (count <= b->cost_cap) return LLAMPC_OK;
+  if (b->d_cost) (void)hipFree(b->d_cost);
+  b->d_cost = nullptr;
+  b->cost_cap = 0;
+  int rc = dev_alloc(&b->d_cost, count);
+  if (rc) return rc;
+  b->cost_cap = count;
+  return LLAMPC_OK;
+}
+
+int check_plan_in(const llampc_bank* b, const llampc_plan_in* in) {
+  if (!in) return fail(LLAMPC_E_ARG, "plan input is NULL");
+  if (in->do_lookback && (in->K < 1 || in->K > LLAMPC_KMAX))
+    return fail(LLAMPC_E_ARG, "K=%d outside [1, %d]", in->K, LLAMPC_KMAX);
+  if (in->do_lookback && (!in->x_prev || !in->u_prev || !in->x_now))
+    return fail(LLAMPC_E_ARG, "look-back needs x_prev, u_prev and x_now");
+  if (in->do_lookahead) {
+    if (in->C < 1 || in->H < 1) return fail(LLAMPC_E_ARG, "C=%d H=%d must be >= 1", in->C, in->H);
+    if ((int64_t)in->C * in->H > (1 << 26)) return fail(LLAMPC_E_ARG, "C*H too large");
+    if (!in->x_now || !in->U || !in->xref || !in->uprev)
+      return fail(LLAMPC_E_ARG, "look-ahead needs x_now, U, xref and uprev");
+    if (in->integrator < LLAMPC_RK4 || in->integrator > LLAMPC_RK6)
+      return fail(LLAMPC_E_ARG, "unknown integrator %d", in->integrator);
+    if ((b->n + 1) * (int64_t)in->C <= 0 || b->n > INT64_MAX / std::max(1, in->C) - 1)
+      return fail(LLAMPC_E_ARG, "n*C overflows");
+  }
+  if (!(in->Ts > 0) || !std::isfinite(in->Ts)) return fail(LLAMPC_E_ARG, "Ts must be finite > 0");
+  return LLAMPC_OK;
+}
+
+// Event bracket around one launch of kernel `k` (0 look-back, 1 look-ahead, 2 select).
+struct TimedLaunch {
+  llampc_bank* b;
+  int k;
+  hipStream_t s;
+  hipEvent_t stop = nullptr;
+  TimedLaunch(llampc_bank* b_, int k_, hipStream_t s_) : b(b_), k(k_), s(s_) {
+    if (!b->timing || 2 * (b->ev_used[k] + 1) > b->ev[k].size()) return;
+    const size_t i = b->ev_used[k]++;
+    (void)hipEventRecord(b->ev[k][2 * i], s);
+    stop = b->ev[k][2 * i + 1];
+  }
+  ~TimedLaunch() {
+    if (stop) (void)hipEventRecord(stop, s);
+  }
+};
+
+void timing_free(llampc_bank* b) {
+  for (auto& v : b->ev) {
+    for (hipEvent_t e : v) (void)hipEventDestroy(e);
+    v.clear();
+  }
+  for (size_t& u : b->ev_used) u = 0;
+  b->timing = false;
+}
+
+// The tick on device pointers.  Advances the window bookkeeping when a look-back runs.
+int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out, double* d_err,
+                double* d_wmean, double* d_cost, hipStream_t s) {
+  const bool lb = in.do_lookback != 0;
+  const bool la = in.do_lookahead != 0;
+  int32_t count = b->count;
+  int32_t full = count >= b->W;
+  if (lb) {
+    const int32_t slot = b->slot;
+    count = std::min(count + 1, b->W);             // rt.py:354
+    full = count >= b->W;                          // rt.py:357
+    LookbackLaunch a{};
+    a.params = b->d_params;
+    a.n = b->n;
+    a.goff = b->goff;
+    a.veh = b->veh;
+    a.x_prev = in.x_prev;
+    a.u_prev = in.u_prev;
+    a.x_now = in.x_now;
+    a.Ts = in.Ts;
+    a.ring = b->d_ring;
+    a.W = b->W;
+    a.slot = slot;
+    a.full = full;
+    a.K = in.K;
+    a.nan_first = in.nan_policy == LLAMPC_NAN_FIRST;
+    a.err_out = d_err;
+    a.wmean_out = d_wmean;
+    a.am_val = b->d_am_val;
+    a.am_idx = b->d_am_idx;
+    a.tk_val = b->d_tk_val;
+    a.tk_idx = b->d_tk_idx;
+    {
+      TimedLaunch tl(b, 0, s);
+      HIP_TRY(launch_lookback(a, s));
+    }
+    b->slot = (slot + 1) % b->W;
+    b->count = count;
+  }
+  if (la) {
+    LookaheadLaunch a{};
+    a.params = b->d_params;
+    a.n = b->n;
+    a.goff = b->goff;
+    a.veh = b->veh;
+    a.x0 = in.x_now;
+    a.U = in.U;
+    a.xref = in.xref;
+    a.uprev = in.uprev;
+    a.C = in.C;
+    a.H = in.H;
+    a.integrator = in.integrator;
+    a.Ts = in.Ts;
+    a.cost = make_cost(in.cost, in.Ts);
+    a.cost_out = d_cost;
+    a.best_cand = b->d_best_cand;
+    a.best_cost = b->d_best_cost;
+    a.pv = b->d_pv;
+    a.pidx = b->d_pidx;
+    a.pnf = b->d_pnf;
+    TimedLaunch tl(b, 1, s);
+    HIP_TRY(launch_lookahead(a, s));
+  }
+  SelectLaunch sl{};
+  sl.do_lb = lb;
+  sl.full = full;
+  sl.window_count = count;
+  sl.K = lb ? in.K : 0;
+  sl.nan_first = in.nan_policy == LLAMPC_NAN_FIRST;
+  sl.lb_blocks = lookback_blocks(b->n);
+  sl.am_val = b->d_am_val;
+  sl.am_idx = b->d_am_idx;
+  sl.tk_val = b->d_tk_val;
+  sl.tk_idx = b->d_tk_idx;
+  sl.do_la = la;
+  sl.la_blocks = la ? lookahead_blocks(b->n, in.C) : 0;
+  sl.C = la ? in.C : 1;
+  sl.pv = b->d_pv;
+  sl.pidx = b->d_pidx;
+  sl.pnf = b->d_pnf;
+  sl.params = b->d_params;
+  sl.n = b->n;
+  sl.goff = b->goff;
+  sl.best_cand = b->d_best_cand;
+  sl.best_cost = b->d_best_cost;
+  sl.current_model = in.current_model;
+  sl.out = d_out;
+  TimedLaunch tl(b, 2, s);
+  HIP_TRY(launch_select(sl, s));
+  return LLAMPC_OK;
+}
+
+// Pack a host plan input into the pinned buffer; return a device-pointer copy of `in`.
+int stage_inputs(llampc_bank* b, const llampc_plan_in* in, llampc_plan_in* dev_in, hipStream_t s) {
+  const int64_t H = in->do_lookahead ? in->H : 0, C = in->do_lookahead ? in->C : 0;
+  const size_t total = 16 + 2 * (H + 1) + 2 * C * H;
+  int rc = ensure_in(b, total);
+  if (rc) return rc;
+  double* h = b->h_in;
+  std::memset(h, 0, 16 * sizeof(double));
+  if (in->x_prev) std::memcpy(h + 0, in->x_prev, 6 * sizeof(double));
+  if (in->u_prev) std::memcpy(h + 6, in->u_prev, 2 * sizeof(double));
+  if (in->x_now) std::memcpy(h + 8, in->x_now, 6 * sizeof(double));
+  if (in->uprev) std::memcpy(h + 14, in->uprev, 2 * sizeof(double));
+  if (in->do_lookahead) {
+    std::memcpy(h + 16, in->xref, 2 * (H + 1) * sizeof(double));
+    std::memcpy(h + 16 + 2 * (H + 1), in->U, 2 * C * H * sizeof(double));
+  }
+  HIP_TRY(hipMemcpyAsync(b->d_in, h, total * sizeof(double), hipMemcpyHostToDevice, s));
+  *dev_in = *in;
+  double* d = b->d_in;
+  dev_in->x_prev = d;
+  dev_in->u_prev = d + 6;
+  dev_in->x_now = d + 8;
+  dev_in->uprev = d + 14;
+  dev_in->xref = d + 16;
+  dev_in->U = d + 16 + 2 * (H + 1);
+  return LLAMPC_OK;
+}
+
+hipStream_t pick_stream(llampc_bank* b, void* s) { return s ? (hipStream_t)s : b->stream; }
+
+
+
+}  // namespace
+
+extern "C" {
+
+int32_t llampc_abi_version(void) { return LLAMPC_ABI_VERSION; }
+
+const char* llampc_last_error(void) { return g_err.c_str(); }
+
+int llampc_device_count(int32_t* count) {
+  if (!count) return fail(LLAMPC_E_ARG, "count is NULL");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(LLAMPC_E_NODEV, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *count = c;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
+                       const llampc_vehicle* veh, int32_t W, int32_t device, llampc_bank** out) {
+  if (!out) return fail(LLAMPC_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (!params || !veh) return fail(LLAMPC_E_ARG, "params/veh is NULL");
+  if (n < 1) return fail(LLAMPC_E_ARG, "n=%lld must be >= 1", (long long)n);
+  if (W < 1 || W > LLAMPC_WMAX) return fail(LLAMPC_E_ARG, "W=%d outside [1, %d]", W, LLAMPC_WMAX);
+  if (global_offset < 0) return fail(LLAMPC_E_ARG, "global_offset < 0");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+    return fail(LLAMPC_E_NODEV, "no HIP device visible (the HIP path has no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(LLAMPC_E_ARG, "device %d of %d", device, ndev);
+  DeviceGuard g(device);
+  if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", device);
+
+  auto* b = new llampc_bank();
+  b->device = device;
+  b->n = n;
+  b->goff = global_offset;
+  b->W = W;
+  b->veh = make_veh(*veh);
+  int rc = LLAMPC_OK;
+  auto cleanup = [&](int code) {
+    llampc_bank_destroy(b);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
+  b->own_stream = true;
+  const int lbb = lookback_blocks(n);
+  const int lab = lookahead_blocks(n, 64);   // worst case: one model per wave
+  if ((rc = dev_alloc(&b->d_params, 6 * (size_t)n)) || (rc = dev_alloc(&b->d_ring, (size_t)W * n)) ||
+      (rc = dev_alloc(&b->d_am_val, lbb)) || (rc = dev_alloc(&b->d_am_idx, lbb)) ||
+      (rc = dev_alloc(&b->d_tk_val, (size_t)lbb * LLAMPC_KMAX)) ||
+      (rc = dev_alloc(&b->d_tk_idx, (size_t)lbb * LLAMPC_KMAX)) || (rc = dev_alloc(&b->d_pv, lab)) ||
+      (rc = dev_alloc(&b->d_pidx, lab)) || (rc = dev_alloc(&b->d_pnf, lab)) ||
+      (rc = dev_alloc(&b->d_best_cand, n)) || (rc = dev_alloc(&b->d_best_cost, n)) ||
+      (rc = dev_alloc(&b->d_err, n)) || (rc = dev_alloc(&b->d_wmean, n)) ||
+      (rc = dev_alloc(&b->d_out, 1)))
+    return cleanup(rc);
+  if (hipHostMalloc(reinterpret_cast<void**>(&b->h_out), sizeof(llampc_plan_out), hipHostMallocDefault) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(out) failed"));
+  if (hipMemcpy(b->d_params, params, 6 * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(b->d_ring, 0, (size_t)W * n * sizeof(double)) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess)
+    return cleanup(fail(LLAMPC_E_HIP, "bank upload failed"));
+  *out = b;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_destroy(llampc_bank* b) {
+  if (!b) return LLAMPC_OK;
+  {
+    DeviceGuard g(b->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    void* dptrs[] = {b->d_params, b->d_ring, b->d_am_val, b->d_am_idx, b->d_tk_val, b->d_tk_idx,
+                     b->d_pv, b->d_pidx, b->d_pnf, b->d_best_cand, b->d_best_cost, b->d_in,
+                     b->d_out, b->d_err, b->d_wmean, b->d_cost};
+    for (void* p : dptrs)
+      if (p) (void)hipFree(p);
+    if (b->h_in) (void)hipHostFree(b->h_in);
+    if (b->h_out) (void)hipHostFree(b->h_out);
+    timing_free(b);
+    if (b->own_stream && b->stream) (void)hipStreamDestroy(b->stream);
+  }
+  delete b;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_info(const llampc_bank* b, int64_t* n, int64_t* goff, int32_t* W,
+                     int32_t* window_count, int32_t* device) {
+  if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
+  if (n) *n = b->n;
+  if (goff) *goff = b->goff;
+  if (W) *W = b->W;
+  if (window_count) *window_count = b->count;
+  if (device) *device = b->device;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_reset(llampc_bank* b) {
+  if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  HIP_TRY(hipMemsetAsync(b->d_ring, 0, (size_t)b->W * b->n * sizeof(double), b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  b->count = 0;
+  b->slot = 0;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_window(llampc_bank* b, double* ring, int32_t* window_count) {
+  if (!b || !ring) return fail(LLAMPC_E_ARG, "bank/ring is NULL");
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  std::vector<double> raw((size_t)b->W * b->n);
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  HIP_TRY(hipMemcpy(raw.data(), b->d_ring, raw.size() * sizeof(double), hipMemcpyDeviceToHost));
+  // rt.py layout [n][W]: newest in column W-1, unfilled (oldest) columns zero.
+  const int W = b->W, cnt = b->count;
+  for (int64_t i = 0; i < b->n; ++i) {
+    for (int c = 0; c < W; ++c) {
+      const int age = W - 1 - c;                   // 0 = newest
+      double v = 0.0;
+      if (age < cnt) {
+        const int s = ((b->slot - 1 - age) % W + W) % W;
+        v = raw[(size_t)s * b->n + i];
+      }
+      ring[(size_t)i * W + c] = v;
+    }
+  }
+  if (window_count) *window_count = cnt;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_set_stream(llampc_bank* b, void* stream) {
+  if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  if (b->own_stream) (void)hipStreamDestroy(b->stream);
+  if (stream) {
+    b->stream = (hipStream_t)stream;
+    b->own_stream = false;
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    b->own_stream = true;
+  }
+  return LLAMPC_OK;
+}
+
+int llampc_bank_timing(llampc_bank* b, int32_t enable, int32_t max_launches) {
+  if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  timing_free(b);
+  if (!enable) return LLAMPC_OK;
+  if (max_launches < 1) return fail(LLAMPC_E_ARG, "max_launches must be >= 1");
+  for (auto& v : b->ev) {
+    v.resize(2 * (size_t)max_launches, nullptr);
+    for (hipEvent_t& e : v) HIP_TRY(hipEventCreate(&e));
+  }
+  b->timing = true;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_timing_read(llampc_bank* b, double* avg_ms, int64_t* count) {
+  if (!b || !avg_ms || !count) return fail(LLAMPC_E_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  for (int k = 0; k < 3; ++k) {
+    double tot = 0.0;
+    for (size_t i = 0; i < b->ev_used[k]; ++i) {
+      HIP_TRY(hipEventSynchronize(b->ev[k][2 * i + 1]));
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, b->ev[k][2 * i], b->ev[k][2 * i + 1]));
+      tot += ms;
+    }
+    count[k] = (int64_t)b->ev_used[k];
+    avg_ms[k] = b->ev_used[k] ? tot / b->ev_used[k] : 0.0;
+    b->ev_used[k] = 0;
+  }
+  return LLAMPC_OK;
+}
+
+int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, double* err_out,
+                double* wmean_out, double* cost_out) {
+  if (!b || !out) return fail(LLAMPC_E_ARG, "bank/out is NULL");
+  int rc = check_plan_in(b, in);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  hipStream_t s = b->stream;
+  if (cost_out && in->do_lookahead && (rc = ensure_cost(b, (size_t)b->n * in->C))) return rc;
+  llampc_plan_in din;
+  if ((rc = stage_inputs(b, in, &din, s))) return rc;
+  double* d_cost = (cost_out && in->do_lookahead) ? b->d_cost : nullptr;
+  if ((rc = plan_launch(b, din, b->d_out, err_out ? b->d_err : nullptr,
+                        wmean_out ? b->d_wmean : nullptr, d_cost, s)))
+    return rc;
+  HIP_TRY(hipMemcpyAsync(b->h_out, b->d_out, sizeof(llampc_plan_out), hipMemcpyDeviceToHost, s));
+  if (err_out && in->do_lookback)
+    HIP_TRY(hipMemcpyAsync(err_out, b->d_err, b->n * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (wmean_out && in->do_lookback && b->count >= b->W)
+    HIP_TRY(hipMemcpyAsync(wmean_out, b->d_wmean, b->n * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (d_cost)
+    HIP_TRY(hipMemcpyAsync(cost_out, d_cost, (size_t)b->n * in->C * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *out = *b->h_out;
+  return LLAMPC_OK;
+}
+
+int llampc_plan_device(llampc_bank* b, const llampc_plan_in* in, void* d_out, double* d_err,
+                       double* d_wmean, double* d_cost, void* stream) {
+  if (!b || !d_out) return fail(LLAMPC_E_ARG, "bank/d_out is NULL");
+  int rc = check_plan_in(b, in);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  return plan_launch(b, *in, (llampc_plan_out*)d_out, d_err, d_wmean, d_cost, pick_stream(b, stream));
+}
+
+int llampc_lookback(llampc_bank* b, const double* x_prev, const double* u_prev, const double* x_now,
+                    double Ts, int32_t K, int32_t nan_policy, double* err_out, double* wmean_out,
+                    int64_t* best, int64_t* topk, double* topk_val, int32_t* window_count) {
+  llampc_plan_in in{};
+  in.x_prev = x_prev;
+  in.u_prev = u_prev;
+  in.x_now = x_now;
+  in.K = K;
+  in.do_lookback = 1;
+  in.do_lookahead = 0;
+  in.nan_policy = nan_policy;
+  in.current_model = -1;
+  in.Ts = Ts;
+  llampc_plan_out o;
+  int rc = llampc_plan(b, &in, &o, err_out, wmean_out, nullptr);
+  if (rc) return rc;
+  if (best) *best = o.window_full ? o.lb_best : -1;
+  for (int k = 0; k < K; ++k) {
+    if (topk) topk[k] = o.topk[k];
+    if (topk_val) topk_val[k] = o.topk_val[k];
+  }
+  if (window_count) *window_count = o.window_count;
+  return LLAMPC_OK;
+}
+
+int llampc_lookahead(llampc_bank* b, const double* x0, const double* U, int32_t C, int32_t H,
+                     const double* xref, const double* uprev, const llampc_cost* cost, double Ts,
+                     int32_t integrator, double* cost_out, int32_t* best_cand_out,
+                     int64_t* best_model, int32_t* best_cand, double* best_cost) {
+  if (!cost) return fail(LLAMPC_E_ARG, "cost is NULL");
+  llampc_plan_in in{};
+  in.x_now = x0;
+  in.U = U;
+  in.C = C;
+  in.H = H;
+  in.xref = xref;
+  in.uprev = uprev;
+  in.K = 1;
+  in.integrator = integrator;
+  in.do_lookback = 0;
+  in.do_lookahead = 1;
+  in.current_model = -1;
+  in.Ts = Ts;
+  in.cost = *cost;
+  llampc_plan_out o;
+  int rc = llampc_plan(b, &in, &o, nullptr, nullptr, cost_out);
+  if (rc) return rc;
+  if (best_cand_out) {
+    DeviceGuard g(b->device);
+    HIP_TRY(hipMemcpy(best_cand_out, b->d_best_cand, b->n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  }
+  if (best_model) *best_model = o.la_best_model;
+  if (best_cand) *best_cand = o.la_best_cand;
+  if (best_cost) *best_cost = o.la_best_cost;
+  return LLAMPC_OK;
+}
+
+int llampc_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_policy, llampc_plan_out* merged) {
+  if (!parts || !merged || G < 1) return fail(LLAMPC_E_ARG, "bad merge arguments");
+  for (int g = 1; g < G; ++g)
+    if (parts[g].K != parts[0].K || parts[g].window_count != parts[0].window_count)
+      return fail(LLAMPC_E_STATE, "shard %d disagrees on K/window (K %d vs %d, count %d vs %d)", g,
+                  parts[g].K, parts[0].K, parts[g].window_count, parts[0].window_count);
+  merge_plan_parts(parts, G, nan_policy == LLAMPC_NAN_FIRST, merged);
+  return LLAMPC_OK;
+}
+
+int llampc_merge_device(const void* d_parts, int32_t G, int32_t nan_policy, void* d_merged,
+                        int32_t device, void* stream) {
+  if (!d_parts || !d_merged || G < 1) return fail(LLAMPC_E_ARG, "bad merge arguments");
+  DeviceGuard g(device);
+  if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", device);
+  HIP_TRY(launch_merge((const llampc_plan_out*)d_parts, G, nan_policy == LLAMPC_NAN_FIRST,
+                       (llampc_plan_out*)d_merged, (hipStream_t)stream));
+  return LLAMPC_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------
+// Raw batched dynamics: per-device cached workspace + stream
+// ------------------------------------------------------------------------------------
+namespace {
+
+struct Workspace {
+  std::mutex mu;
+  void* d = nullptr;
+  size_t cap = 0;
+  hipStream_t stream = nullptr;
+};
+Workspace g_ws[64];
+
+int ws_get(int device, size_t bytes, Workspace** out) {
+  if (device < 0 || device >= 64) return fail(LLAMPC_E_ARG, "device %d", device);
+  Workspace& w = g_ws[device];
+  if (!w.stream) HIP_TRY(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+  if (bytes > w.cap) {
+    if (w.d) (void)hipFree(w.d);
+    w.d = nullptr;
+    w.cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 1 << 20);
+    hipError_t e = hipMalloc(&w.d, cap);
+    if (e != hipSuccess) return fail(LLAMPC_E_OOM, "workspace hipMalloc(%zu): %s", cap, hipGetErrorString(e));
+    w.cap = cap;
+  }
+  *out = &w;
+  return LLAMPC_OK;
+}
+
+int resolve_device(int32_t device, int* out) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+    return fail(LLAMPC_E_NODEV, "no HIP device visible (the HIP path has no CPU fallback)");
+  int d = device;
+  if (d < 0 && hipGetDevice(&d) != hipSuccess) d = 0;
+  if (d >= ndev) return fail(LLAMPC_E_ARG, "device %d of %d", d, ndev);
+  *out = d;
+  return LLAMPC_OK;
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+}  // namespace
+
+extern "C" int llampc_dynamics_batch(int32_t op, const double* x, const double* u,
+                                     const double* params, int64_t P, const llampc_vehicle* veh,
+                                     int64_t n, double* out, int32_t device, int32_t device_ptrs,
+                                     void* stream) {
+  if (!x || !u || !params || !veh || !out) return fail(LLAMPC_E_ARG, "NULL argument");
+  if (op != LLAMPC_OP_FORCES && op != LLAMPC_OP_DERIV) return fail(LLAMPC_E_ARG, "op %d", op);
+  if (n < 0 || !(P == 1 || P == n)) return fail(LLAMPC_E_ARG, "P=%lld must be 1 or n=%lld", (long long)P, (long long)n);
+  if (n == 0) return LLAMPC_OK;
+  int dev, rc;
+  if ((rc = resolve_device(device, &dev))) return rc;
+  DeviceGuard g(dev);
+  const VehK vk = make_veh(*veh);
+  const size_t out_n = (op == LLAMPC_OP_FORCES ? 5 : 6) * (size_t)n;
+  if (device_ptrs) {
+    HIP_TRY(launch_dynamics(op, x, u, params, P, vk, n, out, (hipStream_t)stream));
+    return LLAMPC_OK;
+  }
+  const size_t bx = align_up(6 * n * 8), bu = align_up(2 * n * 8), bp = align_up(6 * P * 8),
+               bo = align_up(out_n * 8);
+  Workspace* w;
+  std::lock_guard<std::mutex> lk(g_ws[dev].mu);
+  if ((rc = ws_get(dev, bx + bu + bp + bo, &w))) return rc;
+  char* base = (char*)w->d;
+  double *dx = (double*)base, *du = (double*)(base + bx), *dp = (double*)(base + bx + bu),
+         *dout = (double*)(base + bx + bu + bp);
+  HIP_TRY(hipMemcpyAsync(dx, x, 6 * n * 8, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(hipMemcpyAsync(du, u, 2 * n * 8, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(hipMemcpyAsync(dp, params, 6 * P * 8, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(launch_dynamics(op, dx, du, dp, P, vk, n, dout, w->stream));
+  HIP_TRY(hipMemcpyAsync(out, dout, out_n * 8, hipMemcpyDeviceToHost, w->stream));
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  return LLAMPC_OK;
+}
+
+extern "C" int llampc_integrate_batch(const double* x0, const double* u, int64_t u_stride_lane,
+                                      const double* h, int32_t S, const double* params, int64_t P,
+                                      const llampc_vehicle* veh, int64_t n, int32_t integrator,
+                                      double* traj_out, int32_t final_only, int32_t device,
+                                      int32_t device_ptrs, void* stream) {
+  if (!x0 || !u || !h || !params || !veh || !traj_out) return fail(LLAMPC_E_ARG, "NULL argument");
+  if (S < 1) return fail(LLAMPC_E_ARG, "S=%d must be >= 1", S);
+  if (n < 0 || !(P == 1 || P == n)) return fail(LLAMPC_E_ARG, "P must be 1 or n");
+  if (!(u_stride_lane == 0 || u_stride_lane == 2 * (int64_t)S))
+    return fail(LLAMPC_E_ARG, "u_stride_lane must be 0 or 2*S");
+  if (integrator < LLAMPC_RK4 || integrator > LLAMPC_RK6) return fail(LLAMPC_E_ARG, "integrator %d", integrator);
+  if (n == 0) return LLAMPC_OK;
+  int dev, rc;
+  if ((rc = resolve_device(device, &dev))) return rc;
+  DeviceGuard g(dev);
+  const VehK vk = make_veh(*veh);
+  const size_t out_n = (final_only ? 1 : (size_t)(S + 1)) * n * 6;
+  if (device_ptrs) {
+    HIP_TRY(launch_integrate(x0, u, u_stride_lane, h, S, params, P, vk, n, integrator, traj_out,
+                             final_only, (hipStream_t)stream));
+    return LLAMPC_OK;
+  }
+  const size_t un = (u_stride_lane ? (size_t)n : 1) * 2 * S;
+  const size_t bx = align_up(6 * n * 8), bu = align_up(un * 8), bh = align_up(S * 8),
+               bp = align_up(6 * P * 8), bo = align_up(out_n * 8);
+  Workspace* w;
+  std::lock_guard<std::mutex> lk(g_ws[dev].mu);
+  if ((rc = ws_get(dev, bx + bu + bh + bp + bo, &w))) return rc;
+  char* base = (char*)w->d;
+  double *dx = (double*)base, *du = (double*)(base + bx), *dh = (double*)(base + bx + bu),
+         *dp = (double*)(base + bx + bu + bh), *dout = (double*)(base + bx + bu + bh + bp);
+  HIP_TRY(hipMemcpyAsync(dx, x0, 6 * n * 8, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(hipMemcpyAsync(du, u, un * 8, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(hipMemcpyAsync(dh, h, S * 8, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(hipMemcpyAsync(dp, params, 6 * P * 8, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(launch_integrate(dx, du, u_stride_lane, dh, S, dp, P, vk, n, integrator, dout, final_only,
+                           w->stream));
+  HIP_TRY(hipMemcpyAsync(traj_out, dout, out_n * 8, hipMemcpyDeviceToHost, w->stream));
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  return LLAMPC_OK;
+}

@@ -1,0 +1,76 @@
+// kernels.hpp — internal launch interface between the C ABI (capi.hip) and the HIP
+// kernels (kernels.hip).  Every pointer here is a device pointer; launches are async.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dyn.hpp"
+#include "llampc.h"
+
+namespace llampc {
+
+constexpr int kBlock = 256;            // 4 waves of 64 lanes
+
+// Cost constants pre-scaled for the kernel (rate bounds multiplied by Ts).
+struct CostK {
+  double Q[4], R[4], P[4];
+  double umin[2], umax[2];
+  double dmax[2];                      // rate_max * Ts, < 0 = unbounded
+  int32_t enforce;
+  int32_t pad;
+};
+
+struct LookbackLaunch {
+  const double* params;  int64_t n;  int64_t goff;  // params [6][n]
+  VehK veh;
+  const double* x_prev; const double* u_prev; const double* x_now;
+  double Ts;
+  double* ring;          // [W][n]
+  int32_t W, slot, full, K, nan_first;
+  double* err_out;       // [n] or null
+  double* wmean_out;     // [n] or null
+  double* am_val;  int64_t* am_idx;   // [blocks]
+  double* tk_val;  int64_t* tk_idx;   // [blocks][K]
+};
+
+struct LookaheadLaunch {
+  const double* params;  int64_t n;  int64_t goff;
+  VehK veh;
+  const double* x0; const double* U; const double* xref; const double* uprev;
+  int32_t C, H, integrator;
+  double Ts;
+  CostK cost;
+  double* cost_out;                      // [n][C] or null
+  int32_t* best_cand;  double* best_cost; // [n]
+  double* pv;  int64_t* pidx;  int32_t* pnf;  // [blocks]
+};
+
+struct SelectLaunch {
+  int32_t do_lb, full, window_count, K, nan_first, lb_blocks;
+  const double* am_val; const int64_t* am_idx; const double* tk_val; const int64_t* tk_idx;
+  int32_t do_la, la_blocks, C;
+  const double* pv; const int64_t* pidx; const int32_t* pnf;
+  const double* params; int64_t n, goff;
+  const int32_t* best_cand; const double* best_cost;
+  int64_t current_model;
+  llampc_plan_out* out;
+};
+
+int lookback_blocks(int64_t n);
+int lookahead_group(int32_t C);
+int lookahead_blocks(int64_t n, int32_t C);
+size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u);
+
+hipError_t launch_lookback(const LookbackLaunch& a, hipStream_t s);
+hipError_t launch_lookahead(const LookaheadLaunch& a, hipStream_t s);
+hipError_t launch_select(const SelectLaunch& a, hipStream_t s);
+hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
+                        llampc_plan_out* merged, hipStream_t s);
+hipError_t launch_dynamics(int32_t op, const double* x, const double* u, const double* params,
+                           int64_t P, VehK veh, int64_t n, double* out, hipStream_t s);
+hipError_t launch_integrate(const double* x0, const double* u, int64_t u_stride_lane,
+                            const double* h, int32_t S, const double* params, int64_t P,
+                            VehK veh, int64_t n, int32_t integrator, double* traj,
+                            int32_t final_only, hipStream_t s);
+
+}  // namespace llampc

@@ -1,0 +1,192 @@
+"""Device-resident model bank (one shard) — the handle behind the look-back/look-ahead.
+
+Replaces the reference's MODEL_BANK list of N ``Dynamic`` objects, its ``params_pass``
+tuple (run_nmpc_orca_llampc_rt.py:161-179) and the ``error_windows`` array
+(rt.py:83-84).  Parameters live on the GPU as SoA [6][N] (Bf, Cf, Df, Br, Cr, Dr);
+the W-window is a slot-major ring [W][N] updated in place each tick.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from llampc import _native as nat
+from llampc.params import ORCA
+
+BANK_ORDER = ("Bf", "Cf", "Df", "Br", "Cr", "Dr")       # rt.py:179 params_pass order
+VARIATION_ORDER = ("Br", "Cr", "Dr", "Bf", "Cf", "Df")  # rt.py:153-158 draw order
+RT_SIGMA = {"Br": 0.2, "Cr": 0.1, "Dr": 0.5, "Bf": 0.2, "Cf": 0.1, "Df": 0.5}
+SHARED_KEYS = ("lf", "lr", "mass", "Iz", "Cm1", "Cm2", "Cr0", "Cr2")
+
+
+def generate_bank(n: int, seed: int, sigma=None, nominal: dict | None = None) -> np.ndarray:
+    """Seeded bank [6, n] with the reference's multiplicative Gaussian variation
+    p <- p * (1 + sigma_p z) (rt.py:161-170).  z is drawn model-major in rt.py's
+    parameter order, so ``np.random.seed(seed)`` + the reference loop gives the same bank;
+    the whole global bank is drawn on every rank, so shards are partition-invariant."""
+    if sigma is None:
+        sigma = RT_SIGMA
+    elif not isinstance(sigma, dict):
+        sigma = {k: float(sigma) for k in VARIATION_ORDER}
+    nominal = ORCA(control='pwm') if nominal is None else nominal
+    z = np.random.RandomState(seed).randn(n, len(VARIATION_ORDER))
+    bank = np.empty((6, n))
+    for j, name in enumerate(VARIATION_ORDER):
+        bank[BANK_ORDER.index(name)] = nominal[name] * (1 + sigma[name] * z[:, j])
+    return bank
+
+
+def shard_range(n_global: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous shard [lo, hi) of rank ``rank``; the remainder goes to the last rank."""
+    per = n_global // world
+    lo = rank * per
+    hi = n_global if rank == world - 1 else lo + per
+    return lo, hi
+
+
+class ModelBank:
+    """A shard of the model bank resident on one HIP device."""
+
+    def __init__(self, params6, shared: dict | None = None, W: int = 10, device: int = 0,
+                 global_offset: int = 0, input_acc: bool = False):
+        params6 = np.ascontiguousarray(np.asarray(params6, dtype=np.float64).reshape(6, -1))
+        self.params = params6
+        self.n = params6.shape[1]
+        self.W = int(W)
+        self.device = int(device)
+        self.global_offset = int(global_offset)
+        shared = ORCA(control='pwm') if shared is None else shared
+        self.shared = {k: float(shared[k]) for k in SHARED_KEYS}
+        self._veh = nat.vehicle(*(self.shared[k] for k in SHARED_KEYS), input_acc=input_acc, approx=False)
+        lib = nat.load()
+        h = nat.C.c_void_p()
+        nat.check(lib.llampc_bank_create(nat.dptr(params6), self.n, self.global_offset,
+                                         nat.C.byref(self._veh), self.W, self.device, nat.C.byref(h)))
+        self._h = h
+
+    # -------------------------------------------------------------- constructors
+    @classmethod
+    def from_models(cls, models, W=10, device=0, global_offset=0):
+        """From a list of ``Dynamic`` objects (the reference's MODEL_BANK); shared
+        constants come from models[0] as in evaluate_models_vectorized.py:15-21."""
+        p = np.array([[getattr(m, k) for m in models] for k in BANK_ORDER], dtype=np.float64)
+        m0 = models[0]
+        return cls(p, {k: getattr(m0, k) for k in SHARED_KEYS}, W=W, device=device,
+                   global_offset=global_offset, input_acc=m0.input_acc)
+
+    @classmethod
+    def generate(cls, n, seed=0, sigma=None, W=10, device=0, rank=0, world=1):
+        full = generate_bank(n, seed, sigma)
+        lo, hi = shard_range(n, rank, world)
+        return cls(full[:, lo:hi], W=W, device=device, global_offset=lo)
+
+    # -------------------------------------------------------------- lifecycle
+    @property
+    def handle(self):
+        if self._h is None:
+            raise nat.NativeError("bank is closed")
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            nat.load().llampc_bank_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_stream(self, stream_ptr: int | None):
+        nat.check(nat.load().llampc_bank_set_stream(self.handle, stream_ptr))
+
+    @property
+    def window_count(self) -> int:
+        c = nat.C.c_int32()
+        nat.check(nat.load().llampc_bank_info(self.handle, None, None, None, nat.C.byref(c), None))
+        return c.value
+
+    def reset(self):
+        nat.check(nat.load().llampc_bank_reset(self.handle))
+
+    def window(self) -> np.ndarray:
+        """The error window as rt.py keeps it: [N, W], newest in the last column."""
+        ring = np.empty((self.n, self.W))
+        nat.check(nat.load().llampc_bank_window(self.handle, nat.dptr(ring), None))
+        return ring
+
+    # -------------------------------------------------------------- hot path
+    def lookback(self, x_prev, u_prev, x_now, Ts=0.02, K=10, nan_policy=nat.NAN_FIRST,
+                 return_errors=False, return_window_mean=False) -> dict:
+        """One look-back tick (evaluate_models_vectorized.py:4-24 + rt.py:347-366)."""
+        err = np.empty(self.n) if return_errors else None
+        wm = np.empty(self.n) if return_window_mean else None
+        best = nat.C.c_int64()
+        topk = np.full(K, -1, dtype=np.int64)
+        topv = np.empty(K)
+        cnt = nat.C.c_int32()
+        nat.check(nat.load().llampc_lookback(
+            self.handle, nat.dptr(nat.f64(x_prev)), nat.dptr(nat.f64(u_prev)), nat.dptr(nat.f64(x_now)),
+            float(Ts), int(K), int(nan_policy), nat.dptr(err), nat.dptr(wm), nat.C.byref(best),
+            topk.ctypes.data_as(nat.C.POINTER(nat.C.c_int64)), nat.dptr(topv), nat.C.byref(cnt)))
+        full = cnt.value >= self.W
+        return dict(best=best.value if full else None, topk=topk if full else None,
+                    topk_val=topv if full else None, window_count=cnt.value, full=full,
+                    errors=err, window_mean=wm if full else None)
+
+    def lookahead(self, x0, U, xref, uprev, Ts=0.02, cost=None, integrator="rk4",
+                  return_costs=False, return_best_cand=False) -> dict:
+        """Roll every (model, candidate) over H steps and evaluate the NLP objective
+        (model.py:32-40 x H + nmpc.py:44-111).  U [C, H, 2]; xref [2, H+1]."""
+        U = nat.f64(U)
+        if U.ndim == 2:
+            U = U.reshape(1, *U.shape)
+        C_, H = U.shape[0], U.shape[1]
+        xref = nat.f64(xref)
+        if xref.shape != (2, H + 1):
+            raise ValueError(f"xref must be [2, {H + 1}], got {xref.shape}")
+        cost = cost if cost is not None else nat.cost_struct()
+        costs = np.empty((self.n, C_)) if return_costs else None
+        bc = np.empty(self.n, dtype=np.int32) if return_best_cand else None
+        bm, bcand, bcost = nat.C.c_int64(), nat.C.c_int32(), nat.C.c_double()
+        nat.check(nat.load().llampc_lookahead(
+            self.handle, nat.dptr(nat.f64(x0)), nat.dptr(U), C_, H, nat.dptr(xref),
+            nat.dptr(nat.f64(uprev)), nat.C.byref(cost), float(Ts), nat.INTEGRATORS[integrator],
+            nat.dptr(costs), None if bc is None else bc.ctypes.data_as(nat.C.POINTER(nat.C.c_int32)),
+            nat.C.byref(bm), nat.C.byref(bcand), nat.C.byref(bcost)))
+        return dict(best_model=bm.value, best_cand=bcand.value, best_cost=bcost.value, costs=costs,
+                    best_cand_per_model=bc)
+
+    def plan_raw(self, x_prev, u_prev, x_now, U, xref, uprev, Ts=0.02, K=10, integrator="rk4",
+                 do_lookback=True, do_lookahead=True, current_model=0, nan_policy=nat.NAN_FIRST,
+                 cost=None, return_errors=False, return_window_mean=False, return_costs=False):
+        """The fused tick (llampc_plan): returns (PlanOut, errors, window_mean, costs)."""
+        U = nat.f64(U)
+        if U.ndim == 2:
+            U = U.reshape(1, *U.shape)
+        C_, H = U.shape[0], U.shape[1]
+        keep = []
+        ptr = lambda a: (keep.append(nat.f64(a)), nat.dptr(keep[-1]))[1] if a is not None else None
+        pin = nat.PlanIn()
+        pin.x_prev, pin.u_prev, pin.x_now = ptr(x_prev), ptr(u_prev), ptr(x_now)
+        pin.U, pin.xref, pin.uprev = ptr(U), ptr(xref), ptr(uprev)
+        pin.C, pin.H, pin.K = C_, H, int(K)
+        pin.integrator = nat.INTEGRATORS[integrator]
+        pin.do_lookback, pin.do_lookahead = int(bool(do_lookback)), int(bool(do_lookahead))
+        pin.nan_policy = int(nan_policy)
+        pin.current_model = int(current_model)
+        pin.Ts = float(Ts)
+        pin.cost = cost if cost is not None else nat.cost_struct()
+        err = np.empty(self.n) if return_errors else None
+        wm = np.empty(self.n) if return_window_mean else None
+        costs = np.empty((self.n, C_)) if return_costs else None
+        out = nat.PlanOut()
+        nat.check(nat.load().llampc_plan(self.handle, nat.C.byref(pin), nat.C.byref(out), nat.dptr(err),
+                                         nat.dptr(wm), nat.dptr(costs)))
+        return out, err, wm, costs

@@ -1,0 +1,201 @@
+"""Closed-loop LLA-MPC controller around the GPU bank: the caller side of ``plan()``.
+
+Host logic restated from the reference driver (llampc/mpc/run_nmpc_orca_llampc_rt.py):
+  * ``update_friction``      friction schedules (rt.py:125-141; windows per track/case)
+  * ``ExponentialSmoother``  rt.py:103-113
+  * ``MuEstimator``          mu-hat from the top-K models (rt.py:326-344)
+  * ``CandidateGenerator``   sampled control sequences for the look-ahead (new; replaces
+                             the per-tick IPOPT solve of nmpc.py:161-203 by candidate search)
+  * ``LLAMPC.tick``          one tick in rt.py order: look-back on the newest transition,
+                             mu-hat, ConstantSpeed reference with mu-hat (rt.py:278-282),
+                             look-ahead of every (model, candidate), chosen control.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from llampc import _native as nat
+from llampc.mpc.bank import ModelBank
+from llampc.mpc.plan import PlanResult, result_from_out
+from llampc.mpc.planner import ConstantSpeed
+
+FRICTION_CASES = {
+    # (style, params) reproducing results/**/MUs.npy of the reference runs
+    "ETHZ_gradual": ("const_decay", dict(start=14.3)),
+    "ETHZ_sudden": ("sudden", dict(window=(14.3, 14.5))),
+    "ETHZ_sudden_begin": ("sudden", dict(window=(3.3, 3.5))),
+    "ETHZMobil_gradual": ("const_decay", dict(start=5.0)),
+    "ETHZMobil_sudden": ("sudden", dict(window=(5.0, 5.2))),
+    "nominal": ("no_change", {}),
+}
+
+
+def update_friction(Df, Dr, curr_time, style="sudden", start=14.3, window=(14.3, 14.5)):
+    """rt.py:125-141: 'const_decay' D -= D/2600 per tick after ``start``; 'sudden'
+    D -= D/22 per tick strictly inside ``window``; 'no_change'."""
+    if style == "const_decay":
+        if curr_time > start:
+            Df -= Df / 2600.
+            Dr -= Dr / 2600.
+    elif style == "sudden":
+        if window[0] < curr_time < window[1]:
+            Df -= Df / 22.
+            Dr -= Dr / 22.
+    return Df, Dr
+
+
+class ExponentialSmoother:
+    def __init__(self, alpha=0.3):
+        self.alpha = alpha
+        self.smooth_value = None
+
+    def update(self, new_value):
+        if self.smooth_value is None:
+            self.smooth_value = new_value
+        else:
+            self.smooth_value = self.alpha * new_value + (1 - self.alpha) * self.smooth_value
+        return self.smooth_value
+
+
+@dataclass
+class MuEstimator:
+    """rt.py:326-344.  While the window fills (tick <= W) the Dr/Df histories take the
+    nominal mu_init split (with g = 9.8, rt.py:327-328); afterwards the top-K mean."""
+    mass: float
+    lf: float
+    lr: float
+    mu_init: float = 1.0
+    S: int = 20                      # smoothing_mu (rt.py:68)
+    alpha: float = 0.08              # mu_alpha (rt.py:72)
+    dr_hist: list = field(default_factory=list)
+    df_hist: list = field(default_factory=list)
+    mu_pred: float | None = None
+    mu_logged: list = field(default_factory=list)
+
+    def __post_init__(self):
+        self.smoother = ExponentialSmoother(self.alpha)
+
+    def warmup(self):
+        self.dr_hist.append(self.mu_init * self.mass * 9.8 * self.lr / (self.lf + self.lr))
+        self.df_hist.append(self.mu_init * self.mass * 9.8 * self.lf / (self.lf + self.lr))
+        self.mu_logged.append(self.mu_init)
+
+    def update(self, topk_Dr, topk_Df) -> float:
+        self.dr_hist.append(np.mean(topk_Dr))
+        self.df_hist.append(np.mean(topk_Df))
+        dr = np.mean(np.array(self.dr_hist)[-self.S:])
+        df = np.mean(np.array(self.df_hist)[-self.S:])
+        self.mu_pred = (dr + df) / (9.81 * self.mass)
+        self.mu_logged.append(self.smoother.update(self.mu_pred) * .95)
+        return self.mu_pred
+
+
+class CandidateGenerator:
+    """C control sequences [C, H, 2] for the look-ahead: candidate 0 is the previous
+    choice shifted one step (warm start); the rest add N(0, diag(sig^2)) noise, clipped to
+    the input bounds and to the steering-rate bound |d delta| <= rate*Ts (orca.py:29-35,
+    nmpc.py:102-105).  Seeded."""
+
+    def __init__(self, C, H, Ts=0.02, sigma=(0.05, 0.02), umin=(-0.1, -0.35), umax=(1.0, 0.35),
+                 rate_max=(None, 5.0), seed=2):
+        self.C, self.H, self.Ts = C, H, Ts
+        self.sigma = np.asarray(sigma, dtype=np.float64)
+        self.umin, self.umax = np.asarray(umin, dtype=np.float64), np.asarray(umax, dtype=np.float64)
+        self.rate = [None if r is None else r * Ts for r in rate_max]
+        self.rng = np.random.RandomState(seed)
+
+    def __call__(self, prev_seq, uprev):
+        """prev_seq [H, 2] (or None), uprev [2] -> U [C, H, 2]."""
+        H = self.H
+        if prev_seq is None:
+            base = np.tile(np.asarray(uprev, dtype=np.float64), (H, 1))
+        else:
+            prev_seq = np.asarray(prev_seq, dtype=np.float64)
+            base = np.concatenate([prev_seq[1:], prev_seq[-1:]], axis=0)
+        U = np.repeat(base[None], self.C, axis=0)
+        if self.C > 1:
+            U[1:] += self.rng.randn(self.C - 1, H, 2) * self.sigma
+        U = np.clip(U, self.umin, self.umax)
+        for j, r in enumerate(self.rate):
+            if r is None:
+                continue
+            prev = np.full(self.C, float(uprev[j]))
+            for k in range(H):
+                U[:, k, j] = np.clip(U[:, k, j], prev - r, prev + r)
+                prev = U[:, k, j]
+        return np.ascontiguousarray(U)
+
+
+class LLAMPC:
+    """Stateful LLA-MPC tick loop over a ``ModelBank`` (rt.py:269-366 without IPOPT)."""
+
+    def __init__(self, bank: ModelBank, track, H=20, Ts=0.02, K=10, C=64, v_factor=0.9,
+                 mu_init=1.0, S=20, alpha=0.08, cost=None, integrator="rk4", seed=2,
+                 nan_policy=nat.NAN_FIRST):
+        self.bank, self.track = bank, track
+        self.H, self.Ts, self.K, self.W = H, Ts, K, bank.W
+        self.v_factor = v_factor
+        sh = bank.shared
+        self.mu = MuEstimator(mass=sh["mass"], lf=sh["lf"], lr=sh["lr"], mu_init=mu_init, S=S, alpha=alpha)
+        self.cost = cost if cost is not None else nat.cost_struct(enforce_bounds=True)
+        self.integrator = integrator
+        self.gen = CandidateGenerator(C, H, Ts, seed=seed)
+        self.nan_policy = nan_policy
+        self.current_model = 0          # rt.py:264
+        self.projidx = 0
+        self.t = 0
+        self.x_prev = None
+        self.u_prev = None
+        self.u_seq = None
+        self.last_topk = None
+
+    def tick(self, x_t) -> PlanResult:
+        x_t = np.asarray(x_t, dtype=np.float64)
+        t = self.t
+        # 1. look-back on the newest transition (the reference scores transition
+        #    idt -> idt+1 for idt >= 1, so tick t >= 2 here; rt.py:347)
+        lb = None
+        if t >= 2:
+            lb = self.bank.lookback(self.x_prev, self.u_prev, x_t, Ts=self.Ts, K=self.K,
+                                    nan_policy=self.nan_policy)
+            if lb["full"]:
+                self.current_model = int(lb["best"])
+                self.last_topk = lb["topk"]
+        # 2. reference (rt.py:278-282); it uses the mu-hat of the previous tick because
+        #    the reference updates mu-hat after its solve (rt.py:326-344)
+        if t > self.W + 1:
+            xref, self.projidx, _ = ConstantSpeed(x_t[:2], x_t[3], self.track, self.H, self.Ts,
+                                                  self.projidx, curr_mu=self.mu.mu_pred,
+                                                  scale=self.v_factor)
+        else:
+            xref, self.projidx, _ = ConstantSpeed(x_t[:2], x_t[3], self.track, self.H, self.Ts,
+                                                  self.projidx)
+        if self.projidx > self.track.lap_projidx:              # lap wrap (rt.py:287-296)
+            self.projidx = 0
+        # 3. mu-hat update from this look-back's top-K (rt.py:326-344)
+        if t <= self.W:
+            self.mu.warmup()
+        else:
+            p = self.bank.params
+            loc = self.last_topk - self.bank.global_offset
+            self.mu.update(p[5][loc], p[2][loc])
+        # 4. look-ahead of every (model, candidate) and the chosen control
+        uprev = np.zeros(2) if self.u_prev is None else self.u_prev
+        U = self.gen(self.u_seq, uprev)
+        o, _, _, _ = self.bank.plan_raw(np.zeros(6), np.zeros(2), x_t, U, xref, uprev, Ts=self.Ts,
+                                        K=self.K, integrator=self.integrator, do_lookback=False,
+                                        do_lookahead=True, current_model=self.current_model,
+                                        cost=self.cost)
+        res = result_from_out(o, U, mu_hat=self.mu.mu_pred)
+        if lb is not None and lb["full"]:
+            res.window_full, res.topk, res.topk_err = True, lb["topk"], lb["topk_val"]
+        res.window_count = self.bank.window_count
+        if res.u_seq is None:                       # selected model lives on another shard
+            res.u_seq = np.ascontiguousarray(U[0].T)
+        self.u_seq = res.u_seq.T
+        self.x_prev = x_t
+        self.u_prev = res.u_seq[:, 0].copy()
+        self.t += 1
+        return res

@@ -1,0 +1,398 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the pinned oracle and the
+reference-generated golden vectors.  Tolerances: fp64 values 1e-9 relative for one
+integration step (ocml vs NumPy transcendentals differ by ulps), 1e-7 for H-step rollouts
+and their costs (north star bound: 1e-5); indices exact (tie-tolerant only where stated)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import llampc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TS = 0.02
+RTOL_STEP = 1e-9
+RTOL_ROLL = 1e-7
+
+
+@pytest.fixture(scope="module")
+def nat():
+    from llampc import _native
+    _native.load()
+    if _native.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X")
+    return _native
+
+
+def shared():
+    p = O.orca_params()
+    return {k: p[k] for k in ("lf", "lr", "mass", "Iz", "Cm1", "Cm2", "Cr0", "Cr2")}
+
+
+def close(a, b, rtol, scale=None):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    fin = np.isfinite(b)
+    np.testing.assert_array_equal(np.isfinite(a), fin)
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    sc = np.max(np.abs(b[fin])) if scale is None and fin.any() else (scale or 1.0)
+    np.testing.assert_allclose(a[fin], b[fin], rtol=rtol, atol=rtol * 1e-3 * sc)
+
+
+# ----------------------------------------------------------------- Dynamic API (a1-a3)
+def test_dynamic_batch_forces_deriv_rk4(nat):
+    from llampc.models import Dynamic
+    g = golden("dynamics_batch.npz")
+    p = O.orca_params()
+    Bf, Cf, Df, Br, Cr, Dr = g["params"]
+    m = Dynamic(**{**p, "Bf": Bf, "Cf": Cf, "Df": Df, "Br": Br, "Cr": Cr, "Dr": Dr})
+    Ffy, Frx, Fry, af, ar = m.calc_forces_batch(g["x"], g["u"], return_slip=True)
+    for a, k in ((Ffy, "Ffy"), (Frx, "Frx"), (Fry, "Fry"), (af, "alphaf"), (ar, "alphar")):
+        close(a, g[k], RTOL_STEP)
+    close(m._diffequation_batch(None, g["x"], g["u"]), g["dxdt"], RTOL_STEP)
+    close(m._integrate_batch(g["x"], g["u"], 0, TS), g["x_rk4"], RTOL_STEP)
+    nom = Dynamic(**p)
+    close(nom._diffequation_batch(None, g["x"], g["u"]), g["dxdt_nominal"], RTOL_STEP)
+    close(nom._integrate_batch(g["x"], g["u"], 0, TS), g["x_rk4_nominal"], RTOL_STEP)
+
+
+def test_dynamic_approx_and_input_acc(nat):
+    from llampc.models import Dynamic
+    g = golden("dynamics_batch.npz")
+    p = O.orca_params()
+    apx = Dynamic(lf=p["lf"], lr=p["lr"], mass=p["mass"], Iz=p["Iz"], Cf=p["Cf"], Cr=p["Cr"])
+    assert apx.approx
+    close(apx._diffequation_batch(None, g["x_apx"], g["u"]), g["dxdt_approx"], RTOL_STEP)
+    acc = Dynamic(**{**p, "input_acc": True})
+    close(acc._diffequation_batch(None, g["x"], g["u"]), g["dxdt_input_acc"], RTOL_STEP)
+
+
+def test_sim_continuous_rk6_plant(nat):
+    from llampc.models import Dynamic
+    g = golden("plant_rk6.npz")
+    p = O.orca_params()
+    x = g["x"][0]
+    for k in range(g["u"].shape[1]):
+        m = Dynamic(**{**p, "Df": g["Df"][k], "Dr": g["Dr"][k]})
+        xn, _ = m.sim_continuous(x, g["u"][:, k:k + 1], [0, TS])
+        x = xn[:, -1]
+        close(x, g["x"][k + 1], RTOL_ROLL)
+    xm, dm = Dynamic(**p).sim_continuous(g["x"][0], g["u"][:, :10], np.arange(11) * TS)
+    close(xm, g["x_multi"], RTOL_ROLL)
+    close(dm, g["dxdt_multi"], RTOL_ROLL)
+    f = Dynamic(**p).calc_forces(g["x"][0], g["u"][:, 0])
+    fo = O.calc_forces(O.Vehicle.from_params(p), g["x"][0], g["u"][:, 0])
+    close(np.array(f), np.array(fo), RTOL_STEP)
+
+
+def test_evaluate_models_vectorized_dropin(nat):
+    from llampc.models import Dynamic
+    from llampc.mpc import evaluate_models_vectorized
+    g = golden("lookback_n1000.npz")
+    d = golden("dyn_slice.npz")
+    bank = golden("bank_rt_seed0_n1000.npz")["bank"]
+    models = [Dynamic(**O.orca_params())] * bank.shape[1]
+    for t in range(3):
+        pred = evaluate_models_vectorized(models, len(models), d["states"][:, t], d["inputs"][:, t], TS, tuple(bank))
+        close(pred, g["pred"][t], RTOL_STEP)
+
+
+# ----------------------------------------------------------------- look-back (a5-a6)
+def test_lookback_window_argmin_topk_vs_golden(nat):
+    from llampc.mpc import ModelBank
+    g = golden("lookback_n1000.npz")
+    d = golden("dyn_slice.npz")
+    bank = golden("bank_rt_seed0_n1000.npz")["bank"]
+    s, u = d["states"], d["inputs"]
+    full = 0
+    with ModelBank(bank, W=int(g["W"]), device=0) as b:
+        for t in range(int(g["ticks"])):
+            r = b.lookback(s[:, t], u[:, t], s[:, t + 1], Ts=TS, K=int(g["K"]), return_errors=True,
+                           return_window_mean=True)
+            close(r["errors"], g["errors"][t], RTOL_STEP)
+            if r["full"]:
+                close(r["window_mean"], g["window_mean"][full], RTOL_STEP)
+                assert r["best"] == g["best"][full]
+                np.testing.assert_array_equal(r["topk"], g["topk"][full])
+                np.testing.assert_allclose(r["topk_val"], g["window_mean"][full][g["topk"][full]], rtol=RTOL_STEP)
+                full += 1
+        assert full == len(g["best"])
+        ring = b.window()
+        np.testing.assert_allclose(ring[:, -1], g["errors"][-1], rtol=RTOL_STEP)
+        np.testing.assert_allclose(ring[:, 0], g["errors"][-int(g["W"])], rtol=RTOL_STEP)
+
+
+@pytest.mark.parametrize("N,W,K", [(1, 1, 1), (5, 3, 10), (257, 10, 10), (1000, 8, 32), (3001, 17, 7)])
+def test_lookback_edge_shapes(nat, N, W, K):
+    """Ragged N (not a multiple of 256), N < K (padding with -1), W below/above 8 (both
+    pairwise-sum branches), K up to KMAX."""
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    p = generate_bank(N, seed=N)
+    win = O.LookbackWindow(N, W, K)
+    with ModelBank(p, W=W, device=0) as b:
+        for t in range(W + 2):
+            r = b.lookback(s[:, t], u[:, t], s[:, t + 1], Ts=TS, K=K, return_errors=True, return_window_mean=True)
+            e = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), s[:, t], u[:, t], TS), s[:, t + 1])
+            close(r["errors"], e, RTOL_STEP)
+            assert win.push(e) == r["full"]
+            if r["full"]:
+                close(r["window_mean"], win.avg, RTOL_STEP)
+                assert r["best"] == win.current
+                kk = min(K, N)
+                np.testing.assert_array_equal(r["topk"][:kk], win.best_k[:kk])
+                assert np.all(r["topk"][kk:] == -1)
+
+
+def test_lookback_nan_semantics(nat):
+    """np.argmin returns the first NaN (rt.py:359); argsort puts NaN last (rt.py:360)."""
+    from llampc.mpc import ModelBank
+    g = golden("rollout_wide.npz")
+    p = g["params"]
+    x0, u0 = g["x0"], g["U"][0, 0]
+    with np.errstate(all="ignore"):
+        e = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), x0, u0, TS), g["x_next"])
+    p = p.copy()
+    p[2, 7] = np.nan          # a NaN model (Df) -> NaN error
+    p[2, 300] = np.nan
+    with np.errstate(all="ignore"):
+        e = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), x0, u0, TS), g["x_next"])
+    assert np.isnan(e[7]) and np.isnan(e[300])
+    for policy in (0, 1):
+        with ModelBank(p, W=1, device=0) as b:
+            r = b.lookback(x0, u0, g["x_next"], Ts=TS, K=10, nan_policy=policy, return_errors=True)
+            close(r["errors"], e, RTOL_STEP)
+            if policy == 0:
+                assert r["best"] == int(np.argmin(e)) == 7
+            else:
+                assert r["best"] == int(np.nanargmin(e))
+            np.testing.assert_array_equal(r["topk"], e.argsort(kind="stable")[:10])
+
+
+# ----------------------------------------------------------------- look-ahead (a8-a10)
+def test_lookahead_rk4_rollout_and_cost_vs_golden(nat):
+    from llampc import _native
+    from llampc.mpc import ModelBank
+    g = golden("rollout_rk4.npz")
+    U, x0, p = g["U"], g["x0"], g["params"]
+    N, C_ = p.shape[1], U.shape[0]
+    Q, R, P = np.diag([1, 1]), np.diag([5e-3, 1]), np.diag([0, 0])
+    for H in (20, 40):
+        xref = np.vstack([g["traj"][:H + 1, 0, 0] + 0.01, g["traj"][:H + 1, 0, 1] - 0.02])
+        cref = O.mpc_cost(g["traj"][:H + 1], U[:, :H], xref, g["uprev"], Q, R, P)
+        with ModelBank(p, device=0) as b:
+            r = b.lookahead(x0, U[:, :H], xref, g["uprev"], Ts=TS, return_costs=True, return_best_cand=True)
+        close(r["costs"].ravel(), cref, RTOL_ROLL)
+        cm = cref.reshape(N, C_)
+        np.testing.assert_array_equal(r["best_cand_per_model"], np.argmin(cm, axis=1))
+        assert (r["best_model"], r["best_cand"]) == divmod(int(np.argmin(cref)), C_)
+    # the final states through the raw integrate API (rk4, per-lane controls)
+    from llampc.models import Dynamic
+    rp = np.repeat(p, C_, axis=1)
+    m = Dynamic(**{**O.orca_params(), **{k: rp[i] for i, k in enumerate(O.BANK_ORDER)}})
+    u = np.tile(U, (N, 1, 1))
+    traj = m._native_integrate(np.tile(x0, (N * C_, 1)), u, np.full(40, TS), _native.RK4, final_only=False)
+    close(traj, g["traj"], RTOL_ROLL)
+
+
+@pytest.mark.parametrize("C,H", [(1, 20), (3, 7), (64, 20), (100, 5), (130, 40)])
+def test_lookahead_candidate_group_shapes(nat, C, H):
+    """C=1 (lane per model), non-power-of-two C, C = 64 (one model per wave), C > 64 (lanes
+    loop over candidates), LDS staging on (small C*H) and off (C*H*16 > 48 KB)."""
+    from llampc.mpc import ModelBank, generate_bank
+    N = 300
+    p = generate_bank(N, seed=C)
+    rng = np.random.RandomState(C)
+    x0 = np.array([0.2, 0.1, -0.7, 1.5, 0.02, 0.3])
+    U = np.stack([rng.uniform(-0.1, 1.0, (C, H)), rng.uniform(-0.35, 0.35, (C, H))], axis=-1)
+    xref = np.vstack([0.2 + 0.03 * np.arange(H + 1), 0.1 - 0.02 * np.arange(H + 1)])
+    uprev = np.array([0.3, 0.0])
+    with np.errstate(all="ignore"):
+        traj = O.rollout_rk4(shared(), tuple(p), x0, U, TS)
+        cref = O.mpc_cost(traj, U, xref, uprev, np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2)))
+    with ModelBank(p, device=0) as b:
+        r = b.lookahead(x0, U, xref, uprev, Ts=TS, return_costs=True, return_best_cand=True)
+    close(r["costs"].ravel(), cref, RTOL_ROLL)
+    cm = np.where(np.isnan(cref), np.inf, cref).reshape(N, C)
+    np.testing.assert_array_equal(r["best_cand_per_model"], np.argmin(cm, axis=1))
+    assert r["best_model"] * C + r["best_cand"] == int(np.argmin(cm.ravel()))
+
+
+def test_lookahead_feasibility_mask(nat):
+    from llampc import _native
+    from llampc.mpc import ModelBank, generate_bank
+    N, C, H = 64, 6, 10
+    p = generate_bank(N, seed=1)
+    U = np.zeros((C, H, 2))
+    U[:, :, 0] = 0.5
+    U[1, 3, 1] = 0.2          # steering jump 0.2 > 5*Ts -> infeasible
+    U[2, 0, 0] = 1.2          # pwm above max -> infeasible
+    U[3, :, 1] = np.linspace(0, 0.09, H)   # within rate
+    xref = np.zeros((2, H + 1))
+    ok = O.candidates_feasible(U, np.zeros(2), [-0.1, -0.35], [1.0, 0.35], 5.0, TS)
+    assert list(ok) == [True, False, False, True, True, True]
+    cost = _native.cost_struct(enforce_bounds=True)
+    x0 = np.array([0, 0, 0, 1.0, 0, 0])
+    with ModelBank(p, device=0) as b:
+        r = b.lookahead(x0, U, xref, np.zeros(2), Ts=TS, cost=cost, return_costs=True)
+    assert np.all(np.isinf(r["costs"][:, ~ok])) and np.all(np.isfinite(r["costs"][:, ok]))
+
+
+def test_lookahead_euler_nlp_and_rk6(nat):
+    """NLP-form Euler (dynamic.py:195-226 + nmpc.py:58-60; restated, parity unpinned) and
+    RK6 look-ahead integrators against the oracle restatements."""
+    from llampc.mpc import ModelBank, generate_bank
+    N, C, H = 200, 2, 20
+    p = generate_bank(N, seed=4)
+    x0 = np.array([0.1, 0.2, 0.3, 0.03, 0.01, 0.2])      # vx < vmin: exercises the clamp
+    U = np.zeros((C, H, 2))
+    U[:, :, 0] = [[0.6], [0.9]]
+    U[:, :, 1] = 0.05
+    xref = np.zeros((2, H + 1))
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    with ModelBank(p, device=0) as b:
+        r = b.lookahead(x0, U, xref, np.zeros(2), Ts=TS, integrator="euler_nlp", return_costs=True)
+        traj = O.rollout_euler_nlp(shared(), tuple(p), x0, U, TS)
+        close(r["costs"].ravel(), O.mpc_cost(traj, U, xref, np.zeros(2), Q, R, P), RTOL_ROLL)
+        x0b = np.array([0.1, 0.2, 0.3, 1.0, 0.01, 0.2])
+        r6 = b.lookahead(x0b, U, xref, np.zeros(2), Ts=TS, integrator="rk6", return_costs=True)
+    # RK6 reference: the oracle's scalar odeintRK6 restatement per model (first 20 models)
+    for n in range(20):
+        v = O.Vehicle.from_params(O.orca_params(), **{k: p[i, n] for i, k in enumerate(O.BANK_ORDER)})
+        for c in range(C):
+            xs, _ = O.sim_continuous(v, x0b, U[c].T, np.arange(H + 1) * TS)
+            cc = O.mpc_cost(xs.T[:, None, :], U[c:c + 1], xref, np.zeros(2), Q, R, P)[0]
+            np.testing.assert_allclose(r6["costs"][n, c], cc, rtol=RTOL_ROLL)
+
+
+# ----------------------------------------------------------------- fused tick + merge
+def test_plan_fused_tick_vs_oracle(nat):
+    from llampc.mpc import ModelBank, generate_bank, plan
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    N, W, K, H, C = 2000, 10, 10, 20, 8
+    p = generate_bank(N, seed=0)
+    win = O.LookbackWindow(N, W, K)
+    rng = np.random.RandomState(2)
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    with ModelBank(p, W=W, device=0) as b:
+        for t in range(1, W + 4):
+            U = np.repeat(u[:, t:t + H].T[None], C, axis=0)
+            U[1:] += rng.randn(C - 1, H, 2) * [0.05, 0.02]
+            xref = s[:2, t:t + H + 1] + 0.01
+            res = plan(b, s[:, t], u[:, t - 1], s[:, t - 1], xref, U, uprev=u[:, t - 1], Ts=TS, K=K,
+                       current_model=3, return_errors=True, return_window_mean=True, return_costs=True)
+            e = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), s[:, t - 1], u[:, t - 1], TS), s[:, t])
+            win.push(e)
+            close(res.lookback_err, e, RTOL_STEP)
+            traj = O.rollout_rk4(shared(), tuple(p), s[:, t], U, TS)
+            cref = O.mpc_cost(traj, U, xref, u[:, t - 1], Q, R, P).reshape(N, C)
+            close(res.costs, cref, RTOL_ROLL)
+            sel = win.current if win.count >= W else 3
+            assert res.best_model == sel
+            assert res.best_cand == int(np.argmin(cref[sel]))
+            np.testing.assert_array_equal(res.u_seq, U[res.best_cand].T)
+            if win.count >= W:
+                np.testing.assert_array_equal(res.topk, win.best_k)
+                np.testing.assert_array_equal(res.topk_Df, p[2][win.best_k])
+                np.testing.assert_array_equal(res.topk_Dr, p[5][win.best_k])
+                np.testing.assert_array_equal(res.raw.topk_cand[:K], np.argmin(cref[win.best_k], axis=1))
+            assert res.global_best[0] * C + res.global_best[1] == int(np.argmin(cref.ravel()))
+
+
+def test_merge_device_equals_host_and_unsharded(nat):
+    """Shard a bank 4 ways on one GPU: device merge == host merge == unsharded tick."""
+    import ctypes
+    import torch
+    from llampc.mpc import ModelBank, generate_bank, shard_range
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    N, W, G, H, C = 3000, 3, 4, 20, 4
+    p = generate_bank(N, seed=9)
+    U = np.repeat(u[:, 5:5 + H].T[None], C, axis=0)
+    U[:, :, 1] += np.linspace(-0.02, 0.02, C)[:, None]
+    xref = s[:2, 5:5 + H + 1]
+    banks = [ModelBank(p[:, lo:hi], W=W, device=0, global_offset=lo)
+             for lo, hi in (shard_range(N, g, G) for g in range(G))]
+    full = ModelBank(p, W=W, device=0)
+    try:
+        for t in range(1, W + 2):
+            outs = [b.plan_raw(s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1], K=10)[0] for b in banks]
+            ref = full.plan_raw(s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1], K=10)[0]
+            host = nat.merge(outs)
+            raw = b"".join(ctypes.string_at(ctypes.addressof(o), nat.PLAN_OUT_BYTES) for o in outs)
+            dparts = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+            dm = torch.empty(nat.PLAN_OUT_BYTES, dtype=torch.uint8, device="cuda")
+            nat.check(nat.load().llampc_merge_device(dparts.data_ptr(), G, 0, dm.data_ptr(), 0, None))
+            torch.cuda.synchronize()
+            dev = nat.PlanOut.from_buffer_copy(dm.cpu().numpy().tobytes())
+            for o in (host, dev):
+                a, r = nat.plan_out_to_dict(o), nat.plan_out_to_dict(ref)
+                for k in ("window_count", "window_full", "lb_best", "sel_model", "sel_cand",
+                          "la_best_model", "la_best_cand", "n_nonfinite"):
+                    assert a[k] == r[k], (k, a[k], r[k])
+                for k in ("topk", "topk_cand"):
+                    np.testing.assert_array_equal(a[k], r[k])
+                for k in ("topk_val", "topk_Df", "topk_Dr", "topk_cost"):
+                    np.testing.assert_array_equal(a[k], r[k])
+    finally:
+        for b in banks + [full]:
+            b.close()
+
+
+# ----------------------------------------------------------------- closed loop + full size
+def test_closed_loop_lookback_and_mu_vs_golden(nat):
+    """The reference tick logic (rt.py:269-366) over 60 ticks: model selection, top-K and
+    mu-hat sequences through ModelBank + MuEstimator."""
+    from llampc.mpc import ModelBank, MuEstimator
+    g = golden("closed_loop.npz")
+    p = O.orca_params()
+    x, u = g["x"], g["u"]
+    bank = g["bank"]
+    mu = MuEstimator(mass=p["mass"], lf=p["lf"], lr=p["lr"])
+    cur, topk = 0, None
+    with ModelBank(bank, W=10, device=0) as b:
+        for idt in range(u.shape[1]):
+            if idt <= 10:
+                mu.warmup()
+            else:
+                mu.update(bank[5][topk], bank[2][topk])
+                np.testing.assert_allclose(mu.mu_pred, g["mu_pred"][idt], rtol=1e-12)
+            np.testing.assert_allclose(mu.mu_logged[-1], g["mu_logged"][idt], rtol=1e-12)
+            if idt > 0:
+                r = b.lookback(x[idt], u[:, idt], x[idt + 1], Ts=TS, K=10)
+                if r["full"]:
+                    cur, topk = r["best"], r["topk"]
+                    np.testing.assert_array_equal(topk, g["topk"][idt])
+            assert cur == g["current"][idt]
+
+
+@pytest.mark.parametrize("N,H,track", [(10000, 20, "ETHZ"), (10000, 40, "ETHZMobil"), (80000, 20, "ETHZ")])
+def test_baseline_sizes_properties(nat, N, H, track):
+    """BASELINE.json sizes: errors/costs vs the oracle on every model (numpy handles these
+    sizes in seconds), selection consistent with the returned arrays, top-K sorted."""
+    from llampc.mpc import ModelBank, generate_bank, plan
+    from llampc.mpc.planner import ConstantSpeed
+    from llampc.tracks import ETHZ, ETHZMobil
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    tr = ETHZ() if track == "ETHZ" else ETHZMobil()
+    p = generate_bank(N, seed=0 if track == "ETHZ" else 1)
+    W, K = 10, 10
+    with ModelBank(p, W=W, device=0) as b:
+        for t in range(1, W + 2):
+            x_t = s[:, t]
+            xref, _, _ = ConstantSpeed(x_t[:2], x_t[3], tr, H, TS, 0)
+            U = np.repeat(np.tile(u[:, t], (H, 1))[None], 1, axis=0)
+            res = plan(b, x_t, u[:, t - 1], s[:, t - 1], xref, U, Ts=TS, K=K, return_errors=True,
+                       return_window_mean=True, return_costs=True)
+        e = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), s[:, W], u[:, W], TS), s[:, W + 1])
+        close(res.lookback_err, e, RTOL_STEP)
+        wm = res.window_mean
+        assert res.best_model == int(np.argmin(wm))
+        assert np.all(np.diff(wm[res.topk]) >= 0) and set(res.topk) == set(np.argsort(wm, kind="stable")[:K])
+        traj = O.rollout_rk4(shared(), tuple(p), s[:, W + 1], U, TS)
+        cref = O.mpc_cost(traj, U, xref, u[:, W], np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2)))
+        close(res.costs.ravel(), cref, RTOL_ROLL)
+        assert res.global_best[0] == int(np.argmin(np.where(np.isnan(cref), np.inf, cref)))

@@ -1,0 +1,104 @@
+"""N>1 path on CPU: world_size-2 gloo processes each produce their shard's llampc_plan_out
+record (the oracle stands in for the GPU kernels here — test infrastructure), exchange
+them with the product's ``gather_merge_host`` (one all-gather) and must reproduce the
+unsharded look-back selection / top-K / look-ahead best on every rank."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO, PKG_ROOT, golden
+
+TS = 0.02
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _local_record(nat, p_all, lo, hi, states, inputs, W, K, U, xref, uprev):
+    """Shard [lo, hi) record computed with the oracle (what the GPU kernels produce)."""
+    from oracle import llampc_oracle as O
+    pp = O.orca_params()
+    shared = {k: pp[k] for k in ("lf", "lr", "mass", "Iz", "Cm1", "Cm2", "Cr0", "Cr2")}
+    p = p_all[:, lo:hi]
+    win = O.LookbackWindow(hi - lo, W, K)
+    for t in range(W):
+        e = O.lookback_errors(O.evaluate_models_vectorized(shared, tuple(p), states[:, t], inputs[:, t], TS), states[:, t + 1])
+        win.push(e)
+    x_now = states[:, W]
+    traj = O.rollout_rk4(shared, tuple(p), x_now, U, TS)
+    C = U.shape[0]
+    cost = O.mpc_cost(traj, U, xref, uprev, np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))).reshape(-1, C)
+    o = nat.PlanOut()
+    o.window_count, o.window_full, o.K = win.count, 1, K
+    j = int(np.argmin(win.avg))
+    o.lb_best, o.lb_best_val = lo + j, win.avg[j]
+    bc = np.argmin(cost, axis=1)
+    o.sel_model, o.sel_owned, o.sel_cand, o.sel_cost = lo + j, 1, int(bc[j]), cost[j, bc[j]]
+    top = win.best_k
+    for k in range(nat.KMAX):
+        if k < K:
+            i = top[k]
+            o.topk[k], o.topk_val[k] = lo + i, win.avg[i]
+            o.topk_Df[k], o.topk_Dr[k] = p[2, i], p[5, i]
+            o.topk_cand[k], o.topk_cost[k] = int(bc[i]), cost[i, bc[i]]
+        else:
+            o.topk[k], o.topk_cand[k] = -1, -1
+    f = int(np.argmin(cost.ravel()))
+    o.la_best_model, o.la_best_cand, o.la_best_cost = lo + f // C, f % C, cost.ravel()[f]
+    o.n_nonfinite = int((~np.isfinite(cost)).sum())
+    return o, win, cost
+
+
+def _worker(rank, world, port, q):
+    try:
+        for pth in (REPO, PKG_ROOT):
+            sys.path.insert(0, pth)
+        import torch.distributed as dist
+        from llampc import _native as nat
+        from llampc.mpc import generate_bank, shard_range
+        from llampc.mpc.sharded import gather_merge_host
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        d = golden("dyn_slice.npz")
+        N, W, K, H, C = 601, 10, 10, 20, 3
+        p = generate_bank(N, seed=0)
+        s, u = d["states"], d["inputs"]
+        U = np.repeat(u[:, W:W + H].T[None], C, axis=0)
+        U[:, :, 1] += np.array([-0.01, 0.0, 0.01])[:, None]
+        xref = s[:2, W:W + H + 1] + 0.02
+        lo, hi = shard_range(N, rank, world)
+        local, _, _ = _local_record(nat, p, lo, hi, s, u, W, K, U, xref, u[:, W - 1])
+        merged = nat.plan_out_to_dict(gather_merge_host(local))
+        ref, win, cost = _local_record(nat, p, 0, N, s, u, W, K, U, xref, u[:, W - 1])
+        ref = nat.plan_out_to_dict(ref)
+        for k in ("lb_best", "sel_model", "sel_cand", "la_best_model", "la_best_cand", "n_nonfinite"):
+            assert merged[k] == ref[k], (k, merged[k], ref[k])
+        for k in ("topk", "topk_val", "topk_Df", "topk_Dr", "topk_cand", "topk_cost"):
+            np.testing.assert_array_equal(merged[k], ref[k])
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_merge_gloo(world):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+    for rank, msg in res:
+        assert msg == "ok", f"rank {rank}: {msg}"
