@@ -4,7 +4,7 @@
 One *step* = one LLA-MPC control tick of the hot path over the whole bank:
 look-back (score every model on the newest transition, slide the W-window, argmin +
 top-K) + look-ahead (H-step RK4 rollout + MPC cost of every (model, candidate)) +
-selection, i.e. ``llampc_plan_device`` (3 kernels).  With --gpus N > 1 each rank owns a
+selection, i.e. ``llampc_plan_device`` (ONE kernel launch).  With --gpus N > 1 each rank owns a
 contiguous shard of N_per_gpu models (weak scaling; config 4 = 8 x 10^4) and every tick
 adds ONE RCCL all-gather of the 1.5 KB shard record plus the on-device merge.
 
@@ -190,7 +190,7 @@ def main():
     if not args.no_timing:
         nat.check(lib.llampc_bank_timing_read(sb.bank.handle, avg, cnt))
         nat.check(lib.llampc_bank_timing(sb.bank.handle, 0, 1))
-    la_ms, lb_ms, sel_ms = avg[1], avg[0], avg[2]
+    plan_ms = avg[0]
 
     merged = sb.fetch(stream)          # result of the last tick (all ranks identical)
 
@@ -201,17 +201,19 @@ def main():
     if rank == 0:
         steps_per_tick = N_total * C * H + N_total
         value = steps_per_tick / (ms / 1e3)
-        # algorithmic HBM bytes of one look-ahead launch (the dominant kernel): params 48 B
-        # + per-model result 12 B per model, candidates 16*C*H, xref 16*(H+1), x0/uprev 64
-        la_bytes = N_local * (48 + 12) + 16 * C * H + 16 * (H + 1) + 64
-        achieved = la_bytes / (la_ms * 1e-3) / 1e9 if la_ms > 0 else None
+        # algorithmic HBM bytes of one fused plan-kernel launch (the dominant kernel), SURVEY
+        # §8(d): per model params 48 B + ring read 8W + ring write 8 + look-ahead result 12;
+        # per launch candidates 16*C*H + xref 16*(H+1) + states/inputs 64
+        plan_bytes = N_local * (48 + 8 * W + 8 + 12) + 16 * C * H + 16 * (H + 1) + 64
+        achieved = plan_bytes / (plan_ms * 1e-3) / 1e9 if plan_ms > 0 else None
         traffic = pmc_traffic(args)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                "kernel": "lookahead_kernel<RK4>", "kernel_avg_us": la_ms * 1e3,
-                "bytes_per_launch": la_bytes,
+                "kernel": "plan_kernel<RK4> (the whole tick: look-back + look-ahead + selection)",
+                "kernel_avg_us": plan_ms * 1e3,
+                "bytes_per_launch": plan_bytes,
                 "note": "binding resource is fp64 VALU/latency, not HBM (see valu)"}
-        valu_gf = N_local * C * H * FLOPS_PER_MODEL_STEP / (la_ms * 1e-3) / 1e9 if la_ms > 0 else None
+        valu_gf = (N_local * C * H + N_local) * FLOPS_PER_MODEL_STEP / (plan_ms * 1e-3) / 1e9 if plan_ms > 0 else None
         line = {
             "metric": "model-rollouts/sec (N_models x H steps) per control tick; wall-clock per plan() call",
             "value": value, "unit": "model-rollout-steps/s", "n_gpus": world, "steps": args.steps,
@@ -228,8 +230,8 @@ def main():
                      "frac": valu_gf / (FP64_VALU_PEAK_TFLOPS * 1e3) if valu_gf else None,
                      "flops_per_model_step": FLOPS_PER_MODEL_STEP,
                      "note": "plain flops only; the 29 fp64 transcendentals per RK4 step are excluded"},
-            "kernel_us": {"lookback": lb_ms * 1e3, "lookahead": la_ms * 1e3, "select": sel_ms * 1e3,
-                          "events": list(cnt)},
+            "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0])},
+            "lpm": lpm_of(N_local, C),
             "result_check": {"sel_model": merged.best_model, "window_full": merged.window_full,
                              "sel_cand": merged.best_cand, "n_nonfinite": merged.n_nonfinite},
             "cpu_baseline": None,
@@ -280,6 +282,24 @@ def extras(args, sb, stream, world):
         out["sync_plan_latency_us"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                        "note": "host-pointer llampc_plan incl. H2D/D2H + stream sync"}
     return out
+
+
+def lpm_of(n, C):
+    """Lanes per rollout the library picks (mirror of kernels.hip lookahead_lpm)."""
+    G = 1
+    while G < C and G < 64:
+        G <<= 1
+    env = os.environ.get("LLAMPC_LPM")
+    if env in ("1", "2", "4"):
+        v = int(env)
+        while v > 1 and G * v > 64:
+            v >>= 1
+        return v
+    if n * G <= 32768 and G <= 16:
+        return 4
+    if n * G <= 131072 and G <= 32:
+        return 2
+    return 1
 
 
 def pmc_traffic(args):

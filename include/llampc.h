@@ -151,11 +151,12 @@ int llampc_bank_window(llampc_bank* bank, double* ring, int32_t* window_count);
 int llampc_bank_set_stream(llampc_bank* bank, void* stream);
 
 /* Per-kernel HIP-event timing of the bank's launches, on the stream they run on (for the
- * benchmark's roofline).  enable=1 arms `max_launches` event pairs per kernel; each
- * launch of {look-back, look-ahead, select} is bracketed by hipEventRecord. */
+ * benchmark's roofline).  enable=1 arms `max_launches` event pairs; each launch of the
+ * plan kernel (the whole tick: look-back + look-ahead + selection) is bracketed by
+ * hipEventRecord. */
 int llampc_bank_timing(llampc_bank* bank, int32_t enable, int32_t max_launches);
-/* Synchronises, returns avg_ms[3] and count[3] for {look-back, look-ahead, select} since
- * the last read, and re-arms the counters. */
+/* Synchronises, returns avg_ms[3] and count[3] for {plan kernel, reserved, reserved}
+ * since the last read, and re-arms the counters. */
 int llampc_bank_timing_read(llampc_bank* bank, double* avg_ms, int64_t* count);
 
 /* ---- look-back (host pointers) -------------------------------------------------- */
@@ -185,7 +186,7 @@ int llampc_plan_device(llampc_bank* bank, const llampc_plan_in* in, void* d_out,
                        double* d_err, double* d_wmean, double* d_cost, void* stream);
 
 /* ---- multi-GPU merge ----------------------------------------------------------- */
-/* Merge G shard results (shards ordered by global_offset) into one, deterministic:
+/* Merge G shard results (shards ordered by global_offset; G <= 32 on the device) into one, deterministic:
  * lowest value, ties -> lowest global index, NaN first for lb_best under NAN_FIRST.
  * Host version runs the same merge code as the device version. */
 int llampc_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_policy,

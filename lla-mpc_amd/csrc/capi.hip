@@ -127,6 +127,7 @@ struct llampc_bank {
   double* d_err = nullptr;         // [n]
   double* d_wmean = nullptr;       // [n]
   double* d_cost = nullptr;        // [n*C]
+  unsigned* d_tickets = nullptr;   // [2] in-launch completion tickets
   size_t cost_cap = 0;
   std::mutex mu;
   // optional per-kernel event timing: [kernel][2*i] start, [kernel][2*i+1] stop
@@ -179,11 +180,12 @@ int check_plan_in(const llampc_bank* b, const llampc_plan_in* in) {
     if ((b->n + 1) * (int64_t)in->C <= 0 || b->n > INT64_MAX / std::max(1, in->C) - 1)
       return fail(LLAMPC_E_ARG, "n*C overflows");
   }
+  if (!in->do_lookback && !in->do_lookahead) return fail(LLAMPC_E_ARG, "nothing to do: look-back and look-ahead both off");
   if (!(in->Ts > 0) || !std::isfinite(in->Ts)) return fail(LLAMPC_E_ARG, "Ts must be finite > 0");
   return LLAMPC_OK;
 }
 
-// Event bracket around one launch of kernel `k` (0 look-back, 1 look-ahead, 2 select).
+// Event bracket around one launch of kernel `k` (0 the plan kernel; 1, 2 reserved).
 struct TimedLaunch {
   llampc_bank* b;
   int k;
@@ -209,95 +211,91 @@ void timing_free(llampc_bank* b) {
   b->timing = false;
 }
 
-// The tick on device pointers.  Advances the window bookkeeping when a look-back runs.
+// The tick on device pointers: ONE launch (look-back + look-ahead + completion).
+// Advances the window bookkeeping when a look-back runs.
 int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out, double* d_err,
                 double* d_wmean, double* d_cost, hipStream_t s) {
   const bool lb = in.do_lookback != 0;
   const bool la = in.do_lookahead != 0;
   int32_t count = b->count;
   int32_t full = count >= b->W;
+  const int32_t slot = b->slot;
+  LookbackLaunch lbl{};
   if (lb) {
-    const int32_t slot = b->slot;
     count = std::min(count + 1, b->W);             // rt.py:354
     full = count >= b->W;                          // rt.py:357
-    LookbackLaunch a{};
-    a.params = b->d_params;
-    a.n = b->n;
-    a.goff = b->goff;
-    a.veh = b->veh;
-    a.x_prev = in.x_prev;
-    a.u_prev = in.u_prev;
-    a.x_now = in.x_now;
-    a.Ts = in.Ts;
-    a.ring = b->d_ring;
-    a.W = b->W;
-    a.slot = slot;
-    a.full = full;
-    a.K = in.K;
-    a.nan_first = in.nan_policy == LLAMPC_NAN_FIRST;
-    a.err_out = d_err;
-    a.wmean_out = d_wmean;
-    a.am_val = b->d_am_val;
-    a.am_idx = b->d_am_idx;
-    a.tk_val = b->d_tk_val;
-    a.tk_idx = b->d_tk_idx;
-    {
-      TimedLaunch tl(b, 0, s);
-      HIP_TRY(launch_lookback(a, s));
-    }
+    lbl.params = b->d_params;
+    lbl.n = b->n;
+    lbl.goff = b->goff;
+    lbl.veh = b->veh;
+    lbl.x_prev = in.x_prev;
+    lbl.u_prev = in.u_prev;
+    lbl.x_now = in.x_now;
+    lbl.Ts = in.Ts;
+    lbl.ring = b->d_ring;
+    lbl.W = b->W;
+    lbl.slot = slot;
+    lbl.full = full;
+    lbl.K = in.K;
+    lbl.nan_first = in.nan_policy == LLAMPC_NAN_FIRST;
+    lbl.err_out = d_err;
+    lbl.wm_buf = d_wmean ? d_wmean : b->d_wmean;
+    lbl.am_val = b->d_am_val;
+    lbl.am_idx = b->d_am_idx;
+    lbl.tk_val = b->d_tk_val;
+    lbl.tk_idx = b->d_tk_idx;
+  }
+  LookaheadLaunch lal{};
+  if (la) {
+    lal.params = b->d_params;
+    lal.n = b->n;
+    lal.goff = b->goff;
+    lal.veh = b->veh;
+    lal.x0 = in.x_now;
+    lal.U = in.U;
+    lal.xref = in.xref;
+    lal.uprev = in.uprev;
+    lal.C = in.C;
+    lal.H = in.H;
+    lal.integrator = in.integrator;
+    lal.Ts = in.Ts;
+    lal.cost = make_cost(in.cost, in.Ts);
+    lal.cost_out = d_cost;
+    lal.best_cand = b->d_best_cand;
+    lal.best_cost = b->d_best_cost;
+    lal.pv = b->d_pv;
+    lal.pidx = b->d_pidx;
+    lal.pnf = b->d_pnf;
+  }
+  FinalLaunch f{};
+  f.out = d_out;
+  f.tickets = b->d_tickets;
+  f.full = full;
+  f.window_count = count;
+  f.K = lb ? in.K : 0;
+  f.nan_first = in.nan_policy == LLAMPC_NAN_FIRST;
+  f.C = la ? in.C : 1;
+  f.current_model = in.current_model;
+  f.n = b->n;
+  f.goff = b->goff;
+  f.params = b->d_params;
+  f.best_cand = b->d_best_cand;
+  f.best_cost = b->d_best_cost;
+  f.am_val = b->d_am_val;
+  f.am_idx = b->d_am_idx;
+  f.tk_val = b->d_tk_val;
+  f.tk_idx = b->d_tk_idx;
+  f.pv = b->d_pv;
+  f.pidx = b->d_pidx;
+  f.pnf = b->d_pnf;
+  {
+    TimedLaunch tl(b, 0, s);
+    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s));
+  }
+  if (lb) {
     b->slot = (slot + 1) % b->W;
     b->count = count;
   }
-  if (la) {
-    LookaheadLaunch a{};
-    a.params = b->d_params;
-    a.n = b->n;
-    a.goff = b->goff;
-    a.veh = b->veh;
-    a.x0 = in.x_now;
-    a.U = in.U;
-    a.xref = in.xref;
-    a.uprev = in.uprev;
-    a.C = in.C;
-    a.H = in.H;
-    a.integrator = in.integrator;
-    a.Ts = in.Ts;
-    a.cost = make_cost(in.cost, in.Ts);
-    a.cost_out = d_cost;
-    a.best_cand = b->d_best_cand;
-    a.best_cost = b->d_best_cost;
-    a.pv = b->d_pv;
-    a.pidx = b->d_pidx;
-    a.pnf = b->d_pnf;
-    TimedLaunch tl(b, 1, s);
-    HIP_TRY(launch_lookahead(a, s));
-  }
-  SelectLaunch sl{};
-  sl.do_lb = lb;
-  sl.full = full;
-  sl.window_count = count;
-  sl.K = lb ? in.K : 0;
-  sl.nan_first = in.nan_policy == LLAMPC_NAN_FIRST;
-  sl.lb_blocks = lookback_blocks(b->n);
-  sl.am_val = b->d_am_val;
-  sl.am_idx = b->d_am_idx;
-  sl.tk_val = b->d_tk_val;
-  sl.tk_idx = b->d_tk_idx;
-  sl.do_la = la;
-  sl.la_blocks = la ? lookahead_blocks(b->n, in.C) : 0;
-  sl.C = la ? in.C : 1;
-  sl.pv = b->d_pv;
-  sl.pidx = b->d_pidx;
-  sl.pnf = b->d_pnf;
-  sl.params = b->d_params;
-  sl.n = b->n;
-  sl.goff = b->goff;
-  sl.best_cand = b->d_best_cand;
-  sl.best_cost = b->d_best_cost;
-  sl.current_model = in.current_model;
-  sl.out = d_out;
-  TimedLaunch tl(b, 2, s);
-  HIP_TRY(launch_select(sl, s));
   return LLAMPC_OK;
 }
 
@@ -383,7 +381,7 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
     return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
   b->own_stream = true;
   const int lbb = lookback_blocks(n);
-  const int lab = lookahead_blocks(n, 64);   // worst case: one model per wave
+  const int lab = lookahead_blocks(n, 64, 1);   // worst case: one model per wave
   if ((rc = dev_alloc(&b->d_params, 6 * (size_t)n)) || (rc = dev_alloc(&b->d_ring, (size_t)W * n)) ||
       (rc = dev_alloc(&b->d_am_val, lbb)) || (rc = dev_alloc(&b->d_am_idx, lbb)) ||
       (rc = dev_alloc(&b->d_tk_val, (size_t)lbb * LLAMPC_KMAX)) ||
@@ -391,12 +389,13 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
       (rc = dev_alloc(&b->d_pidx, lab)) || (rc = dev_alloc(&b->d_pnf, lab)) ||
       (rc = dev_alloc(&b->d_best_cand, n)) || (rc = dev_alloc(&b->d_best_cost, n)) ||
       (rc = dev_alloc(&b->d_err, n)) || (rc = dev_alloc(&b->d_wmean, n)) ||
-      (rc = dev_alloc(&b->d_out, 1)))
+      (rc = dev_alloc(&b->d_out, 1)) || (rc = dev_alloc(&b->d_tickets, 2)))
     return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&b->h_out), sizeof(llampc_plan_out), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(out) failed"));
   if (hipMemcpy(b->d_params, params, 6 * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(b->d_ring, 0, (size_t)W * n * sizeof(double)) != hipSuccess ||
+      hipMemset(b->d_tickets, 0, 2 * sizeof(unsigned)) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "bank upload failed"));
   *out = b;
@@ -410,7 +409,7 @@ int llampc_bank_destroy(llampc_bank* b) {
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     void* dptrs[] = {b->d_params, b->d_ring, b->d_am_val, b->d_am_idx, b->d_tk_val, b->d_tk_idx,
                      b->d_pv, b->d_pidx, b->d_pnf, b->d_best_cand, b->d_best_cost, b->d_in,
-                     b->d_out, b->d_err, b->d_wmean, b->d_cost};
+                     b->d_out, b->d_err, b->d_wmean, b->d_cost, b->d_tickets};
     for (void* p : dptrs)
       if (p) (void)hipFree(p);
     if (b->h_in) (void)hipHostFree(b->h_in);
@@ -438,6 +437,7 @@ int llampc_bank_reset(llampc_bank* b) {
   std::lock_guard<std::mutex> lk(b->mu);
   DeviceGuard g(b->device);
   HIP_TRY(hipMemsetAsync(b->d_ring, 0, (size_t)b->W * b->n * sizeof(double), b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_tickets, 0, 2 * sizeof(unsigned), b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   b->count = 0;
   b->slot = 0;

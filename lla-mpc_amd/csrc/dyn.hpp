@@ -191,6 +191,128 @@ __device__ __host__ __forceinline__ void step(const VehK& v, const Tire& t, doub
 }
 
 // ------------------------------------------------------------------------------------
+// Lane-split evaluation (latency regime).  LPM lanes (a pair or a quad of consecutive
+// lanes) carry the SAME state; each lane runs ONE transcendental chain of the stage with
+// an identical instruction stream (lane-dependent operands via selects, no divergence),
+// and the results are exchanged with DPP quad_perm broadcasts:
+//   LPM=2: lane 0 front tire   atan2 -> atan -> sin -> Ffy   (+ sincos(psi) in both)
+//          lane 1 rear tire    atan2 -> atan -> sin -> Fry
+//   LPM=4: lane 0 sin(psi), lane 1 Ffy, lane 2 Fry, lane 3 cos(psi): one
+//          atan2 -> atan -> sincos chain per lane (lanes 0/3 discard their atan results)
+// Every lane then forms dx/dt and the integrator update redundantly (cheap, identical).
+// ------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_bcast(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// quad_perm encodings: broadcast lane k of each quad = k * 0x55; pairs [0,0,2,2] = 0xA0,
+// [1,1,3,3] = 0xF5.
+constexpr int kQuad0 = 0x00, kQuad1 = 0x55, kQuad2 = 0xAA, kQuad3 = 0xFF;
+constexpr int kPair0 = 0xA0, kPair1 = 0xF5;
+
+template <Form F, int LPM>
+__device__ __forceinline__ void rhs_split(const VehK& v, const Tire& t, const double* x,
+                                          const Input& u, double* dx, int sub) {
+  if (LPM == 1 || v.approx) {           // wave-uniform: no transcendental chains to split
+    rhs<F>(v, t, x, u, dx);
+    return;
+  }
+  double vx = x[3], vy = x[4], om = x[5];
+  double d = u.d, sd = u.sd, cd = u.cd;
+  if (F == Form::Nlp) {
+    const double vmin = 0.05;
+    if (vx < vmin) {                    // same state in every lane of the group: uniform per group
+      vy = 0.0;
+      om = 0.0;
+      d = 0.0;
+      sd = 0.0;
+      cd = 1.0;
+      vx = vmin;
+    }
+  }
+  const bool front = (LPM == 2) ? (sub == 0) : (sub == 1);
+  const double den = (F == Form::Ref) ? fabs(vx) : vx;
+  const double yy = front ? (v.lf * om + vy) : (v.lr * om - vy);
+  const double a2 = atan2(yy, den);
+  const double slip = front ? (d - a2) : a2;
+  const double B = front ? t.Bf : t.Br, Cc = front ? t.Cf : t.Cr, D = front ? t.Df : t.Dr;
+  double arg = Cc * atan(B * slip);
+  double Ffy, Fry, sp, cp;
+  if (LPM == 2) {
+    const double r = D * sin(arg);
+    Ffy = dpp_bcast<kPair0>(r);
+    Fry = dpp_bcast<kPair1>(r);
+    sincos(x[2], &sp, &cp);
+  } else {
+    const bool psi_lane = (sub == 0) | (sub == 3);
+    arg = psi_lane ? x[2] : arg;
+    double s, c;
+    sincos(arg, &s, &c);
+    const double r = (sub == 3) ? c : (psi_lane ? s : D * s);
+    sp = dpp_bcast<kQuad0>(r);
+    Ffy = dpp_bcast<kQuad1>(r);
+    Fry = dpp_bcast<kQuad2>(r);
+    cp = dpp_bcast<kQuad3>(r);
+  }
+  const double Frx = v.input_acc ? v.mass * u.a : (v.Cm1 - v.Cm2 * vx) * u.a - v.Cr0 - v.Cr2 * (vx * vx);
+  dx[0] = vx * cp - vy * sp;
+  dx[1] = vx * sp + vy * cp;
+  dx[2] = om;
+  dx[3] = v.inv_mass * (Frx - Ffy * sd) + vy * om;
+  dx[4] = v.inv_mass * (Fry + Ffy * cd) - vx * om;
+  dx[5] = v.inv_Iz * (Ffy * v.lf * cd - Fry * v.lr);
+}
+
+template <int LPM>
+__device__ __forceinline__ void rk4_step_split(const VehK& v, const Tire& t, double* x,
+                                               const Input& u, double h, int sub) {
+  double y[6], d[6], acc[6];
+  rhs_split<Form::Ref, LPM>(v, t, x, u, d, sub);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double k = h * d[i];
+    acc[i] = k;
+    y[i] = x[i] + k / 2;
+  }
+  rhs_split<Form::Ref, LPM>(v, t, y, u, d, sub);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double k = h * d[i];
+    acc[i] = acc[i] + 2 * k;
+    y[i] = x[i] + k / 2;
+  }
+  rhs_split<Form::Ref, LPM>(v, t, y, u, d, sub);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double k = h * d[i];
+    acc[i] = acc[i] + 2 * k;
+    y[i] = x[i] + k;
+  }
+  rhs_split<Form::Ref, LPM>(v, t, y, u, d, sub);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = x[i] + (acc[i] + h * d[i]) / 6;
+}
+
+template <int INTEG, int LPM>
+__device__ __forceinline__ void step_split(const VehK& v, const Tire& t, double* x,
+                                           const Input& u, double h, int sub) {
+  if (LPM == 1) {
+    step<INTEG>(v, t, x, u, h);
+  } else if (INTEG == 0) {
+    rk4_step_split<LPM>(v, t, x, u, h, sub);
+  } else if (INTEG == 1) {
+    double d[6];
+    rhs_split<Form::Nlp, LPM>(v, t, x, u, d, sub);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = x[i] + h * d[i];
+  } else {
+    step<INTEG>(v, t, x, u, h);        // RK6 (plant) stays one lane per rollout
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Ordering keys (value, index).  Total orders; indices are unique so ties never remain.
 // NaN-last: np.argsort order (rt.py:360) and the look-ahead argmin.
 // NaN-first: np.argmin (rt.py:359) — the first NaN wins.

@@ -15,11 +15,34 @@
 //                      model.py:18-40, rk6.py).
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "kernels.hpp"
 #include "merge.hpp"
 
 namespace llampc {
+
+#ifdef LLAMPC_STAMPS
+// Diagnostic build only (-DLLAMPC_STAMPS, libllampc_hip_stamps.so): tid-0 stamps of
+// s_memtime (shader clock) and s_memrealtime (100 MHz) at phase boundaries of the select
+// kernel; never compiled into the product library.
+__device__ unsigned long long g_stamps[64][8][2];
+__device__ unsigned int g_stamp_launch;
+#define STAMP(slot)                                                                      \
+  do {                                                                                   \
+    if (threadIdx.x == 0) {                                                              \
+      const unsigned l = g_stamp_launch & 63;                                            \
+      g_stamps[l][slot][0] = __builtin_amdgcn_s_memtime();                               \
+      g_stamps[l][slot][1] = __builtin_amdgcn_s_memrealtime();                           \
+    }                                                                                    \
+  } while (0)
+#else
+#define STAMP(slot) \
+  do {              \
+  } while (0)
+#endif
 
 namespace {
 
@@ -39,28 +62,6 @@ __device__ __forceinline__ void wave_min(double& v, int64_t& i) {
       i = oi;
     }
   }
-}
-
-// Block-wide min of (v, i); every thread returns the result.  sv/si: 4-entry LDS scratch.
-template <int NAN_FIRST>
-__device__ __forceinline__ void block_min(double& v, int64_t& i, double* sv, int64_t* si) {
-  wave_min<NAN_FIRST>(v, i);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    sv[w] = v;
-    si[w] = i;
-  }
-  __syncthreads();
-  v = sv[0];
-  i = si[0];
-#pragma unroll
-  for (int k = 1; k < kBlock / 64; ++k) {
-    if (kless<NAN_FIRST>(sv[k], si[k], v, i)) {
-      v = sv[k];
-      i = si[k];
-    }
-  }
-  __syncthreads();
 }
 
 __device__ __forceinline__ int block_sum(int x, int32_t* sn) {
@@ -117,19 +118,87 @@ __device__ __forceinline__ double window_mean(const double* ring, int64_t ld, in
 }  // namespace
 
 // ------------------------------------------------------------------------------------
-// Look-back
+// Look-back body (one block = 256 models, lane per model)
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void lookback_kernel(LookbackLaunch a) {
-  __shared__ double sv[kBlock / 64];
-  __shared__ int64_t si[kBlock / 64];
-  const int64_t n = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const bool live = n < a.n;
-  double wm = 0.0;
-  if (live) {
+// Dynamic LDS carve shared by every role (16-B aligned offsets, cdna_hip_programming.md
+// G17): [0,64) sv[2][4] double | [64,128) si[2][4] int64 | [128,144) sn[4] int32 |
+// pad to 160 | role-specific region from 160.
+constexpr int kScratchBytes = 160;
+
+struct Scratch {
+  double* sv;
+  int64_t* si;
+  int32_t* sn;
+  __device__ explicit Scratch(unsigned char* smem)
+      : sv(reinterpret_cast<double*>(smem)),
+        si(reinterpret_cast<int64_t*>(smem + 64)),
+        sn(reinterpret_cast<int32_t*>(smem + 128)) {}
+};
+
+// Block min with ONE barrier: consecutive calls alternate between two scratch buffers, so
+// a buffer is rewritten only after the next call's barrier has retired all its readers.
+template <int NAN_FIRST>
+__device__ __forceinline__ void block_min1(double& v, int64_t& i, const Scratch& s, int& par) {
+  wave_min<NAN_FIRST>(v, i);
+  double* sv = s.sv + 4 * par;
+  int64_t* si = s.si + 4 * par;
+  par ^= 1;
+  if ((threadIdx.x & 63) == 0) {
+    sv[threadIdx.x >> 6] = v;
+    si[threadIdx.x >> 6] = i;
+  }
+  __syncthreads();
+  v = sv[0];
+  i = si[0];
+#pragma unroll
+  for (int k = 1; k < kBlock / 64; ++k) {
+    if (kless<NAN_FIRST>(sv[k], si[k], v, i)) {
+      v = sv[k];
+      i = si[k];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// In-launch completion tickets (wait-free; cdna_hip_programming.md Guideline 16 form):
+// every storing wave drains its stores, the block barriers, lane 0 releases at agent scope
+// and bumps the ticket; the block that draws the last ticket acquires and continues.  No
+// block ever waits on another, so residency/dispatch order cannot deadlock.  Tickets are
+// reset by the final block (and zeroed when a bank is created or reset).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ bool ticket_last(unsigned* t, unsigned expected, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == expected - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// ------------------------------------------------------------------------------------
+// Look-back body: one block = 256*R models (R models per lane, coalesced in r).
+// RK4 step from (x_{t-1}, u_{t-1}), 4-state MSE against x_t, in-place ring write, window
+// mean in NumPy's pairwise order; then the block's argmin and its SORTED top-K list.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk, const Scratch& sc) {
+  const int64_t base = (int64_t)blk * kBlock * a.R;
+  const Input u = make_input(a.u_prev[0], a.u_prev[1]);
+  double wm0 = 0.0;                     // R == 1 keeps the window mean in a register
+  for (int r = 0; r < a.R; ++r) {
+    const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
+    if (n >= a.n) break;
     double x[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
-    const Input u = make_input(a.u_prev[0], a.u_prev[1]);
     const Tire t = load_tire(a.params, a.n, n);
     rk4_step(a.veh, t, x, u, a.Ts);                       // model.py:32-40, one RK4 step
     double s = 0.0;                                       // rt.py:349 mean over 4 states
@@ -143,37 +212,53 @@ __global__ __launch_bounds__(kBlock) void lookback_kernel(LookbackLaunch a) {
     a.ring[(int64_t)a.slot * a.n + n] = err;             // rt.py:352-353 without np.roll
     if (a.full) {
       const int o = (a.slot + 1 == a.W) ? 0 : a.slot + 1;   // oldest slot
-      wm = window_mean(a.ring, a.n, n, o, a.W);           // rt.py:358
-      if (a.wmean_out) a.wmean_out[n] = wm;
+      const double wm = window_mean(a.ring, a.n, n, o, a.W);   // rt.py:358
+      a.wm_buf[n] = wm;
+      if (r == 0) wm0 = wm;
     }
   }
-  if (!a.full) return;  // grid-uniform
+  if (!a.full) return;  // launch-uniform
 
-  const int64_t gi = live ? a.goff + n : kNoIndex;
-  // per-block argmin (rt.py:359)
-  double v = live ? wm : (a.nan_first ? __builtin_inf() : __builtin_nan(""));
-  int64_t i = gi;
-  if (a.nan_first) block_min<1>(v, i, sv, si);
-  else block_min<0>(v, i, sv, si);
-  if (threadIdx.x == 0) {
-    a.am_val[blockIdx.x] = v;
-    a.am_idx[blockIdx.x] = i;
+  // the block's argmin (rt.py:359 semantics) over its 256*R models
+  int par = 0;
+  double v = a.nan_first ? __builtin_inf() : __builtin_nan("");
+  int64_t i = kNoIndex;
+  for (int r = 0; r < a.R; ++r) {
+    const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
+    if (n >= a.n) break;
+    const double w = (a.R == 1) ? wm0 : a.wm_buf[n];
+    if (key_less(a.nan_first, w, a.goff + n, v, i)) {
+      v = w;
+      i = a.goff + n;
+    }
   }
-  // per-block top-K in argsort order (rt.py:360): K rounds of "next larger key"
-  const double mv = live ? wm : __builtin_nan("");
+  if (a.nan_first) block_min1<1>(v, i, sc, par);
+  else block_min1<0>(v, i, sc, par);
+  if (threadIdx.x == 0) {
+    a.am_val[blk] = v;
+    a.am_idx[blk] = i;
+  }
+  // sorted top-K of the block (rt.py:360 argsort order): K rounds of "next larger key"
   double lv = 0.0;
   int64_t li = -1;
   for (int k = 0; k < a.K; ++k) {
-    double cv = mv;
-    int64_t ci = gi;
-    if (li >= 0 && !less_nan_last(lv, li, mv, gi)) {
-      cv = __builtin_nan("");
-      ci = kNoIndex;
+    double cv = __builtin_nan("");
+    int64_t ci = kNoIndex;
+    for (int r = 0; r < a.R; ++r) {
+      const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
+      if (n >= a.n) break;
+      const double w = (a.R == 1) ? wm0 : a.wm_buf[n];
+      const int64_t gi = a.goff + n;
+      if (li >= 0 && !less_nan_last(lv, li, w, gi)) continue;
+      if (less_nan_last(w, gi, cv, ci)) {
+        cv = w;
+        ci = gi;
+      }
     }
-    block_min<0>(cv, ci, sv, si);
+    block_min1<0>(cv, ci, sc, par);
     if (threadIdx.x == 0) {
-      a.tk_val[(int64_t)blockIdx.x * a.K + k] = cv;
-      a.tk_idx[(int64_t)blockIdx.x * a.K + k] = ci;
+      a.tk_val[(int64_t)blk * a.K + k] = cv;
+      a.tk_idx[(int64_t)blk * a.K + k] = ci;
     }
     lv = cv;
     li = ci;
@@ -181,23 +266,16 @@ __global__ __launch_bounds__(kBlock) void lookback_kernel(LookbackLaunch a) {
 }
 
 // ------------------------------------------------------------------------------------
-// Look-ahead
+// Look-ahead body.  Lane layout inside a block: sub = lane % LPM (lane-split of one
+// rollout), cl = lane / LPM; G candidate-lanes per model (power of two); a model's
+// candidates c = g + j*G, j < cpl, run sequentially in its G*LPM lanes.
+//   LDS from kScratchBytes: xref as [k][2]; U as [k][c][2] when staged.
 // ------------------------------------------------------------------------------------
-// Dynamic LDS carve (16-B aligned offsets, cdna_hip_programming.md G17):
-//   [0, 32)  sv[4] double  | [32, 64) si[4] int64 | [64, 80) sn[4] int32 | pad to 96
-//   [96, 96 + 16(H+1))     xref as [k][2]
-//   [.., + 16*C*H)         U as [k][c][2] when staged (consecutive c -> consecutive 16 B)
-constexpr int kScratchBytes = 96;
-
-template <int INTEG, bool STAGE>
-__global__ __launch_bounds__(kBlock) void lookahead_kernel(LookaheadLaunch a, int G, int cpl) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* sv = reinterpret_cast<double*>(smem);
-  int64_t* si = reinterpret_cast<int64_t*>(smem + 32);
-  int32_t* sn = reinterpret_cast<int32_t*>(smem + 64);
+template <int INTEG, bool STAGE, int LPM>
+__device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int blk, int G, int cpl,
+                                                unsigned char* smem, const Scratch& sc) {
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);
   double* su = sx + 2 * (a.H + 1);
-
   const int H = a.H, C = a.C;
   for (int e = threadIdx.x; e <= H; e += kBlock) {
     sx[2 * e] = a.xref[e];
@@ -212,8 +290,10 @@ __global__ __launch_bounds__(kBlock) void lookahead_kernel(LookaheadLaunch a, in
   }
   __syncthreads();
 
-  const int g = threadIdx.x & (G - 1);
-  const int64_t n = (int64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  const int sub = threadIdx.x % LPM;
+  const int cl = threadIdx.x / LPM;
+  const int g = cl & (G - 1);
+  const int64_t n = (int64_t)blk * (kBlock / (G * LPM)) + cl / G;
   const bool live = n < a.n;
   const CostK& q = a.cost;
   const double up0 = a.uprev[0], up1 = a.uprev[1];
@@ -249,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void lookahead_kernel(LookaheadLaunch a, in
           if (q.dmax[1] >= 0) feas = feas && d1 <= q.dmax[1] && -d1 <= q.dmax[1];
         }
         const Input u = make_input(ua, ud);
-        step<INTEG>(a.veh, t, x, u, a.Ts);
+        step_split<INTEG, LPM>(a.veh, t, x, u, a.Ts, sub);
         const double e0 = x[0] - sx[2 * (k + 1)], e1 = x[1] - sx[2 * (k + 1) + 1];
         track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
         act = act + (d0 * (q.R[0] * d0 + q.R[1] * d1) + d1 * (q.R[2] * d0 + q.R[3] * d1));
@@ -260,16 +340,18 @@ __global__ __launch_bounds__(kBlock) void lookahead_kernel(LookaheadLaunch a, in
       const double term = e0 * (q.P[0] * e0 + q.P[1] * e1) + e1 * (q.P[2] * e0 + q.P[3] * e1);
       double J = (term + track) + act;                                // nmpc.py:111
       if (!feas) J = __builtin_inf();
-      if (a.cost_out) a.cost_out[n * C + c] = J;
-      nf += !isfinite(J);
+      if (sub == 0) {
+        if (a.cost_out) a.cost_out[n * C + c] = J;
+        nf += !isfinite(J);
+      }
       if (less_nan_last(J, c, bv, bc)) {
         bv = J;
         bc = c;
       }
     }
   }
-  // per-model argmin over its candidates: xor-shuffles inside the G-lane group
-  for (int off = G >> 1; off > 0; off >>= 1) {
+  // per-model argmin over its candidates: xor-shuffles across the model's G*LPM lanes
+  for (int off = (G * LPM) >> 1; off >= LPM; off >>= 1) {
     const double ov = __shfl_xor(bv, off, 64);
     const int64_t oc = __shfl_xor(bc, off, 64);
     if (less_nan_last(ov, oc, bv, bc)) {
@@ -277,140 +359,346 @@ __global__ __launch_bounds__(kBlock) void lookahead_kernel(LookaheadLaunch a, in
       bc = oc;
     }
   }
-  if (live && g == 0) {
+  if (live && g == 0 && sub == 0) {
     a.best_cand[n] = (int32_t)bc;
     a.best_cost[n] = bv;
   }
   // per-block argmin over (model, candidate) in flattened order (goff+n)*C + c
   int64_t key = (live && bc != kNoIndex) ? (a.goff + n) * C + bc : kNoIndex;
   double v = (key == kNoIndex) ? __builtin_nan("") : bv;
-  block_min<0>(v, key, sv, si);
-  const int nfs = block_sum(nf, sn);
+  int par = 0;
+  block_min1<0>(v, key, sc, par);
+  const int nfs = block_sum(nf, sc.sn);
   if (threadIdx.x == 0) {
-    a.pv[blockIdx.x] = v;
-    a.pidx[blockIdx.x] = key;
-    a.pnf[blockIdx.x] = nfs;
+    a.pv[blk] = v;
+    a.pidx[blk] = key;
+    a.pnf[blk] = nfs;
   }
 }
 
-// ------------------------------------------------------------------------------------
-// Select: merge per-block partials into the tick's llampc_plan_out
-// ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void select_kernel(SelectLaunch a) {
-  __shared__ double sv[kBlock / 64];
-  __shared__ int64_t si[kBlock / 64];
-  __shared__ int32_t sn[kBlock / 64];
-  __shared__ int64_t s_top[LLAMPC_KMAX];
-  __shared__ double s_topv[LLAMPC_KMAX];
-  const int tid = threadIdx.x;
-  const bool lb = a.do_lb && a.full;
+struct Ent {
+  double v;
+  int64_t i;
+};
 
-  double lbv = __builtin_nan("");
-  int64_t lbi = -1;
-  if (lb) {
-    double v = a.nan_first ? __builtin_inf() : __builtin_nan("");
-    int64_t i = kNoIndex;
-    for (int b = tid; b < a.lb_blocks; b += kBlock) {
-      if (a.am_idx[b] == kNoIndex) continue;
-      if (key_less(a.nan_first, a.am_val[b], a.am_idx[b], v, i)) {
-        v = a.am_val[b];
-        i = a.am_idx[b];
-      }
+__device__ __forceinline__ bool ent_less(const Ent& x, const Ent& y) {
+  return less_nan_last(x.v, x.i, y.v, y.i);
+}
+
+// Element k (0-based) of merge(A, B), |A| = |B| = K, both sorted with sentinel padding:
+// co-rank binary search (merge path), ~log2(K) dependent LDS reads.
+__device__ __forceinline__ Ent merge_path_at(const Ent* A, const Ent* B, int K, int k) {
+  int lo = 0, hi = k;                       // i = elements taken from A before output k
+  while (lo < hi) {
+    const int i = (lo + hi) >> 1;
+    if (ent_less(A[i], B[k - i - 1])) lo = i + 1;   // A[i] precedes B[k-i-1]: take more A
+    else hi = i;
+  }
+  const int i = lo, j = k - lo;
+  return ent_less(A[i], B[j]) ? A[i] : B[j];
+}
+
+// Tree-merge L sorted K-lists in LDS (buf0 holds them; buf1 same size); every output
+// element of a level is computed by its own thread.  Returns the buffer holding the merged
+// list (first K entries).
+__device__ __forceinline__ Ent* tree_merge(Ent* buf0, Ent* buf1, int L, int K) {
+  Ent* src = buf0;
+  Ent* dst = buf1;
+  while (L > 1) {
+    const int P = (L + 1) >> 1;
+    for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
+      const int p = t / K, k = t - p * K;
+      const Ent* A = src + (size_t)(2 * p) * K;
+      dst[t] = (2 * p + 1 < L) ? merge_path_at(A, A + K, K, k) : A[k];
     }
-    if (a.nan_first) block_min<1>(v, i, sv, si);
-    else block_min<0>(v, i, sv, si);
-    if (i != kNoIndex) {
-      lbv = v;
-      lbi = i;
-    }
-    double lv = 0.0;
-    int64_t li = -1;
-    const int M = a.lb_blocks * a.K;
-    for (int k = 0; k < a.K; ++k) {
-      double cv = __builtin_nan("");
-      int64_t ci = kNoIndex;
-      for (int e = tid; e < M; e += kBlock) {
-        const int64_t idx = a.tk_idx[e];
-        if (idx == kNoIndex) continue;
-        const double val = a.tk_val[e];
-        if (li >= 0 && !less_nan_last(lv, li, val, idx)) continue;
-        if (less_nan_last(val, idx, cv, ci)) {
-          cv = val;
-          ci = idx;
-        }
-      }
-      block_min<0>(cv, ci, sv, si);
-      if (tid == 0) {
-        s_top[k] = ci;
-        s_topv[k] = cv;
-      }
-      lv = cv;
-      li = ci;
+    __syncthreads();
+    Ent* tmp = src;
+    src = dst;
+    dst = tmp;
+    L = P;
+  }
+  return src;
+}
+
+// ------------------------------------------------------------------------------------
+// Completion stages run by ticket winners inside the plan launch.
+// lb_final  (last look-back block): argmin over the blocks' argmins; tree merge of the
+//           blocks' sorted top-K lists in LDS; writes the look-back fields of the record.
+//           It runs while look-ahead blocks are still rolling out, off the critical path.
+// final     (last block overall): look-ahead best over the block partials, the selected
+//           model's choice, each top-K model's best candidate; completes the record.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* smem, const Scratch& sc) {
+  STAMP(0);
+  const int tid = threadIdx.x;
+  const int M = f.nb_lb * f.K;
+  Ent* buf0 = reinterpret_cast<Ent*>(smem + kScratchBytes);
+  Ent* buf1 = buf0 + M;
+  for (int e = tid; e < M; e += kBlock) buf0[e] = Ent{f.tk_val[e], f.tk_idx[e]};
+  double v = f.nan_first ? __builtin_inf() : __builtin_nan("");
+  int64_t i = kNoIndex;
+  for (int b = tid; b < f.nb_lb; b += kBlock) {
+    const int64_t bi = f.am_idx[b];
+    const double bv = f.am_val[b];
+    if (bi != kNoIndex && key_less(f.nan_first, bv, bi, v, i)) {
+      v = bv;
+      i = bi;
     }
   }
+  int par = 0;
+  if (f.nan_first) block_min1<1>(v, i, sc, par);   // its barrier also publishes buf0
+  else block_min1<0>(v, i, sc, par);
+  STAMP(1);
+  const Ent* r = tree_merge(buf0, buf1, f.nb_lb, f.K);
+  STAMP(2);
+  llampc_plan_out* o = f.out;
+  if (tid < LLAMPC_KMAX) {
+    const int k = tid;
+    const int64_t id = k < f.K ? r[k].i : kNoIndex;
+    if (id != kNoIndex) {
+      const int64_t li = id - f.goff;
+      o->topk[k] = id;
+      o->topk_val[k] = r[k].v;
+      o->topk_Df[k] = f.params[2 * f.n + li];
+      o->topk_Dr[k] = f.params[5 * f.n + li];
+    } else {
+      o->topk[k] = -1;
+      o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = __builtin_nan("");
+    }
+  }
+  if (tid == 0) {
+    o->lb_best = i == kNoIndex ? -1 : i;
+    o->lb_best_val = i == kNoIndex ? __builtin_nan("") : v;
+  }
+}
 
+__device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch& sc) {
+  STAMP(3);
+  const int tid = threadIdx.x;
+  llampc_plan_out* o = f.out;
+  const bool lb = f.do_lb && f.full;
   double lav = __builtin_nan("");
   int64_t lai = kNoIndex;
   int nf = 0;
-  if (a.do_la) {
-    for (int b = tid; b < a.la_blocks; b += kBlock) {
-      nf += a.pnf[b];
-      if (a.pidx[b] == kNoIndex) continue;
-      if (less_nan_last(a.pv[b], a.pidx[b], lav, lai)) {
-        lav = a.pv[b];
-        lai = a.pidx[b];
+  if (f.do_la) {
+    for (int b = tid; b < f.nb_la; b += kBlock) {
+      nf += f.pnf[b];
+      const int64_t pi = f.pidx[b];
+      const double pv = f.pv[b];
+      if (pi != kNoIndex && less_nan_last(pv, pi, lav, lai)) {
+        lav = pv;
+        lai = pi;
       }
     }
-    block_min<0>(lav, lai, sv, si);
-    nf = block_sum(nf, sn);
-  }
-  __syncthreads();
-
-  if (tid != 0) return;
-  llampc_plan_out* o = a.out;
-  o->window_count = a.window_count;
-  o->window_full = a.full;
-  o->K = a.K;
-  o->lb_best = lbi;
-  o->lb_best_val = lbv;
-  o->n_nonfinite = nf;
-  o->reserved = 0;
-  const int64_t sel = lb && lbi >= 0 ? lbi : a.current_model;
-  const bool owned = sel >= a.goff && sel < a.goff + a.n;
-  o->sel_model = sel;
-  o->sel_owned = owned;
-  o->sel_cand = (owned && a.do_la) ? a.best_cand[sel - a.goff] : -1;
-  o->sel_cost = (owned && a.do_la) ? a.best_cost[sel - a.goff] : __builtin_nan("");
-  if (a.do_la && lai != kNoIndex) {
-    o->la_best_model = lai / a.C;
-    o->la_best_cand = (int32_t)(lai % a.C);
-    o->la_best_cost = lav;
-  } else {
-    o->la_best_model = -1;
-    o->la_best_cand = -1;
-    o->la_best_cost = __builtin_nan("");
-  }
-  for (int k = 0; k < LLAMPC_KMAX; ++k) {
-    const bool have = lb && k < a.K && s_top[k] != kNoIndex;
-    if (!have) {
-      o->topk[k] = -1;
-      o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = o->topk_cost[k] = __builtin_nan("");
-      o->topk_cand[k] = -1;
-      continue;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(lav, off, 64);
+      const int64_t oi = __shfl_xor(lai, off, 64);
+      nf += __shfl_xor(nf, off, 64);
+      if (less_nan_last(ov, oi, lav, lai)) {
+        lav = ov;
+        lai = oi;
+      }
     }
-    const int64_t gi = s_top[k], li = gi - a.goff;
-    o->topk[k] = gi;
-    o->topk_val[k] = s_topv[k];
-    o->topk_Df[k] = a.params[2 * a.n + li];
-    o->topk_Dr[k] = a.params[5 * a.n + li];
-    o->topk_cand[k] = a.do_la ? a.best_cand[li] : -1;
-    o->topk_cost[k] = a.do_la ? a.best_cost[li] : __builtin_nan("");
+    if ((tid & 63) == 0) {
+      sc.sv[4 + (tid >> 6)] = lav;
+      sc.si[4 + (tid >> 6)] = lai;
+      sc.sn[tid >> 6] = nf;
+    }
+    __syncthreads();
+    lav = sc.sv[4];
+    lai = sc.si[4];
+    nf = sc.sn[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) {
+      if (less_nan_last(sc.sv[4 + w], sc.si[4 + w], lav, lai)) {
+        lav = sc.sv[4 + w];
+        lai = sc.si[4 + w];
+      }
+      nf += sc.sn[w];
+    }
   }
+  STAMP(4);
+  if (tid < LLAMPC_KMAX) {
+    const int k = tid;
+    const int64_t id = lb ? o->topk[k] : -1;
+    if (!lb) {
+      o->topk[k] = -1;
+      o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = __builtin_nan("");
+    }
+    const bool have = lb && id >= 0 && f.do_la;
+    o->topk_cand[k] = have ? f.best_cand[id - f.goff] : -1;
+    o->topk_cost[k] = have ? f.best_cost[id - f.goff] : __builtin_nan("");
+  }
+  if (tid == 0) {
+    const int64_t lbi = lb ? o->lb_best : -1;
+    if (!lb) {
+      o->lb_best = -1;
+      o->lb_best_val = __builtin_nan("");
+    }
+    o->window_count = f.window_count;
+    o->window_full = f.full;
+    o->K = f.K;
+    o->n_nonfinite = nf;
+    o->reserved = 0;
+    const int64_t sel = lbi >= 0 ? lbi : f.current_model;
+    const bool owned = sel >= f.goff && sel < f.goff + f.n;
+    o->sel_model = sel;
+    o->sel_owned = owned;
+    o->sel_cand = (owned && f.do_la) ? f.best_cand[sel - f.goff] : -1;
+    o->sel_cost = (owned && f.do_la) ? f.best_cost[sel - f.goff] : __builtin_nan("");
+    if (f.do_la && lai != kNoIndex) {
+      o->la_best_model = lai / f.C;
+      o->la_best_cand = (int32_t)(lai % f.C);
+      o->la_best_cost = lav;
+    } else {
+      o->la_best_model = -1;
+      o->la_best_cand = -1;
+      o->la_best_cost = __builtin_nan("");
+    }
+    __hip_atomic_store(&f.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&f.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  STAMP(5);
+#ifdef LLAMPC_STAMPS
+  if (tid == 0) g_stamp_launch++;
+#endif
 }
 
-__global__ void merge_kernel(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
-                             llampc_plan_out* merged) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) merge_plan_parts(parts, G, nan_first, merged);
+// ------------------------------------------------------------------------------------
+// The tick: ONE launch.  Blocks [0, nb_lb) run the look-back, blocks [nb_lb, nb_lb+nb_la)
+// the look-ahead (the halves are independent: x_{t-1} -> x_t vs. rollouts from x_t).
+// Look-back blocks come first in dispatch order; the last of them merges the look-back
+// (lb_final) while look-ahead blocks still run; the last block overall completes the
+// llampc_plan_out record (final_select).
+// ------------------------------------------------------------------------------------
+template <int INTEG, bool STAGE, int LPM>
+__global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
+                                                      FinalLaunch fin, int G, int cpl) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Scratch sc(smem);
+  int* flag = reinterpret_cast<int*>(smem + 144);
+  if ((int)blockIdx.x < fin.nb_lb) {
+    lookback_block(lb, blockIdx.x, sc);
+    if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
+    if (fin.full) lb_final(fin, smem, sc);
+  } else {
+    lookahead_block<INTEG, STAGE, LPM>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
+  }
+  const unsigned expected = (unsigned)fin.nb_la + (fin.nb_lb > 0 ? 1u : 0u);
+  if (!ticket_last(&fin.tickets[1], expected, flag)) return;
+  final_select(fin, sc);
+}
+
+// Cross-shard merge after the all-gather: one wave.  Scalars by lane-parallel reads and
+// shuffles; the shards' sorted top-K lists by the LDS tree merge.  merge.hpp holds the
+// same semantics as straight-line host code (llampc_merge); the tests check both agree.
+__global__ __launch_bounds__(64) void merge_kernel(const llampc_plan_out* parts, int32_t G,
+                                                   int32_t nan_first, llampc_plan_out* m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int K = parts[0].K;
+  const int M = G * K;
+  Ent* buf0 = reinterpret_cast<Ent*>(smem);
+  Ent* buf1 = buf0 + M;
+  int64_t* sidx = reinterpret_cast<int64_t*>(buf1 + M);
+  for (int e = lane; e < M; e += 64) {
+    const int g = e / K, j = e - g * K;
+    const int64_t id = parts[g].topk[j] < 0 ? kNoIndex : parts[g].topk[j];
+    buf0[e] = Ent{id == kNoIndex ? __builtin_nan("") : parts[g].topk_val[j], id};
+    sidx[e] = id;
+  }
+  // look-back argmin over the shards' local argmins; look-ahead best; counts; owners
+  double bv = nan_first ? __builtin_inf() : __builtin_nan("");
+  int64_t bi = kNoIndex;
+  double av = __builtin_nan("");
+  int64_t am = kNoIndex;
+  int32_t ac = INT32_MAX;
+  int nf = 0;
+  for (int g = lane; g < G; g += 64) {
+    const llampc_plan_out& p = parts[g];
+    if (p.lb_best >= 0 && key_less(nan_first, p.lb_best_val, p.lb_best, bv, bi)) {
+      bv = p.lb_best_val;
+      bi = p.lb_best;
+    }
+    nf += p.n_nonfinite;
+    if (p.la_best_model >= 0 && la_less(p.la_best_cost, p.la_best_model, p.la_best_cand, av, am, ac)) {
+      av = p.la_best_cost;
+      am = p.la_best_model;
+      ac = p.la_best_cand;
+    }
+  }
+  if (nan_first) wave_min<1>(bv, bi);
+  else wave_min<0>(bv, bi);
+  int owner_lb = -1, owner_sel = -1;
+  for (int g = lane; g < G; g += 64) {
+    if (bi != kNoIndex && parts[g].lb_best == bi) owner_lb = g;
+    if (parts[g].sel_owned) owner_sel = g;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(av, off, 64);
+    const int64_t om = __shfl_xor(am, off, 64);
+    const int32_t oc = __shfl_xor(ac, off, 64);
+    if (la_less(ov, om, oc, av, am, ac)) {
+      av = ov;
+      am = om;
+      ac = oc;
+    }
+    nf += __shfl_xor(nf, off, 64);
+    owner_lb = max(owner_lb, __shfl_xor(owner_lb, off, 64));
+    owner_sel = max(owner_sel, __shfl_xor(owner_sel, off, 64));
+  }
+  __syncthreads();
+  const Ent* r = tree_merge(buf0, buf1, G, K);
+  if (lane < LLAMPC_KMAX) {
+    const int k = lane;
+    const int64_t id = k < K ? r[k].i : kNoIndex;
+    int src = -1;
+    if (id != kNoIndex)
+      for (int e = 0; e < M; ++e)
+        if (sidx[e] == id) {
+          src = e;
+          break;
+        }
+    if (src >= 0) {
+      const int g = src / K, j = src - g * K;
+      m->topk[k] = id;
+      m->topk_val[k] = r[k].v;
+      m->topk_Df[k] = parts[g].topk_Df[j];
+      m->topk_Dr[k] = parts[g].topk_Dr[j];
+      m->topk_cand[k] = parts[g].topk_cand[j];
+      m->topk_cost[k] = parts[g].topk_cost[j];
+    } else {
+      m->topk[k] = -1;
+      m->topk_val[k] = m->topk_Df[k] = m->topk_Dr[k] = m->topk_cost[k] =
+          k < K ? __builtin_nan("") : 0.0;
+      m->topk_cand[k] = -1;
+    }
+  }
+  if (lane != 0) return;
+  const llampc_plan_out& p0 = parts[0];
+  m->window_count = p0.window_count;
+  m->window_full = p0.window_full;
+  m->K = K;
+  m->reserved = 0;
+  m->lb_best = bi == kNoIndex ? -1 : bi;
+  m->lb_best_val = bi == kNoIndex ? __builtin_nan("") : bv;
+  if (m->window_full && owner_lb >= 0) {
+    m->sel_model = bi;
+    m->sel_owned = parts[owner_lb].sel_owned;
+    m->sel_cand = parts[owner_lb].sel_cand;
+    m->sel_cost = parts[owner_lb].sel_cost;
+  } else {
+    m->sel_model = p0.sel_model;
+    m->sel_owned = owner_sel >= 0;
+    m->sel_cand = owner_sel >= 0 ? parts[owner_sel].sel_cand : -1;
+    m->sel_cost = owner_sel >= 0 ? parts[owner_sel].sel_cost : __builtin_nan("");
+  }
+  m->la_best_model = am == kNoIndex ? -1 : am;
+  m->la_best_cand = am == kNoIndex ? -1 : ac;
+  m->la_best_cost = av;
+  m->n_nonfinite = nf;
 }
 
 // ------------------------------------------------------------------------------------
@@ -483,8 +771,26 @@ int lookahead_group(int32_t C) {
   return G;
 }
 
-int lookahead_blocks(int64_t n, int32_t C) {
-  const int mpb = kBlock / lookahead_group(C);
+// Lanes per rollout: split the transcendental chains over 4 (2) lanes while the launch is
+// latency-bound (few waves per SIMD); one lane per rollout once the chip is full.
+int lookahead_lpm(int64_t n, int32_t C, int32_t integrator) {
+  if (integrator == LLAMPC_RK6) return 1;
+  const int G = lookahead_group(C);
+  if (const char* e = getenv("LLAMPC_LPM")) {     // benchmarking override
+    int v = atoi(e);
+    if (v == 1 || v == 2 || v == 4) {
+      while (v > 1 && G * v > 64) v >>= 1;         // a model's lanes stay inside one wave
+      return v;
+    }
+  }
+  const int64_t lanes = n * G;
+  if (lanes <= 32768 && G <= 16) return 4;
+  if (lanes <= 131072 && G <= 32) return 2;
+  return 1;
+}
+
+int lookahead_blocks(int64_t n, int32_t C, int lpm) {
+  const int mpb = kBlock / (lookahead_group(C) * lpm);
   return (int)((n + mpb - 1) / mpb);
 }
 
@@ -497,44 +803,88 @@ size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u) {
   return *stage_u ? base + ub : base;
 }
 
-hipError_t launch_lookback(const LookbackLaunch& a, hipStream_t s) {
-  const int nb = lookback_blocks(a.n);
-  hipLaunchKernelGGL(lookback_kernel, dim3(nb), dim3(kBlock), 0, s, a);
-  return hipGetLastError();
+// Models per look-back lane: keep the block lists small enough for the in-LDS tree merge
+// (nb_lb * K <= 640 entries = 20 KB for both buffers).
+int lookback_r(int64_t n, int32_t K) {
+  const int64_t per = (int64_t)kBlock * 640 / std::max(1, K);   // models per list budget
+  return (int)std::max<int64_t>(1, (n + per - 1) / per);
 }
 
-template <int INTEG>
-static void launch_la_integ(const LookaheadLaunch& a, hipStream_t s, int nb, int G, int cpl,
-                            bool stage, size_t lds) {
-  if (stage)
-    hipLaunchKernelGGL((lookahead_kernel<INTEG, true>), dim3(nb), dim3(kBlock), lds, s, a, G, cpl);
-  else
-    hipLaunchKernelGGL((lookahead_kernel<INTEG, false>), dim3(nb), dim3(kBlock), lds, s, a, G, cpl);
+int lookback_blocks_r(int64_t n, int R) { return (int)((n + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R)); }
+
+template <int INTEG, bool STAGE, int LPM>
+static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
+                          int G, int cpl, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, LPM>), dim3(f.nb_lb + f.nb_la), dim3(kBlock), lds, s,
+                     lb, la, f, G, cpl);
 }
 
-hipError_t launch_lookahead(const LookaheadLaunch& a, hipStream_t s) {
-  const int G = lookahead_group(a.C);
-  const int cpl = (a.C + G - 1) / G;
-  const int nb = lookahead_blocks(a.n, a.C);
+template <int INTEG, bool STAGE>
+static void launch_plan_l(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
+                          int G, int cpl, int lpm, size_t lds, hipStream_t s) {
+  if (lpm == 4) launch_plan_t<INTEG, STAGE, 4>(lb, la, f, G, cpl, lds, s);
+  else if (lpm == 2) launch_plan_t<INTEG, STAGE, 2>(lb, la, f, G, cpl, lds, s);
+  else launch_plan_t<INTEG, STAGE, 1>(lb, la, f, G, cpl, lds, s);
+}
+
+hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
+                       hipStream_t s) {
+  LookbackLaunch lbv{};
+  LookaheadLaunch lav{};
+  int G = 1, cpl = 1, lpm = 1, integ = LLAMPC_RK4;
   bool stage = false;
-  const size_t lds = lookahead_lds_bytes(a.C, a.H, &stage);
-  switch (a.integrator) {
-    case LLAMPC_RK4: launch_la_integ<0>(a, s, nb, G, cpl, stage, lds); break;
-    case LLAMPC_EULER_NLP: launch_la_integ<1>(a, s, nb, G, cpl, stage, lds); break;
-    case LLAMPC_RK6: launch_la_integ<2>(a, s, nb, G, cpl, stage, lds); break;
+  size_t lds = kScratchBytes;
+  f.nb_lb = 0;
+  f.nb_la = 0;
+  if (lb) {
+    lbv = *lb;
+    lbv.R = lookback_r(lb->n, std::max(1, lb->K));
+    f.nb_lb = lookback_blocks_r(lb->n, lbv.R);
+    if (lb->full) lds = std::max(lds, kScratchBytes + 2 * (size_t)f.nb_lb * lb->K * sizeof(Ent));
+  }
+  if (la) {
+    lav = *la;
+    G = lookahead_group(la->C);
+    cpl = (la->C + G - 1) / G;
+    integ = la->integrator;
+    lpm = lookahead_lpm(la->n, la->C, integ);
+    f.nb_la = lookahead_blocks(la->n, la->C, lpm);
+    lds = std::max(lds, lookahead_lds_bytes(la->C, la->H, &stage));
+  }
+  f.do_lb = lb != nullptr;
+  f.do_la = la != nullptr;
+  if (f.nb_lb + f.nb_la == 0) return hipErrorInvalidValue;
+  switch (integ) {
+    case LLAMPC_RK4:
+      if (stage) launch_plan_l<0, true>(lbv, lav, f, G, cpl, lpm, lds, s);
+      else launch_plan_l<0, false>(lbv, lav, f, G, cpl, lpm, lds, s);
+      break;
+    case LLAMPC_EULER_NLP:
+      if (stage) launch_plan_l<1, true>(lbv, lav, f, G, cpl, lpm, lds, s);
+      else launch_plan_l<1, false>(lbv, lav, f, G, cpl, lpm, lds, s);
+      break;
+    case LLAMPC_RK6:
+      if (stage) launch_plan_t<2, true, 1>(lbv, lav, f, G, cpl, lds, s);
+      else launch_plan_t<2, false, 1>(lbv, lav, f, G, cpl, lds, s);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t launch_select(const SelectLaunch& a, hipStream_t s) {
-  hipLaunchKernelGGL(select_kernel, dim3(1), dim3(kBlock), 0, s, a);
-  return hipGetLastError();
+#ifdef LLAMPC_STAMPS
+extern "C" int llampc_debug_stamps(unsigned long long* out, unsigned* launches) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -2;
+  return hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_stamp_launch), sizeof(unsigned)) == hipSuccess ? 0 : -2;
 }
+#endif
 
 hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
                         llampc_plan_out* merged, hipStream_t s) {
-  hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(64), 0, s, parts, G, nan_first, merged);
+  if (G < 1 || G > 32) return hipErrorInvalidValue;   // LDS: 40 KB at G = 32
+  const size_t M = (size_t)G * LLAMPC_KMAX;      // K <= KMAX (read on device)
+  const size_t lds = 2 * M * sizeof(Ent) + M * sizeof(int64_t);
+  hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(64), lds, s, parts, G, nan_first, merged);
   return hipGetLastError();
 }
 

@@ -27,8 +27,9 @@ struct LookbackLaunch {
   double Ts;
   double* ring;          // [W][n]
   int32_t W, slot, full, K, nan_first;
+  int32_t R;             // models per lane (set by launch_plan)
   double* err_out;       // [n] or null
-  double* wmean_out;     // [n] or null
+  double* wm_buf;        // [n] window means (always written when the window is full)
   double* am_val;  int64_t* am_idx;   // [blocks]
   double* tk_val;  int64_t* tk_idx;   // [blocks][K]
 };
@@ -45,25 +46,28 @@ struct LookaheadLaunch {
   double* pv;  int64_t* pidx;  int32_t* pnf;  // [blocks]
 };
 
-struct SelectLaunch {
-  int32_t do_lb, full, window_count, K, nan_first, lb_blocks;
-  const double* am_val; const int64_t* am_idx; const double* tk_val; const int64_t* tk_idx;
-  int32_t do_la, la_blocks, C;
-  const double* pv; const int64_t* pidx; const int32_t* pnf;
-  const double* params; int64_t n, goff;
-  const int32_t* best_cand; const double* best_cost;
-  int64_t current_model;
+// What the ticket winners of the plan launch need (see plan_kernel).
+struct FinalLaunch {
   llampc_plan_out* out;
+  unsigned* tickets;                      // [2], zero between launches
+  int32_t do_lb, do_la, full, window_count, K, nan_first, nb_lb, nb_la, C;
+  int64_t current_model, n, goff;
+  const double* params;
+  const int32_t* best_cand; const double* best_cost;
+  const double* am_val; const int64_t* am_idx; const double* tk_val; const int64_t* tk_idx;
+  const double* pv; const int64_t* pidx; const int32_t* pnf;
 };
 
 int lookback_blocks(int64_t n);
 int lookahead_group(int32_t C);
-int lookahead_blocks(int64_t n, int32_t C);
+int lookahead_lpm(int64_t n, int32_t C, int32_t integrator);
+int lookahead_blocks(int64_t n, int32_t C, int lpm);
 size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u);
 
-hipError_t launch_lookback(const LookbackLaunch& a, hipStream_t s);
-hipError_t launch_lookahead(const LookaheadLaunch& a, hipStream_t s);
-hipError_t launch_select(const SelectLaunch& a, hipStream_t s);
+// The whole tick in ONE launch: look-back blocks (if lb), look-ahead blocks (if la), and
+// the completion stages run by ticket winners; writes f.out.  f.nb_* / f.do_* are set here.
+hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
+                       hipStream_t s);
 hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
                         llampc_plan_out* merged, hipStream_t s);
 hipError_t launch_dynamics(int32_t op, const double* x, const double* u, const double* params,

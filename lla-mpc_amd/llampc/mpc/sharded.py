@@ -59,7 +59,8 @@ class ShardedBank:
         self._torch = torch
         self.d_local = torch.empty(B, dtype=torch.uint8, device=dev)
         self.d_all = torch.empty(B * world, dtype=torch.uint8, device=dev)
-        self.d_merged = torch.empty(B, dtype=torch.uint8, device=dev)
+        # one shard: its record IS the result (no gather, no merge launch)
+        self.d_merged = torch.empty(B, dtype=torch.uint8, device=dev) if world > 1 else self.d_local
         self.h_merged = torch.empty(B, dtype=torch.uint8).pin_memory()
         self._inputs = None
 
@@ -111,11 +112,8 @@ class ShardedBank:
             import torch.distributed as dist
             with torch.cuda.stream(s):
                 dist.all_gather_into_tensor(self.d_all, self.d_local, group=self.group)
-            src, G = self.d_all, self.world
-        else:
-            src, G = self.d_local, 1
-        nat.check(lib.llampc_merge_device(src.data_ptr(), G, pin.nan_policy, self.d_merged.data_ptr(),
-                                          self.device, s.cuda_stream))
+            nat.check(lib.llampc_merge_device(self.d_all.data_ptr(), self.world, pin.nan_policy,
+                                              self.d_merged.data_ptr(), self.device, s.cuda_stream))
         return s
 
     def plan_device(self, staged: dict, stream=None, **kw):
