@@ -212,6 +212,14 @@ int llampc_integrate_batch(const double* x0, const double* u, int64_t u_stride_l
                            double* traj_out, int32_t final_only, int32_t device,
                            int32_t device_ptrs, void* stream);
 
+/* ---- model transcendentals (accuracy tests) -------------------------------------- */
+/* The fp64 atan2 (x >= 0) / atan / sin / cos the kernels use (csrc/fastmath.hpp),
+ * elementwise on host arrays: out[i] = f(a[i][, b[i]]). */
+enum llampc_math_fn { LLAMPC_MATH_ATAN2_XPOS = 0, LLAMPC_MATH_ATAN = 1, LLAMPC_MATH_SIN = 2,
+                      LLAMPC_MATH_COS = 3 };
+int llampc_math_batch(int32_t fn, const double* a, const double* b, int64_t n, double* out,
+                      int32_t device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -755,3 +755,25 @@ extern "C" int llampc_integrate_batch(const double* x0, const double* u, int64_t
   HIP_TRY(hipStreamSynchronize(w->stream));
   return LLAMPC_OK;
 }
+
+extern "C" int llampc_math_batch(int32_t fn, const double* a, const double* b, int64_t n,
+                                 double* out, int32_t device) {
+  if (!a || !out || (fn == LLAMPC_MATH_ATAN2_XPOS && !b)) return fail(LLAMPC_E_ARG, "NULL argument");
+  if (fn < LLAMPC_MATH_ATAN2_XPOS || fn > LLAMPC_MATH_COS) return fail(LLAMPC_E_ARG, "fn %d", fn);
+  if (n <= 0) return LLAMPC_OK;
+  int dev, rc;
+  if ((rc = resolve_device(device, &dev))) return rc;
+  DeviceGuard g(dev);
+  const size_t bn = align_up(n * 8);
+  Workspace* w;
+  std::lock_guard<std::mutex> lk(g_ws[dev].mu);
+  if ((rc = ws_get(dev, 3 * bn, &w))) return rc;
+  char* base = (char*)w->d;
+  double *da = (double*)base, *db = (double*)(base + bn), *dout = (double*)(base + 2 * bn);
+  HIP_TRY(hipMemcpyAsync(da, a, n * 8, hipMemcpyHostToDevice, w->stream));
+  if (b) HIP_TRY(hipMemcpyAsync(db, b, n * 8, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(launch_math(fn, da, db, n, dout, w->stream));
+  HIP_TRY(hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, w->stream));
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  return LLAMPC_OK;
+}

@@ -13,6 +13,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fastmath.hpp"
+
+// Transcendentals of the model: the short-chain versions (fastmath.hpp) by default;
+// -DLLAMPC_OCML_MATH selects ocml's for A/B measurements.
+#ifdef LLAMPC_OCML_MATH
+#define LL_ATAN2P(y, x) atan2((y), (x))
+#define LL_ATAN(z) atan(z)
+#define LL_SIN(a) sin(a)
+#define LL_SINCOS(a, s, c) sincos((a), (s), (c))
+#else
+#define LL_ATAN2P(y, x) ::llampc::fm::atan2_xpos((y), (x))
+#define LL_ATAN(z) ::llampc::fm::atan_(z)
+#define LL_SIN(a) ::llampc::fm::sin_(a)
+#define LL_SINCOS(a, s, c) ::llampc::fm::sincos_((a), (s), (c))
+#endif
+
 namespace llampc {
 
 // Per-bank constants in kernel-argument space (wave-uniform → SGPRs).
@@ -50,10 +66,10 @@ __device__ __host__ __forceinline__ Forces forces(const VehK& v, const Tire& t, 
                       : (v.Cm1 - v.Cm2 * vx) * pwm - v.Cr0 - v.Cr2 * (vx * vx);  // :146
   // Ref form: atan2(., |vx|) (dynamic.py:149-150); NLP form: atan2(., vx) (:215-216)
   const double den = (F == Form::Ref) ? fabs(vx) : vx;
-  f.af = delta - atan2(v.lf * om + vy, den);
-  f.ar = atan2(v.lr * om - vy, den);
-  f.Ffy = t.Df * sin(t.Cf * atan(t.Bf * f.af));                      // dynamic.py:151
-  f.Fry = t.Dr * sin(t.Cr * atan(t.Br * f.ar));                      // dynamic.py:152
+  f.af = delta - LL_ATAN2P(v.lf * om + vy, den);
+  f.ar = LL_ATAN2P(v.lr * om - vy, den);
+  f.Ffy = t.Df * LL_SIN(t.Cf * LL_ATAN(t.Bf * f.af));                // dynamic.py:151
+  f.Fry = t.Dr * LL_SIN(t.Cr * LL_ATAN(t.Br * f.ar));                // dynamic.py:152
   return f;
 }
 
@@ -66,7 +82,7 @@ __device__ __host__ __forceinline__ Input make_input(double a, double d) {
   Input u;
   u.a = a;
   u.d = d;
-  sincos(d, &u.sd, &u.cd);
+  LL_SINCOS(d, &u.sd, &u.cd);
   return u;
 }
 
@@ -89,7 +105,7 @@ __device__ __host__ __forceinline__ void rhs(const VehK& v, const Tire& t, const
   }
   const Forces f = forces<F>(v, t, vx, vy, om, u.a, d);
   double sp, cp;
-  sincos(x[2], &sp, &cp);
+  LL_SINCOS(x[2], &sp, &cp);
   dx[0] = vx * cp - vy * sp;
   dx[1] = vx * sp + vy * cp;
   dx[2] = om;
@@ -235,21 +251,21 @@ __device__ __forceinline__ void rhs_split(const VehK& v, const Tire& t, const do
   const bool front = (LPM == 2) ? (sub == 0) : (sub == 1);
   const double den = (F == Form::Ref) ? fabs(vx) : vx;
   const double yy = front ? (v.lf * om + vy) : (v.lr * om - vy);
-  const double a2 = atan2(yy, den);
+  const double a2 = LL_ATAN2P(yy, den);
   const double slip = front ? (d - a2) : a2;
   const double B = front ? t.Bf : t.Br, Cc = front ? t.Cf : t.Cr, D = front ? t.Df : t.Dr;
-  double arg = Cc * atan(B * slip);
+  double arg = Cc * LL_ATAN(B * slip);
   double Ffy, Fry, sp, cp;
   if (LPM == 2) {
-    const double r = D * sin(arg);
+    const double r = D * LL_SIN(arg);
     Ffy = dpp_bcast<kPair0>(r);
     Fry = dpp_bcast<kPair1>(r);
-    sincos(x[2], &sp, &cp);
+    LL_SINCOS(x[2], &sp, &cp);
   } else {
     const bool psi_lane = (sub == 0) | (sub == 3);
     arg = psi_lane ? x[2] : arg;
     double s, c;
-    sincos(arg, &s, &c);
+    LL_SINCOS(arg, &s, &c);
     const double r = (sub == 3) ? c : (psi_lane ? s : D * s);
     sp = dpp_bcast<kQuad0>(r);
     Ffy = dpp_bcast<kQuad1>(r);

@@ -76,6 +76,11 @@ __device__ __forceinline__ int block_sum(int x, int32_t* sn) {
   return s;
 }
 
+// Keep a wave-uniform value in a VGPR: the rollout loop needs ~25 uniform vehicle/cost
+// constants; left in SGPRs they overflow the 102-SGPR budget together with the
+// polynomial constants and get spilled to VGPR lanes (v_readlane reloads in the loop).
+__device__ __forceinline__ void pin_vgpr(double& x) { asm volatile("" : "+v"(x)); }
+
 __device__ __forceinline__ Tire load_tire(const double* p, int64_t ld, int64_t i) {
   Tire t;
   t.Bf = p[i];
@@ -295,7 +300,29 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   const int g = cl & (G - 1);
   const int64_t n = (int64_t)blk * (kBlock / (G * LPM)) + cl / G;
   const bool live = n < a.n;
-  const CostK& q = a.cost;
+  CostK q = a.cost;
+  VehK veh = a.veh;
+  double Ts = a.Ts;
+  for (int m = 0; m < 4; ++m) {
+    pin_vgpr(q.Q[m]);
+    pin_vgpr(q.R[m]);
+    pin_vgpr(q.P[m]);
+  }
+  for (int m = 0; m < 2; ++m) {
+    pin_vgpr(q.umin[m]);
+    pin_vgpr(q.umax[m]);
+    pin_vgpr(q.dmax[m]);
+  }
+  pin_vgpr(veh.lf);
+  pin_vgpr(veh.lr);
+  pin_vgpr(veh.mass);
+  pin_vgpr(veh.inv_mass);
+  pin_vgpr(veh.inv_Iz);
+  pin_vgpr(veh.Cm1);
+  pin_vgpr(veh.Cm2);
+  pin_vgpr(veh.Cr0);
+  pin_vgpr(veh.Cr2);
+  pin_vgpr(Ts);
   const double up0 = a.uprev[0], up1 = a.uprev[1];
 
   double bv = __builtin_nan("");
@@ -329,7 +356,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
           if (q.dmax[1] >= 0) feas = feas && d1 <= q.dmax[1] && -d1 <= q.dmax[1];
         }
         const Input u = make_input(ua, ud);
-        step_split<INTEG, LPM>(a.veh, t, x, u, a.Ts, sub);
+        step_split<INTEG, LPM>(veh, t, x, u, Ts, sub);
         const double e0 = x[0] - sx[2 * (k + 1)], e1 = x[1] - sx[2 * (k + 1) + 1];
         track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
         act = act + (d0 * (q.R[0] * d0 + q.R[1] * d1) + d1 * (q.R[2] * d0 + q.R[3] * d1));
@@ -730,6 +757,22 @@ __global__ __launch_bounds__(kBlock) void dynamics_kernel(int32_t op, const doub
   }
 }
 
+// Elementwise transcendentals of the model (accuracy tests of fastmath.hpp).
+__global__ __launch_bounds__(kBlock) void math_kernel(int32_t fn, const double* a, const double* b,
+                                                      int64_t n, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  double r = 0.0, s, c;
+  switch (fn) {
+    case 0: r = LL_ATAN2P(a[i], b[i]); break;
+    case 1: r = LL_ATAN(a[i]); break;
+    case 2: LL_SINCOS(a[i], &s, &c); r = s; break;
+    case 3: LL_SINCOS(a[i], &s, &c); r = c; break;
+    default: r = __builtin_nan("");
+  }
+  out[i] = r;
+}
+
 template <int INTEG>
 __global__ __launch_bounds__(kBlock) void integrate_kernel(const double* x0, const double* u,
                                                            int64_t us, const double* h, int32_t S,
@@ -892,6 +935,13 @@ hipError_t launch_dynamics(int32_t op, const double* x, const double* u, const d
                            int64_t P, VehK veh, int64_t n, double* out, hipStream_t s) {
   const int nb = (int)((n + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(dynamics_kernel, dim3(nb), dim3(kBlock), 0, s, op, x, u, params, P, veh, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_math(int32_t fn, const double* a, const double* b, int64_t n, double* out,
+                       hipStream_t s) {
+  const int nb = (int)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(math_kernel, dim3(nb), dim3(kBlock), 0, s, fn, a, b, n, out);
   return hipGetLastError();
 }
 

@@ -72,6 +72,8 @@ hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_fir
                         llampc_plan_out* merged, hipStream_t s);
 hipError_t launch_dynamics(int32_t op, const double* x, const double* u, const double* params,
                            int64_t P, VehK veh, int64_t n, double* out, hipStream_t s);
+hipError_t launch_math(int32_t fn, const double* a, const double* b, int64_t n, double* out,
+                       hipStream_t s);
 hipError_t launch_integrate(const double* x0, const double* u, int64_t u_stride_lane,
                             const double* h, int32_t S, const double* params, int64_t P,
                             VehK veh, int64_t n, int32_t integrator, double* traj,

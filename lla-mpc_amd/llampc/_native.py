@@ -97,6 +97,7 @@ _SIGNATURES = {
     "llampc_dynamics_batch": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                         C.POINTER(Vehicle), C.c_int64, C.c_void_p, C.c_int32,
                                         C.c_int32, C.c_void_p]),
+    "llampc_math_batch": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]),
     "llampc_integrate_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32,
                                          C.c_void_p, C.c_int64, C.POINTER(Vehicle), C.c_int64,
                                          C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,

@@ -396,3 +396,41 @@ def test_baseline_sizes_properties(nat, N, H, track):
         cref = O.mpc_cost(traj, U, xref, u[:, W], np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2)))
         close(res.costs.ravel(), cref, RTOL_ROLL)
         assert res.global_best[0] == int(np.argmin(np.where(np.isnan(cref), np.inf, cref)))
+
+
+# ----------------------------------------------------------------- model transcendentals
+def _math(nat, fn, a, b=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    bb = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+    out = np.empty_like(a)
+    nat.check(nat.load().llampc_math_batch(fn, a.ctypes.data, None if bb is None else bb.ctypes.data,
+                                           a.size, out.ctypes.data, 0))
+    return out
+
+
+def _ulp(got, want):
+    fin = np.isfinite(want)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_array_equal(got[~fin], want[~fin])
+    return np.max(np.abs(got[fin] - want[fin]) / np.spacing(np.maximum(np.abs(want[fin]), 1e-300)))
+
+
+def test_fast_transcendentals_ulp_vs_libm(nat):
+    """csrc/fastmath.hpp vs NumPy (libm): <= 4 ulp over the model's argument ranges and
+    wide random ranges; C99 special cases exactly."""
+    rng = np.random.RandomState(0)
+    n = 1 << 20
+    y = np.concatenate([rng.uniform(-3, 3, n), rng.standard_cauchy(n), [0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 5.0, 0.0]])
+    x = np.concatenate([rng.uniform(0, 4, n), np.abs(rng.standard_cauchy(n)), [0.0, 0.0, 0.0, 0.0, np.inf, np.inf, 1.0, np.inf, 3.0]])
+    assert _ulp(_math(nat, 0, y, x), np.arctan2(y, x)) <= 4
+    z = np.concatenate([rng.uniform(-2, 2, n), rng.standard_cauchy(n) * 10, [0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e300, 1e-300]])
+    assert _ulp(_math(nat, 1, z), np.arctan(z)) <= 4
+    a = np.concatenate([rng.uniform(-4, 4, n), rng.uniform(-300, 300, n), rng.uniform(-3e6, 3e6, 1000),
+                        [0.0, -0.0, np.pi / 2, np.pi, 1e-300, np.inf, -np.inf, np.nan, 1e20]])
+    s, c = _math(nat, 2, a), _math(nat, 3, a)
+    # absolute error near the zeros of sin/cos (reduction), relative elsewhere
+    for got, want in ((s, np.sin(a)), (c, np.cos(a))):
+        fin = np.isfinite(want)
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+        err = np.abs(got[fin] - want[fin])
+        assert np.all(err <= 4 * np.spacing(np.maximum(np.abs(want[fin]), 1e-16))), err.max()
