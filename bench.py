@@ -290,16 +290,9 @@ def lpm_of(n, C):
     while G < C and G < 64:
         G <<= 1
     env = os.environ.get("LLAMPC_LPM")
-    if env in ("1", "2", "4"):
-        v = int(env)
-        while v > 1 and G * v > 64:
-            v >>= 1
-        return v
-    if n * G <= 32768 and G <= 16:
-        return 4
-    if n * G <= 131072 and G <= 32:
-        return 2
-    return 1
+    if env == "1" or (env == "2" and G <= 32):
+        return int(env)
+    return 2 if (n * G <= 32768 and G <= 32) else 1
 
 
 def pmc_traffic(args):

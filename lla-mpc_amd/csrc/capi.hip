@@ -381,7 +381,7 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
     return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
   b->own_stream = true;
   const int lbb = lookback_blocks(n);
-  const int lab = lookahead_blocks(n, 64, 1);   // worst case: one model per wave
+  const int64_t lab = n;                 // worst case: one model per block (wave-role, G=64)
   if ((rc = dev_alloc(&b->d_params, 6 * (size_t)n)) || (rc = dev_alloc(&b->d_ring, (size_t)W * n)) ||
       (rc = dev_alloc(&b->d_am_val, lbb)) || (rc = dev_alloc(&b->d_am_idx, lbb)) ||
       (rc = dev_alloc(&b->d_tk_val, (size_t)lbb * LLAMPC_KMAX)) ||

@@ -28,6 +28,18 @@
 #define LL_SIN(a) ::llampc::fm::sin_(a)
 #define LL_SINCOS(a, s, c) ::llampc::fm::sincos_((a), (s), (c))
 #endif
+// Estrin (short-chain) variants for the latency-bound split kernels.
+#ifdef LLAMPC_OCML_MATH
+#define LL_ATAN2P_E(y, x) atan2((y), (x))
+#define LL_ATAN_E(z) atan(z)
+#define LL_SIN_E(a) sin(a)
+#define LL_SINCOS_E(a, s, c) sincos((a), (s), (c))
+#else
+#define LL_ATAN2P_E(y, x) ::llampc::fm::atan2_xpos<true>((y), (x))
+#define LL_ATAN_E(z) ::llampc::fm::atan_<true>(z)
+#define LL_SIN_E(a) ::llampc::fm::sin_<true>(a)
+#define LL_SINCOS_E(a, s, c) ::llampc::fm::sincos_<true>((a), (s), (c))
+#endif
 
 namespace llampc {
 
@@ -142,7 +154,7 @@ __device__ __host__ __forceinline__ void rk4_step(const VehK& v, const Tire& t, 
   }
   rhs<Form::Ref>(v, t, y, u, d);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) x[i] = x[i] + (acc[i] + h * d[i]) / 6;
+  for (int i = 0; i < 6; ++i) x[i] = x[i] + fm::div6(acc[i] + h * d[i]);
 }
 
 // x_{k+1} = x_k + Ts * f_nlp(x_k, u_k)  (nmpc.py:58-60 equality constraints).
@@ -207,15 +219,18 @@ __device__ __host__ __forceinline__ void step(const VehK& v, const Tire& t, doub
 }
 
 // ------------------------------------------------------------------------------------
-// Lane-split evaluation (latency regime).  LPM lanes (a pair or a quad of consecutive
-// lanes) carry the SAME state; each lane runs ONE transcendental chain of the stage with
-// an identical instruction stream (lane-dependent operands via selects, no divergence),
-// and the results are exchanged with DPP quad_perm broadcasts:
-//   LPM=2: lane 0 front tire   atan2 -> atan -> sin -> Ffy   (+ sincos(psi) in both)
-//          lane 1 rear tire    atan2 -> atan -> sin -> Fry
-//   LPM=4: lane 0 sin(psi), lane 1 Ffy, lane 2 Fry, lane 3 cos(psi): one
-//          atan2 -> atan -> sincos chain per lane (lanes 0/3 discard their atan results)
-// Every lane then forms dx/dt and the integrator update redundantly (cheap, identical).
+// Rollout stage of the look-ahead (the hot loop).  One stage of odeintRK4_batch
+// (rk6.py:58-66) is dx/dt of dynamic.py:98-115 (Ref) / :195-226 (Nlp); its cost is two
+// serial transcendental chains — front and rear tire, atan2 -> atan -> sin — plus
+// sincos(psi).  With ~1 wave per SIMD a wave pays for every instruction it issues and for
+// every branch/select latency on its chains (tools/micro), so this path
+//  * evaluates each chain with the branch-free cores of fastmath.hpp and re-does the rare
+//    lanes whose operands leave the cores' domains with the general rhs<F>, behind ONE
+//    wave-uniform branch per stage that is normally not taken.  Which cores a lane used
+//    depends only on its own operands, never on the other rollouts sharing the wave;
+//  * LPM = 2 splits the two chains over a lane pair (lane 0 front, lane 1 rear; exchanged
+//    with DPP) — the latency regime, fewer waves than SIMDs; LPM = 1 runs both chains in
+//    one lane — the throughput regime (fewest instructions per rollout).
 // ------------------------------------------------------------------------------------
 template <int CTRL>
 __device__ __forceinline__ double dpp_bcast(double v) {
@@ -223,108 +238,154 @@ __device__ __forceinline__ double dpp_bcast(double v) {
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
-// quad_perm encodings: broadcast lane k of each quad = k * 0x55; pairs [0,0,2,2] = 0xA0,
-// [1,1,3,3] = 0xF5.
-constexpr int kQuad0 = 0x00, kQuad1 = 0x55, kQuad2 = 0xAA, kQuad3 = 0xFF;
+// quad_perm broadcasts within lane pairs: [0,0,2,2] = 0xA0, [1,1,3,3] = 0xF5.
 constexpr int kPair0 = 0xA0, kPair1 = 0xF5;
 
+// One tire's constants in this lane: front (lw = lf, sg = +1) or rear (lw = lr, sg = -1).
+struct Chain {
+  double lw, sg, B, C, D;
+};
+
+__device__ __host__ __forceinline__ Chain make_chain(const VehK& v, const Tire& t, bool front) {
+  return front ? Chain{v.lf, 1.0, t.Bf, t.Cf, t.Df} : Chain{v.lr, -1.0, t.Br, t.Cr, t.Dr};
+}
+
+// Static part of the fast chain's domain: |C atan(.)| <= |C| pi/2 must stay inside
+// sin_wide's |a| <= 3 (|C| <= 1.9 -> 2.985; NaN -> false).
+__device__ __host__ __forceinline__ bool chain_static_ok(const Chain& c) { return fabs(c.C) <= 1.9; }
+
+// F = D sin(C atan(B slip)) with slip = dsel - atan2(yy, den) for the front tire
+// (dsel = delta) and atan2(yy, den) for the rear (dsel = 0); yy = lf om + vy | lr om - vy
+// (dynamic.py:149-152 / :215-220).  `ok` &= the lane's dynamic domain.
+__device__ __forceinline__ double chain_fast(const Chain& c, double den, double vy, double om,
+                                             double dsel, bool& ok, const fm::FmK& K) {
+  const double yy = fma(c.lw, om, c.sg * vy);
+  const double a2 = fm::atan2_fast(yy, den, K);
+  const double z = c.B * fma(-c.sg, a2, dsel);
+  ok = ok && fm::atan2_fast_ok(yy, den) && fm::atan_fast_ok(z);
+  return c.D * fm::sin_wide(c.C * fm::atan_fast(z, K), K);
+}
+
+// Per-rollout constants of the fast stage.  ch[0] is this lane's chain (LPM = 2) or the
+// front chain and ch[1] the rear (LPM = 1); fw = 1 for a front lane, 0 for a rear lane;
+// sok = the static domain (chain_static_ok of the lane's chains).
+struct StageK {
+  Chain ch[2];
+  double fw;
+  bool sok;
+};
+
+template <int LPM>
+__device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int sub) {
+  const bool front = (LPM == 1) || sub == 0;
+  StageK s;
+  s.ch[0] = make_chain(v, t, front);
+  s.ch[1] = make_chain(v, t, false);
+  s.fw = front ? 1.0 : 0.0;
+  s.sok = chain_static_ok(s.ch[0]) && ((LPM == 2) || chain_static_ok(s.ch[1]));
+  return s;
+}
+
+// dx/dt on the fast path, falling back to the general rhs<F> for out-of-domain lanes.
 template <Form F, int LPM>
-__device__ __forceinline__ void rhs_split(const VehK& v, const Tire& t, const double* x,
-                                          const Input& u, double* dx, int sub) {
-  if (LPM == 1 || v.approx) {           // wave-uniform: no transcendental chains to split
-    rhs<F>(v, t, x, u, dx);
-    return;
-  }
+__device__ __forceinline__ void rhs_fast(const VehK& v, const Tire& t, const StageK& sk,
+                                         const double* x, const Input& u, double* dx,
+                                         const fm::FmK& K) {
   double vx = x[3], vy = x[4], om = x[5];
   double d = u.d, sd = u.sd, cd = u.cd;
-  if (F == Form::Nlp) {
-    const double vmin = 0.05;
-    if (vx < vmin) {                    // same state in every lane of the group: uniform per group
-      vy = 0.0;
-      om = 0.0;
-      d = 0.0;
-      sd = 0.0;
-      cd = 1.0;
-      vx = vmin;
-    }
+  if (F == Form::Nlp && vx < 0.05) {      // dynamic.py:208-212 (vmin clamp)
+    vy = 0.0;
+    om = 0.0;
+    d = 0.0;
+    sd = 0.0;
+    cd = 1.0;
+    vx = 0.05;
   }
-  const bool front = (LPM == 2) ? (sub == 0) : (sub == 1);
   const double den = (F == Form::Ref) ? fabs(vx) : vx;
-  const double yy = front ? (v.lf * om + vy) : (v.lr * om - vy);
-  const double a2 = LL_ATAN2P(yy, den);
-  const double slip = front ? (d - a2) : a2;
-  const double B = front ? t.Bf : t.Br, Cc = front ? t.Cf : t.Cr, D = front ? t.Df : t.Dr;
-  double arg = Cc * LL_ATAN(B * slip);
-  double Ffy, Fry, sp, cp;
+  bool ok = sk.sok && !v.approx && fm::sincos_fast_ok(x[2]);
+  double Ffy, Fry;
   if (LPM == 2) {
-    const double r = D * LL_SIN(arg);
+    const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, ok, K);
     Ffy = dpp_bcast<kPair0>(r);
     Fry = dpp_bcast<kPair1>(r);
-    LL_SINCOS(x[2], &sp, &cp);
+    const int oi = ok;                    // the pair shares one state: both or neither
+    ok = __builtin_amdgcn_mov_dpp(oi, kPair0, 0xF, 0xF, false) &
+         __builtin_amdgcn_mov_dpp(oi, kPair1, 0xF, 0xF, false);
   } else {
-    const bool psi_lane = (sub == 0) | (sub == 3);
-    arg = psi_lane ? x[2] : arg;
-    double s, c;
-    LL_SINCOS(arg, &s, &c);
-    const double r = (sub == 3) ? c : (psi_lane ? s : D * s);
-    sp = dpp_bcast<kQuad0>(r);
-    Ffy = dpp_bcast<kQuad1>(r);
-    Fry = dpp_bcast<kQuad2>(r);
-    cp = dpp_bcast<kQuad3>(r);
+    Ffy = chain_fast(sk.ch[0], den, vy, om, d, ok, K);
+    Fry = chain_fast(sk.ch[1], den, vy, om, 0.0, ok, K);
   }
-  const double Frx = v.input_acc ? v.mass * u.a : (v.Cm1 - v.Cm2 * vx) * u.a - v.Cr0 - v.Cr2 * (vx * vx);
+  double sp, cp;
+  fm::sincos_fast(x[2], &sp, &cp, K);
+  const double Frx = v.input_acc ? v.mass * u.a
+                                 : (v.Cm1 - v.Cm2 * vx) * u.a - v.Cr0 - v.Cr2 * (vx * vx);
   dx[0] = vx * cp - vy * sp;
   dx[1] = vx * sp + vy * cp;
   dx[2] = om;
   dx[3] = v.inv_mass * (Frx - Ffy * sd) + vy * om;
   dx[4] = v.inv_mass * (Fry + Ffy * cd) - vx * om;
   dx[5] = v.inv_Iz * (Ffy * v.lf * cd - Fry * v.lr);
+  // Out-of-domain lanes (and linear-tire banks): the general evaluation.  One copy per
+  // kernel (the stage loop below is not unrolled), normally skipped wave-uniformly.
+  if (__builtin_expect(__any(!ok), 0)) {
+    if (!ok) rhs<F>(v, t, x, u, dx);
+  }
 }
 
-template <int LPM>
-__device__ __forceinline__ void rk4_step_split(const VehK& v, const Tire& t, double* x,
-                                               const Input& u, double h, int sub) {
-  double y[6], d[6], acc[6];
-  rhs_split<Form::Ref, LPM>(v, t, x, u, d, sub);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const double k = h * d[i];
-    acc[i] = k;
-    y[i] = x[i] + k / 2;
+__device__ __forceinline__ Input make_input_fast(double a, double d, const fm::FmK& K) {
+  Input u;
+  u.a = a;
+  u.d = d;
+  fm::sincos_fast(d, &u.sd, &u.cd, K);
+  const bool ok = fm::sincos_fast_ok(d);
+  if (__builtin_expect(__any(!ok), 0)) {
+    if (!ok) LL_SINCOS(d, &u.sd, &u.cd);
   }
-  rhs_split<Form::Ref, LPM>(v, t, y, u, d, sub);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const double k = h * d[i];
-    acc[i] = acc[i] + 2 * k;
-    y[i] = x[i] + k / 2;
-  }
-  rhs_split<Form::Ref, LPM>(v, t, y, u, d, sub);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const double k = h * d[i];
-    acc[i] = acc[i] + 2 * k;
-    y[i] = x[i] + k;
-  }
-  rhs_split<Form::Ref, LPM>(v, t, y, u, d, sub);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) x[i] = x[i] + (acc[i] + h * d[i]) / 6;
+  return u;
 }
 
+// One look-ahead step on the fast path.
+//  RK4 (rk6.py:58-66): the four stages as a (not unrolled) loop over ONE rhs_fast, with
+//    the stage combinations as FMAs by per-stage weights — the same roundings as rk4_step:
+//    acc = k | acc + 2k (fma(w, k, acc * wb), wb in {0, 1}), y = x + k/2 | x + k
+//    (fma(c, k, x), c in {1/2, 1}); the final sum divided by 6 through fm::div6
+//    (correctly rounded, = x / 6.0).
+//  NLP Euler (nmpc.py:58-60): x + Ts f_nlp(x, u).
+//  RK6 (rk6.py:13-28): the general rk6_step, one lane per rollout (LPM must be 1).
 template <int INTEG, int LPM>
-__device__ __forceinline__ void step_split(const VehK& v, const Tire& t, double* x,
-                                           const Input& u, double h, int sub) {
-  if (LPM == 1) {
-    step<INTEG>(v, t, x, u, h);
-  } else if (INTEG == 0) {
-    rk4_step_split<LPM>(v, t, x, u, h, sub);
+__device__ __forceinline__ void step_fast(const VehK& v, const Tire& t, const StageK& sk,
+                                          double* x, const Input& u, double h,
+                                          const fm::FmK& K) {
+  if (INTEG == 0) {
+    double y[6], d[6], acc[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      y[i] = x[i];
+      acc[i] = 0.0;
+    }
+#pragma unroll 1
+    for (int st = 0;; ++st) {
+      rhs_fast<Form::Ref, LPM>(v, t, sk, y, u, d, K);
+      if (st == 3) break;
+      const double w = st == 0 ? 1.0 : 2.0, wb = st == 0 ? 0.0 : 1.0;
+      const double c = st == 2 ? 1.0 : 0.5;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double k = h * d[i];
+        acc[i] = fma(w, k, acc[i] * wb);
+        y[i] = fma(c, k, x[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = x[i] + fm::div6(acc[i] + h * d[i], K);
   } else if (INTEG == 1) {
     double d[6];
-    rhs_split<Form::Nlp, LPM>(v, t, x, u, d, sub);
+    rhs_fast<Form::Nlp, LPM>(v, t, sk, x, u, d, K);
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = x[i] + h * d[i];
   } else {
-    step<INTEG>(v, t, x, u, h);        // RK6 (plant) stays one lane per rollout
+    static_assert(INTEG != 2 || LPM == 1, "RK6 look-ahead runs one lane per rollout");
+    rk6_step(v, t, x, u, h);
   }
 }
 

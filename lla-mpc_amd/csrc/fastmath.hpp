@@ -47,20 +47,36 @@ constexpr double kTwoOverPi = 0.6366197723675814, kPio2 = 1.5707963267948966,
 constexpr double kPio2Tail = 6.123233995736766e-17;   // pi/2 - (double)(pi/2)
 constexpr double kSinCosMax = 1647099.3291652855;      // 2^20 * pi/2
 
-// The kernels are VALU-issue-bound (rocprofv3: ~1 fp64 instruction per 4 cycles, few
-// dependency stalls), so the cores use Horner (one SGPR constant per v_fmac, no moves)
-// rather than Estrin.
+// Two evaluation schemes for every polynomial core:
+//   EST = false  Horner: one SGPR constant per v_fmac, fewest instructions — for the
+//                issue-bound one-lane-per-rollout kernels (many waves per SIMD);
+//   EST = true   Estrin: dependency depth ~log2(terms) — for the lane/wave-split kernels
+//                where ONE dependent chain per wave bounds the stage (latency-bound).
+template <bool EST>
 __device__ __host__ __forceinline__ double atan_q(double s) {
-  double p = kAtanQ[21];
+  const double* c = kAtanQ;
+  if (!EST) {
+    double p = c[21];
 #pragma unroll
-  for (int i = 20; i >= 0; --i) p = fma(p, s, kAtanQ[i]);
-  return p;
+    for (int i = 20; i >= 0; --i) p = fma(p, s, c[i]);
+    return p;
+  }
+  const double s2 = s * s, s4 = s2 * s2, s8 = s4 * s4, s16 = s8 * s8;
+  const double p0 = fma(c[1], s, c[0]), p1 = fma(c[3], s, c[2]), p2 = fma(c[5], s, c[4]),
+               p3 = fma(c[7], s, c[6]), p4 = fma(c[9], s, c[8]), p5 = fma(c[11], s, c[10]),
+               p6 = fma(c[13], s, c[12]), p7 = fma(c[15], s, c[14]), p8 = fma(c[17], s, c[16]),
+               p9 = fma(c[19], s, c[18]), p10 = fma(c[21], s, c[20]);
+  const double q0 = fma(p1, s2, p0), q1 = fma(p3, s2, p2), q2 = fma(p5, s2, p4),
+               q3 = fma(p7, s2, p6), q4 = fma(p9, s2, p8);
+  const double r0 = fma(q1, s4, q0), r1 = fma(q3, s4, q2), r2 = fma(p10, s4, q4);
+  return fma(r2, s16, fma(r1, s8, r0));
 }
 
 // atan(t) for |t| <= 1.
+template <bool EST>
 __device__ __host__ __forceinline__ double atan_core(double t) {
   const double s = t * t;
-  return fma(t * s, atan_q(s), t);
+  return fma(t * s, atan_q<EST>(s), t);
 }
 
 // num / den by reciprocal + two Newton steps + one residual correction (8 VALU instead of
@@ -84,10 +100,11 @@ __device__ __host__ __forceinline__ double div_(double num, double den) {
 
 // atan2(y, x) for x >= +0 (or NaN): one division, no quadrant branches.  Special cases
 // follow C99 atan2 for x >= 0: (+-0, +0) -> +-0, (+-inf, +inf) -> +-pi/4.
+template <bool EST = false>
 __device__ __host__ __forceinline__ double atan2_xpos(double y, double x) {
   const bool swap = fabs(y) > x;
   const double num = swap ? x : y, den = swap ? y : x;
-  const double r = atan_core(div_(num, den));
+  const double r = atan_core<EST>(div_(num, den));
   double out = swap ? (copysign(kPio2, y) - r) + copysign(kPio2Tail, y) : r;
   if (x == 0.0 && y == 0.0) out = y;
   if (isinf(x) && isinf(y)) out = copysign(kPio4, y);
@@ -95,34 +112,45 @@ __device__ __host__ __forceinline__ double atan2_xpos(double y, double x) {
 }
 
 // atan(z): the division only when some |z| > 1.
+template <bool EST = false>
 __device__ __host__ __forceinline__ double atan_(double z) {
   const bool swap = fabs(z) > 1.0;
   double t = z;
   if (swap) t = 1.0 / z;
-  const double r = atan_core(t);
+  const double r = atan_core<EST>(t);
   return swap ? (copysign(kPio2, z) - r) + copysign(kPio2Tail, z) : r;
 }
 
+template <bool EST>
+__device__ __host__ __forceinline__ double poly7(const double* a, double s1) {
+  if (!EST) {
+    double p = a[6];
+#pragma unroll
+    for (int i = 5; i >= 0; --i) p = fma(p, s1, a[i]);
+    return p;
+  }
+  const double s2 = s1 * s1, s4 = s2 * s2;
+  return fma(fma(a[6], s2, fma(a[5], s1, a[4])), s4, fma(fma(a[3], s1, a[2]), s2, fma(a[1], s1, a[0])));
+}
+
+template <bool EST>
 __device__ __host__ __forceinline__ double sin_poly(double r, double s1) {
-  double p = kSinQ[6];
-#pragma unroll
-  for (int i = 5; i >= 0; --i) p = fma(p, s1, kSinQ[i]);
-  return fma(r * s1, p, r);
+  return fma(r * s1, poly7<EST>(kSinQ, s1), r);
 }
 
+template <bool EST>
 __device__ __host__ __forceinline__ double cos_poly(double s1) {
-  double p = kCosQ[6];
-#pragma unroll
-  for (int i = 5; i >= 0; --i) p = fma(p, s1, kCosQ[i]);
-  return fma(s1 * s1, p, fma(-0.5, s1, 1.0));
+  return fma(s1 * s1, poly7<EST>(kCosQ, s1), fma(-0.5, s1, 1.0));
 }
 
+template <bool EST>
 __device__ __host__ __forceinline__ void sincos_core(double r, double* s, double* c) {
   const double s1 = r * r;
-  *s = sin_poly(r, s1);
-  *c = cos_poly(s1);
+  *s = sin_poly<EST>(r, s1);
+  *c = cos_poly<EST>(s1);
 }
 
+template <bool EST = false>
 __device__ __host__ __forceinline__ void sincos_(double a, double* s, double* c) {
   if (!(fabs(a) <= kSinCosMax)) {       // huge or non-finite: ocml (Payne-Hanek)
     sincos(a, s, c);
@@ -134,7 +162,7 @@ __device__ __host__ __forceinline__ void sincos_(double a, double* s, double* c)
   r = fma(-k, kPio2Lo, r);
   const int q = (int)k & 3;
   double sr, cr;
-  sincos_core(r, &sr, &cr);
+  sincos_core<EST>(r, &sr, &cr);
   double so = (q & 1) ? cr : sr, co = (q & 1) ? sr : cr;
   so = (q & 2) ? -so : so;
   co = ((q + 1) & 2) ? -co : co;
@@ -144,13 +172,153 @@ __device__ __host__ __forceinline__ void sincos_(double a, double* s, double* c)
 
 // sin(a): wave-uniform fast path when every |a| <= pi/4 (no reduction, one polynomial) —
 // the common case for the tire argument C*atan(B*alpha) at moderate slip.
+template <bool EST = false>
 __device__ __host__ __forceinline__ double sin_(double a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (__all(fabs(a) <= kPio4)) return sin_poly(a, a * a);
+  if (__all(fabs(a) <= kPio4)) return sin_poly<EST>(a, a * a);
 #endif
   double s, c;
-  sincos_(a, &s, &c);
+  sincos_<EST>(a, &s, &c);
   return s;
+}
+
+// ------------------------------------------------------------------------------------
+// Branch-free cores for the rollout stage (dyn.hpp rhs_fast).
+//
+// Measured on gfx950 with ONE wave per SIMD (the regime of a tick at N*C ~ 1e4):
+// a dependent fp64 FMA costs ~6 cycles, but a compare+select ~25, a wave-uniform branch
+// ~70, v_rcp_f64 / v_rndne_f64 ~40 (tools/micro/lat_bench.hip).  So these cores carry no
+// branches and as few selects as possible, and are valid only on a stated domain; the
+// caller evaluates the domain predicate (the *_ok helpers, off the critical path) and
+// re-does the rare out-of-domain lanes with the general functions above, behind ONE
+// wave-uniform branch per stage that is normally not taken.
+// ------------------------------------------------------------------------------------
+constexpr double kSinWQ[11] = {
+    -0.16666666666666666,   0.008333333333333333,   -0.0001984126984126983,
+    2.755731922398403e-06,  -2.5052108385275923e-08, 1.6059043828214877e-10,
+    -7.647163453155476e-13, 2.8114514557344955e-15, -8.21985910722077e-18,
+    1.950826068108976e-20,  -3.56150612064771e-23};
+constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 3 ulp up to 2
+
+// Constants of the fast cores, held in VGPRs for the whole kernel (FmK::load pins them
+// with an empty asm so the compiler cannot rematerialise them): a VOP3 v_fma_f64 reads a
+// VGPR constant for free, while a rematerialised 64-bit constant costs two v_mov/s_mov
+// issue slots per use — 2.5x on a Horner chain in the one-wave-per-SIMD regime.
+struct FmK {
+  double at[22], sw[11], sq[7], cq[7];
+  double pio2, pio2t, two_pi, cw0, cw1, cw2, sixth, six;
+
+  __device__ __forceinline__ static void pin(double& x) { asm volatile("" : "+v"(x)); }
+  __device__ __forceinline__ static FmK load() {
+    FmK k;
+#pragma unroll
+    for (int i = 0; i < 22; ++i) { k.at[i] = kAtanQ[i]; pin(k.at[i]); }
+#pragma unroll
+    for (int i = 0; i < 11; ++i) { k.sw[i] = kSinWQ[i]; pin(k.sw[i]); }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      k.sq[i] = kSinQ[i];
+      k.cq[i] = kCosQ[i];
+      pin(k.sq[i]);
+      pin(k.cq[i]);
+    }
+    k.pio2 = kPio2;
+    k.pio2t = kPio2Tail;
+    k.two_pi = kTwoOverPi;
+    k.cw0 = kPio2Hi;
+    k.cw1 = kPio2Mid;
+    k.cw2 = kPio2Lo;
+    k.sixth = 1.0 / 6.0;
+    k.six = 6.0;
+    pin(k.pio2); pin(k.pio2t); pin(k.two_pi); pin(k.cw0); pin(k.cw1); pin(k.cw2);
+    pin(k.sixth); pin(k.six);
+    return k;
+  }
+};
+
+template <int N>
+__device__ __forceinline__ double horner(const double* c, double s) {
+  double p = c[N - 1];
+#pragma unroll
+  for (int i = N - 2; i >= 0; --i) p = fma(p, s, c[i]);
+  return p;
+}
+
+// num / den, den in [2^-1001, 2^1000]: reciprocal + two Newton steps + residual.
+__device__ __forceinline__ double div_fast(double num, double den) {
+  double r = __builtin_amdgcn_rcp(den);
+  double e = fma(-den, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-den, r, 1.0);
+  r = fma(r, e, r);
+  const double q = num * r;
+  return fma(r, fma(-den, q, num), q);
+}
+
+// v / 6 correctly rounded (Markstein: q = RN(v/6 approx), exact residual, one correction;
+// checked bit-exact against v / 6.0 in tests/test_host_cpu.py::test_div6_correctly_rounded).
+__device__ __host__ __forceinline__ double div6(double v) {
+  const double y = 1.0 / 6.0;
+  const double q = v * y;
+  return fma(fma(-6.0, q, v), y, q);
+}
+__device__ __forceinline__ double div6(double v, const FmK& K) {
+  const double q = v * K.sixth;
+  return fma(fma(-K.six, q, v), K.sixth, q);
+}
+
+__device__ __forceinline__ double atan_core_k(double t, const FmK& K) {
+  const double s = t * t;
+  return fma(t * s, horner<22>(K.at, s), t);
+}
+
+// atan2(y, x) for x >= 0 on the domain atan2_fast_ok(y, x): the sum |y| + x in
+// [2^-1000, 2^1000] (so max(|y|, x) is a safe divisor; NaN -> not ok).
+__device__ __host__ __forceinline__ bool atan2_fast_ok(double y, double x) {
+  const double s = fabs(y) + x;
+  return s >= 0x1p-1000 && s <= 0x1p1000;
+}
+__device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K) {
+  const double ay = fabs(y);
+  const double r = atan_core_k(div_fast(fmin(ay, x), fmax(ay, x)), K);
+  const double o = (ay > x) ? (K.pio2 - r) + K.pio2t : r;
+  return copysign(o, y);
+}
+
+// atan(z) on the domain |z| <= 2^1000: the reciprocal branch as a division by max(|z|, 1)
+// (exact when |z| <= 1).
+__device__ __host__ __forceinline__ bool atan_fast_ok(double z) { return fabs(z) <= 0x1p1000; }
+__device__ __forceinline__ double atan_fast(double z, const FmK& K) {
+  const double az = fabs(z);
+  const double r = atan_core_k(div_fast(fmin(az, 1.0), fmax(az, 1.0)), K);
+  const double o = (az > 1.0) ? (K.pio2 - r) + K.pio2t : r;
+  return copysign(o, z);
+}
+
+// sin(a) for |a| <= kSinWideMax, one polynomial (the Pacejka argument C*atan(.) is
+// bounded by |C| pi/2, so |C| <= 1.9 keeps every call in range).
+__device__ __forceinline__ double sin_wide(double a, const FmK& K) {
+  const double s = a * a;
+  return fma(a * s, horner<11>(K.sw, s), a);
+}
+
+// sincos(a) for |a| <= kSinCosMax (NaN/inf -> not ok): Cody-Waite reduction, quadrant
+// fix-up with integer sign flips.
+__device__ __host__ __forceinline__ bool sincos_fast_ok(double a) { return fabs(a) <= kSinCosMax; }
+__device__ __forceinline__ void sincos_fast(double a, double* s, double* c, const FmK& K) {
+  const double k = rint(a * K.two_pi);
+  double r = fma(-k, K.cw0, a);
+  r = fma(-k, K.cw1, r);
+  r = fma(-k, K.cw2, r);
+  const int q = (int)k;
+  const double s1 = r * r;
+  const double sr = fma(r * s1, horner<7>(K.sq, s1), r);
+  const double cr = fma(s1 * s1, horner<7>(K.cq, s1), fma(-0.5, s1, 1.0));
+  const bool odd = q & 1;
+  const double so = odd ? cr : sr, co = odd ? sr : cr;
+  const int fs = (q & 2) << 30, fc = ((q + 1) & 2) << 30;
+  *s = __hiloint2double(__double2hiint(so) ^ fs, __double2loint(so));
+  *c = __hiloint2double(__double2hiint(co) ^ fc, __double2loint(co));
 }
 
 }  // namespace fm

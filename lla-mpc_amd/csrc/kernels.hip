@@ -30,6 +30,14 @@ namespace llampc {
 // kernel; never compiled into the product library.
 __device__ unsigned long long g_stamps[64][8][2];
 __device__ unsigned int g_stamp_launch;
+__device__ unsigned long long g_la_stamps[8][8][2];   // first 8 look-ahead blocks, last launch
+#define LA_STAMP(blk, slot)                                                              \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && (blk) < 8) {                                                 \
+      g_la_stamps[blk][slot][0] = __builtin_amdgcn_s_memtime();                          \
+      g_la_stamps[blk][slot][1] = __builtin_amdgcn_s_memrealtime();                      \
+    }                                                                                    \
+  } while (0)
 #define STAMP(slot)                                                                      \
   do {                                                                                   \
     if (threadIdx.x == 0) {                                                              \
@@ -41,6 +49,9 @@ __device__ unsigned int g_stamp_launch;
 #else
 #define STAMP(slot) \
   do {              \
+  } while (0)
+#define LA_STAMP(blk, slot) \
+  do {                      \
   } while (0)
 #endif
 
@@ -271,14 +282,15 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
 }
 
 // ------------------------------------------------------------------------------------
-// Look-ahead body.  Lane layout inside a block: sub = lane % LPM (lane-split of one
-// rollout), cl = lane / LPM; G candidate-lanes per model (power of two); a model's
+// Look-ahead body.  Lane layout inside a block: sub = lane % LPM (LPM = 2: the lane pair
+// of one rollout, front/rear chain), cl = lane / LPM; G candidate-lanes per model (power of two); a model's
 // candidates c = g + j*G, j < cpl, run sequentially in its G*LPM lanes.
 //   LDS from kScratchBytes: xref as [k][2]; U as [k][c][2] when staged.
 // ------------------------------------------------------------------------------------
 template <int INTEG, bool STAGE, int LPM>
 __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int blk, int G, int cpl,
                                                 unsigned char* smem, const Scratch& sc) {
+  LA_STAMP(blk, 0);
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);
   double* su = sx + 2 * (a.H + 1);
   const int H = a.H, C = a.C;
@@ -328,8 +340,12 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   double bv = __builtin_nan("");
   int64_t bc = kNoIndex;
   int nf = 0;
+  LA_STAMP(blk, 1);
   if (live) {
     const Tire t = load_tire(a.params, a.n, n);
+    // LPM = 2: lane 0 of the pair evaluates the front chain, lane 1 the rear (dyn.hpp)
+    const StageK sk = make_stage<LPM>(veh, t, sub);
+    const fm::FmK K = fm::FmK::load();
     for (int j = 0; j < cpl; ++j) {
       const int c = g + j * G;
       if (c >= C) break;
@@ -355,8 +371,8 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
           if (q.dmax[0] >= 0) feas = feas && d0 <= q.dmax[0] && -d0 <= q.dmax[0];
           if (q.dmax[1] >= 0) feas = feas && d1 <= q.dmax[1] && -d1 <= q.dmax[1];
         }
-        const Input u = make_input(ua, ud);
-        step_split<INTEG, LPM>(veh, t, x, u, Ts, sub);
+        const Input u = make_input_fast(ua, ud, K);
+        step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K);
         const double e0 = x[0] - sx[2 * (k + 1)], e1 = x[1] - sx[2 * (k + 1) + 1];
         track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
         act = act + (d0 * (q.R[0] * d0 + q.R[1] * d1) + d1 * (q.R[2] * d0 + q.R[3] * d1));
@@ -377,6 +393,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       }
     }
   }
+  LA_STAMP(blk, 2);
   // per-model argmin over its candidates: xor-shuffles across the model's G*LPM lanes
   for (int off = (G * LPM) >> 1; off >= LPM; off >>= 1) {
     const double ov = __shfl_xor(bv, off, 64);
@@ -814,22 +831,18 @@ int lookahead_group(int32_t C) {
   return G;
 }
 
-// Lanes per rollout: split the transcendental chains over 4 (2) lanes while the launch is
-// latency-bound (few waves per SIMD); one lane per rollout once the chip is full.
+// Lanes per rollout: split the two tire chains over a lane pair while the launch has
+// fewer waves than the chip has SIMDs (latency-bound: a wave's time is its instruction
+// stream); one lane per rollout once the chip fills (fewest instructions per rollout).
 int lookahead_lpm(int64_t n, int32_t C, int32_t integrator) {
   if (integrator == LLAMPC_RK6) return 1;
   const int G = lookahead_group(C);
   if (const char* e = getenv("LLAMPC_LPM")) {     // benchmarking override
-    int v = atoi(e);
-    if (v == 1 || v == 2 || v == 4) {
-      while (v > 1 && G * v > 64) v >>= 1;         // a model's lanes stay inside one wave
-      return v;
-    }
+    const int v = atoi(e);
+    if (v == 1 || (v == 2 && G <= 32)) return v;
   }
   const int64_t lanes = n * G;
-  if (lanes <= 32768 && G <= 16) return 4;
-  if (lanes <= 131072 && G <= 32) return 2;
-  return 1;
+  return (lanes <= 32768 && G <= 32) ? 2 : 1;
 }
 
 int lookahead_blocks(int64_t n, int32_t C, int lpm) {
@@ -865,8 +878,7 @@ static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, c
 template <int INTEG, bool STAGE>
 static void launch_plan_l(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
                           int G, int cpl, int lpm, size_t lds, hipStream_t s) {
-  if (lpm == 4) launch_plan_t<INTEG, STAGE, 4>(lb, la, f, G, cpl, lds, s);
-  else if (lpm == 2) launch_plan_t<INTEG, STAGE, 2>(lb, la, f, G, cpl, lds, s);
+  if (lpm == 2) launch_plan_t<INTEG, STAGE, 2>(lb, la, f, G, cpl, lds, s);
   else launch_plan_t<INTEG, STAGE, 1>(lb, la, f, G, cpl, lds, s);
 }
 
@@ -916,6 +928,9 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
 }
 
 #ifdef LLAMPC_STAMPS
+extern "C" int llampc_debug_la_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_stamps), sizeof(g_la_stamps)) == hipSuccess ? 0 : -2;
+}
 extern "C" int llampc_debug_stamps(unsigned long long* out, unsigned* launches) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -2;
   return hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_stamp_launch), sizeof(unsigned)) == hipSuccess ? 0 : -2;

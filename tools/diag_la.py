@@ -1,0 +1,27 @@
+"""Diagnostic (not product): phase stamps of the first 8 look-ahead blocks (stamps build)."""
+import ctypes, os, sys
+import numpy as np
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["LLAMPC_HIP_LIB"] = os.path.join(REPO, "lla-mpc_amd/llampc/_lib/libllampc_hip_stamps.so")
+sys.path[:0] = [REPO, os.path.join(REPO, "lla-mpc_amd")]
+from llampc import _native as nat
+from llampc.mpc import ModelBank, generate_bank
+lib = nat.load()
+d = np.load(os.path.join(REPO, "tests/golden/dyn_slice.npz"))
+s, u = d["states"], d["inputs"]
+N, H = int(sys.argv[1]) if len(sys.argv) > 1 else 10000, 20
+b = ModelBank(generate_bank(N, 0), W=10, device=0)
+xref = s[:2, :H + 1]
+U = np.tile(u[:, 0], (H, 1))[None]
+for t in range(1, 30):
+    b.plan_raw(s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1])
+st = (ctypes.c_ulonglong * (8 * 8 * 2))()
+fn = lib.llampc_debug_la_stamps
+fn.argtypes = [ctypes.c_void_p]
+fn(st)
+a = np.frombuffer(st, dtype=np.uint64).reshape(8, 8, 2).astype(np.int64)
+t0 = a[:, 0, 1].min()
+for blk in range(8):
+    mt, rt = a[blk, :5, 0], a[blk, :5, 1]
+    print(f"la block {blk}: start +{(rt[0]-t0)/100:.2f}us | phases(cycles) staging {mt[1]-mt[0]}, rollout {mt[2]-mt[1]}, "
+          f"reduce {mt[3]-mt[2]}, ticket {mt[4]-mt[3]} | total {(rt[4]-rt[0])/100:.2f}us  clk {(mt[4]-mt[0])/max(1,rt[4]-rt[0])*100:.0f}MHz")

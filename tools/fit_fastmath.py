@@ -3,6 +3,7 @@
 atan(t)   = t + t*s*QA(s),            s = t^2,  |t| <= 1
 sin(r)    = r + r*s*QS(s),            s = r^2,  |r| <= pi/4
 cos(r)    = 1 - s/2 + s^2*QC(s),      s = r^2,  |r| <= pi/4
+sin(a)    = a + a*s*QW(s),            s = a^2,  |a| <= 3   (no range reduction: tire sin)
 Chebyshev fits in mpmath at 60 digits; the max error is then measured with the
 coefficients rounded to double and the final assembly done in float64.
 """
@@ -68,12 +69,17 @@ for nS in (7, 8, 9):
 cS, _ = fit(QS, 0, r4 * r4, 8)
 cC, _ = fit(QC, 0, r4 * r4, 8)
 
+cW, eW = fit(QS, 0, 9.0, 11)
+print(f"QW n=11 chebyfit err {float(eW):.3e}", file=sys.stderr)
+
 atan_f = lambda t, c: t + t * (t * t) * horner(c, t * t)
 sin_f = lambda r, c: r + r * (r * r) * horner(c, r * r)
 cos_f = lambda r, c: 1 - (r * r) / 2 + (r * r) ** 2 * horner(c, r * r)
 check("atan [0,1]", cA, atan_f, mp.atan, 1e-8, 1.0)
 check("sin [0,pi/4]", cS, sin_f, mp.sin, 1e-8, r4)
 check("cos [0,pi/4]", cC, cos_f, mp.cos, 0.0, r4)
+check("sin [0,2]", cW, sin_f, mp.sin, 1e-8, 2.0)
+check("sin [0,3]", cW, sin_f, mp.sin, 1e-8, 3.0)
 
 def emit(name, c):
     body = ",\n    ".join(f"{x!r}" for x in c)
@@ -82,6 +88,7 @@ def emit(name, c):
 emit("kAtanQ", cA)
 emit("kSinQ", cS)
 emit("kCosQ", cC)
+emit("kSinWQ", cW)
 # Cody-Waite split of pi/2 (26+26+rest bits) for |k| <= 2^20
 pio2 = mp.pi / 2
 h = float(mp.mpf(int(pio2 * 2 ** 26)) / 2 ** 26)

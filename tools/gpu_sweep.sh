@@ -6,12 +6,12 @@ mkdir -p gpurun_out
 out=gpurun_out/sweep.jsonl
 : > $out
 for C in 1 64; do
-  for L in 1 2 4; do
+  for L in 0 1 2 4; do
     LLAMPC_LPM=$L timeout -k 10 120 python bench.py --C $C --steps 100 --warmup 10 --no-cpu-baseline --no-extra >> $out 2>> gpurun_out/sweep.err || exit 1
   done
 done
 for H in 40; do
-  for L in 1 2 4; do
+  for L in 0 2 4; do
     LLAMPC_LPM=$L timeout -k 10 120 python bench.py --track ETHZMobil --H $H --steps 100 --warmup 10 --no-cpu-baseline --no-extra >> $out 2>> gpurun_out/sweep.err || exit 1
   done
 done

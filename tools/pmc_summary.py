@@ -3,7 +3,7 @@ import csv, glob, os, sys
 from collections import defaultdict
 root = sys.argv[1]
 vals = defaultdict(lambda: defaultdict(list))
-for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         k = r.get("Kernel_Name", "?")
         name = r.get("Counter_Name", "?")
