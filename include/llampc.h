@@ -214,9 +214,14 @@ int llampc_integrate_batch(const double* x0, const double* u, int64_t u_stride_l
 
 /* ---- model transcendentals (accuracy tests) -------------------------------------- */
 /* The fp64 atan2 (x >= 0) / atan / sin / cos the kernels use (csrc/fastmath.hpp),
- * elementwise on host arrays: out[i] = f(a[i][, b[i]]). */
+ * elementwise on host arrays: out[i] = f(a[i][, b[i]]).  0-3: the general versions (any
+ * argument); 4-9: the branch-free cores of the rollout stage, defined on their domains only
+ * (atan2: |a| + b in [2^-1000, 2^1000], b >= 0; atan: |a| <= 2^1000; sin_wide: |a| <= 3;
+ * sincos: |a| <= 2^20 pi/2) — the stage re-does out-of-domain lanes with 0-3; 9 = a / 6. */
 enum llampc_math_fn { LLAMPC_MATH_ATAN2_XPOS = 0, LLAMPC_MATH_ATAN = 1, LLAMPC_MATH_SIN = 2,
-                      LLAMPC_MATH_COS = 3 };
+                      LLAMPC_MATH_COS = 3, LLAMPC_MATH_ATAN2_FAST = 4, LLAMPC_MATH_ATAN_FAST = 5,
+                      LLAMPC_MATH_SIN_WIDE = 6, LLAMPC_MATH_SIN_FAST = 7, LLAMPC_MATH_COS_FAST = 8,
+                      LLAMPC_MATH_DIV6 = 9 };
 int llampc_math_batch(int32_t fn, const double* a, const double* b, int64_t n, double* out,
                       int32_t device);
 

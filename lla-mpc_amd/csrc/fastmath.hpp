@@ -198,7 +198,8 @@ constexpr double kSinWQ[11] = {
     2.755731922398403e-06,  -2.5052108385275923e-08, 1.6059043828214877e-10,
     -7.647163453155476e-13, 2.8114514557344955e-15, -8.21985910722077e-18,
     1.950826068108976e-20,  -3.56150612064771e-23};
-constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 3 ulp up to 2
+constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 4 ulp up to
+                                       // |a| = 2, then <= 2^-49 absolute (cancellation)
 
 // Constants of the fast cores, held in VGPRs for the whole kernel (FmK::load pins them
 // with an empty asm so the compiler cannot rematerialise them): a VOP3 v_fma_f64 reads a

@@ -780,11 +780,18 @@ __global__ __launch_bounds__(kBlock) void math_kernel(int32_t fn, const double* 
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   double r = 0.0, s, c;
+  const fm::FmK K = fm::FmK::load();
   switch (fn) {
     case 0: r = LL_ATAN2P(a[i], b[i]); break;
     case 1: r = LL_ATAN(a[i]); break;
     case 2: LL_SINCOS(a[i], &s, &c); r = s; break;
     case 3: LL_SINCOS(a[i], &s, &c); r = c; break;
+    case 4: r = fm::atan2_fast(a[i], b[i], K); break;
+    case 5: r = fm::atan_fast(a[i], K); break;
+    case 6: r = fm::sin_wide(a[i], K); break;
+    case 7: fm::sincos_fast(a[i], &s, &c, K); r = s; break;
+    case 8: fm::sincos_fast(a[i], &s, &c, K); r = c; break;
+    case 9: r = fm::div6(a[i], K); break;
     default: r = __builtin_nan("");
   }
   out[i] = r;

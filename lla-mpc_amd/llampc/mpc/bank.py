@@ -47,7 +47,7 @@ class ModelBank:
     """A shard of the model bank resident on one HIP device."""
 
     def __init__(self, params6, shared: dict | None = None, W: int = 10, device: int = 0,
-                 global_offset: int = 0, input_acc: bool = False):
+                 global_offset: int = 0, input_acc: bool = False, approx: bool = False):
         params6 = np.ascontiguousarray(np.asarray(params6, dtype=np.float64).reshape(6, -1))
         self.params = params6
         self.n = params6.shape[1]
@@ -56,7 +56,7 @@ class ModelBank:
         self.global_offset = int(global_offset)
         shared = ORCA(control='pwm') if shared is None else shared
         self.shared = {k: float(shared[k]) for k in SHARED_KEYS}
-        self._veh = nat.vehicle(*(self.shared[k] for k in SHARED_KEYS), input_acc=input_acc, approx=False)
+        self._veh = nat.vehicle(*(self.shared[k] for k in SHARED_KEYS), input_acc=input_acc, approx=approx)
         lib = nat.load()
         h = nat.C.c_void_p()
         nat.check(lib.llampc_bank_create(nat.dptr(params6), self.n, self.global_offset,
@@ -71,7 +71,8 @@ class ModelBank:
         p = np.array([[getattr(m, k) for m in models] for k in BANK_ORDER], dtype=np.float64)
         m0 = models[0]
         return cls(p, {k: getattr(m0, k) for k in SHARED_KEYS}, W=W, device=device,
-                   global_offset=global_offset, input_acc=m0.input_acc)
+                   global_offset=global_offset, input_acc=m0.input_acc,
+                   approx=bool(getattr(m0, "approx", False)))
 
     @classmethod
     def generate(cls, n, seed=0, sigma=None, W=10, device=0, rank=0, world=1):

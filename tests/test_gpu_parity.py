@@ -2,6 +2,8 @@
 reference-generated golden vectors.  Tolerances: fp64 values 1e-9 relative for one
 integration step (ocml vs NumPy transcendentals differ by ulps), 1e-7 for H-step rollouts
 and their costs (north star bound: 1e-5); indices exact (tie-tolerant only where stated)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -434,3 +436,67 @@ def test_fast_transcendentals_ulp_vs_libm(nat):
         np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
         err = np.abs(got[fin] - want[fin])
         assert np.all(err <= 4 * np.spacing(np.maximum(np.abs(want[fin]), 1e-16))), err.max()
+
+
+def test_fast_cores_ulp_on_domain(nat):
+    """The branch-free cores of the rollout stage (fastmath.hpp, math fn 4-9) on their
+    domains vs NumPy (libm): atan2/atan <= 4 ulp, sin_wide <= 4 ulp for |a| <= 2 and
+    <= 2^-49 absolute up to 3 (no reduction: a + a s P(s) cancels as sin(3) ~ 0.14),
+    sincos <= 4 ulp / absolute near zeros, a / 6 bit-exact."""
+    rng = np.random.RandomState(1)
+    n = 1 << 20
+    y = np.concatenate([rng.uniform(-3, 3, n), rng.standard_cauchy(n), [0.0, -0.0, 1.0, -1.0, 1e-300, 5.0]])
+    x = np.concatenate([rng.uniform(0, 4, n), np.abs(rng.standard_cauchy(n)), [1.0, 1.0, 0.0, 0.0, 0.0, 3.0]])
+    ok = (np.abs(y) + x >= 2.0 ** -1000) & (np.abs(y) + x <= 2.0 ** 1000)
+    assert _ulp(_math(nat, 4, y[ok], x[ok]), np.arctan2(y[ok], x[ok])) <= 4
+    z = np.concatenate([rng.uniform(-2, 2, n), rng.standard_cauchy(n) * 10, [0.0, -0.0, 1.0, -1.0, 1e300, -1e-300]])
+    assert _ulp(_math(nat, 5, z), np.arctan(z)) <= 4
+    a = rng.uniform(-2, 2, n)
+    assert _ulp(_math(nat, 6, a), np.sin(a)) <= 4
+    a = np.concatenate([rng.uniform(-3, 3, n), [3.0, -3.0, 0.0, -0.0, 1e-300]])
+    err = np.abs(_math(nat, 6, a) - np.sin(a))
+    assert np.all(err <= 4 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -49), err.max()
+    a = np.concatenate([rng.uniform(-4, 4, n), rng.uniform(-300, 300, n), rng.uniform(-1.6e6, 1.6e6, 1000),
+                        [0.0, -0.0, np.pi / 2, np.pi, 1e-300]])
+    for fn, want in ((7, np.sin(a)), (8, np.cos(a))):
+        err = np.abs(_math(nat, fn, a) - want)
+        assert np.all(err <= 4 * np.spacing(np.maximum(np.abs(want), 1e-16))), err.max()
+    v = np.concatenate([rng.standard_normal(n) * 10.0 ** rng.randint(-300, 300, n), [0.0, -0.0, 6.0, 1e308, 5e-324]])
+    np.testing.assert_array_equal(_math(nat, 9, v), v / 6.0)
+
+
+def test_lookahead_out_of_domain_fallback(nat):
+    """Rollouts whose operands leave the fast cores' domains take the general evaluation
+    (dyn.hpp rhs_fast): models with |C| > 1.9, a yaw beyond 2^20 pi/2, a standing start
+    (|y| + |vx| = 0), and a linear-tire bank — all against the oracle, in waves that mix
+    fast and fallback lanes (both LPM = 1 and the lane-pair split)."""
+    from llampc.mpc import ModelBank, generate_bank
+    N, C, H = 640, 3, 12
+    p = generate_bank(N, seed=11)
+    p[1, 5::37] = 2.6          # Cf beyond the sin_wide bound
+    p[4, 9::41] = -2.2         # Cr
+    rng = np.random.RandomState(3)
+    U = np.stack([rng.uniform(0.1, 0.9, (C, H)), rng.uniform(-0.3, 0.3, (C, H))], axis=-1)
+    xref = np.vstack([np.linspace(0, 0.5, H + 1), np.linspace(0, -0.2, H + 1)])
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    cases = [np.array([0.2, 0.1, -0.7, 1.5, 0.02, 0.3]),
+             np.array([0.2, 0.1, 3.0e6, 1.5, 0.02, 0.3]),           # huge yaw: sincos fallback
+             np.array([0.0, 0.0, 0.4, 0.0, 0.0, 0.0])]              # standing start
+    for x0 in cases:
+        with np.errstate(all="ignore"):
+            traj = O.rollout_rk4(shared(), tuple(p), x0, U, TS)
+            cref = O.mpc_cost(traj, U, xref, np.zeros(2), Q, R, P)
+        for lpm in ("1", "2"):
+            os.environ["LLAMPC_LPM"] = lpm
+            try:
+                with ModelBank(p, device=0) as b:
+                    r = b.lookahead(x0, U, xref, np.zeros(2), Ts=TS, return_costs=True)
+            finally:
+                del os.environ["LLAMPC_LPM"]
+            close(r["costs"].ravel(), cref, RTOL_ROLL)
+    # linear tires (Dynamic(approx=True), dynamic.py:126-136): every lane takes the fallback
+    x0 = cases[0]
+    with ModelBank(p, device=0, approx=True) as b:
+        r = b.lookahead(x0, U, xref, np.zeros(2), Ts=TS, return_costs=True)
+    traj = O.rollout_rk4(shared(), tuple(p), x0, U, TS, approx=True)
+    close(r["costs"].ravel(), O.mpc_cost(traj, U, xref, np.zeros(2), Q, R, P), RTOL_ROLL)

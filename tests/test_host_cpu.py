@@ -235,3 +235,20 @@ def test_oracle_not_imported_by_product():
         for f in files:
             if f.endswith((".py", ".hip", ".hpp", ".h")):
                 assert "oracle" not in open(os.path.join(dp, f)).read(), f
+
+
+def test_div6_correctly_rounded():
+    """fastmath.hpp div6: q = RN(v * RN(1/6)); r = v - 6q (exact by FMA); RN(q + r * RN(1/6))
+    equals RN(v / 6) (Markstein's theorem).  Exact rational arithmetic on random values
+    over the whole exponent range plus the neighbours of multiples of 6."""
+    from fractions import Fraction as F
+    y = F(1.0 / 6.0)
+    rng = np.random.default_rng(7)
+    vals = list(rng.standard_normal(20000) * 10.0 ** rng.integers(-300, 300, 20000))
+    vals += [float(np.nextafter(6.0 * k, s)) for k in range(1, 500) for s in (0.0, np.inf)]
+    vals += [1.0, -1.0, 6.0, 3.0, 2.0 ** -1000, 1e308]
+    for v in vals:
+        q = float(F(v) * y)
+        r = F(v) - 6 * F(q)
+        assert float(r) == r                       # the FMA residual is exact
+        assert float(F(q) + r * y) == v / 6.0, v
