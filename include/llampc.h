@@ -151,9 +151,10 @@ int llampc_bank_window(llampc_bank* bank, double* ring, int32_t* window_count);
 int llampc_bank_set_stream(llampc_bank* bank, void* stream);
 
 /* Per-kernel HIP-event timing of the bank's launches, on the stream they run on (for the
- * benchmark's roofline).  enable=1 arms `max_launches` event pairs; each launch of the
- * plan kernel (the whole tick: look-back + look-ahead + selection) is bracketed by
- * hipEventRecord. */
+ * benchmark's roofline).  enable=k >= 1 arms `max_launches` event pairs and brackets
+ * every k-th launch of the plan kernel (the whole tick: look-back + look-ahead +
+ * selection) with hipEventRecord (k > 1 keeps the events' own cost out of a timed loop);
+ * enable=0 disarms. */
 int llampc_bank_timing(llampc_bank* bank, int32_t enable, int32_t max_launches);
 /* Synchronises, returns avg_ms[3] and count[3] for {plan kernel, reserved, reserved}
  * since the last read, and re-arms the counters. */
@@ -179,6 +180,14 @@ int llampc_lookahead(llampc_bank* bank, const double* x0, const double* U, int32
 /* Host pointers; blocking.  err_out [n], wmean_out [n], cost_out [n][C] may be NULL. */
 int llampc_plan(llampc_bank* bank, const llampc_plan_in* in, llampc_plan_out* out,
                 double* err_out, double* wmean_out, double* cost_out);
+/* Host pointers; asynchronous (SURVEY.md §8b "_async" variant): the inputs are copied
+ * into the bank's pinned staging buffer before the call returns (the caller may reuse
+ * them), and the H2D copy, the plan kernel and the D2H copy of the result record are
+ * enqueued on the bank's stream.  llampc_plan_wait synchronises and returns the record.
+ * At most one outstanding async tick per bank (LLAMPC_E_STATE otherwise); independent
+ * banks (e.g. two tracks) overlap on the device. */
+int llampc_plan_async(llampc_bank* bank, const llampc_plan_in* in);
+int llampc_plan_wait(llampc_bank* bank, llampc_plan_out* out);
 /* Device pointers in `in`; d_out is a device llampc_plan_out; asynchronous on
  * `stream` (hipStream_t, NULL = the bank's stream).  d_err/d_wmean/d_cost: device
  * arrays or NULL. */

@@ -134,6 +134,9 @@ struct llampc_bank {
   std::vector<hipEvent_t> ev[3];
   size_t ev_used[3] = {0, 0, 0};
   bool timing = false;
+  int64_t timing_stride = 1;       // bracket every stride-th launch
+  bool async_pending = false;      // llampc_plan_async issued, llampc_plan_wait not yet
+  int64_t timing_seen[3] = {0, 0, 0};
 };
 
 namespace {
@@ -193,6 +196,7 @@ struct TimedLaunch {
   hipEvent_t stop = nullptr;
   TimedLaunch(llampc_bank* b_, int k_, hipStream_t s_) : b(b_), k(k_), s(s_) {
     if (!b->timing || 2 * (b->ev_used[k] + 1) > b->ev[k].size()) return;
+    if (b->timing_seen[k]++ % b->timing_stride) return;
     const size_t i = b->ev_used[k]++;
     (void)hipEventRecord(b->ev[k][2 * i], s);
     stop = b->ev[k][2 * i + 1];
@@ -208,7 +212,9 @@ void timing_free(llampc_bank* b) {
     v.clear();
   }
   for (size_t& u : b->ev_used) u = 0;
+  for (int64_t& u : b->timing_seen) u = 0;
   b->timing = false;
+  b->timing_stride = 1;
 }
 
 // The tick on device pointers: ONE launch (look-back + look-ahead + completion).
@@ -491,12 +497,14 @@ int llampc_bank_timing(llampc_bank* b, int32_t enable, int32_t max_launches) {
   HIP_TRY(hipStreamSynchronize(b->stream));
   timing_free(b);
   if (!enable) return LLAMPC_OK;
+  if (enable < 0) return fail(LLAMPC_E_ARG, "enable must be >= 0");
   if (max_launches < 1) return fail(LLAMPC_E_ARG, "max_launches must be >= 1");
   for (auto& v : b->ev) {
     v.resize(2 * (size_t)max_launches, nullptr);
     for (hipEvent_t& e : v) HIP_TRY(hipEventCreate(&e));
   }
   b->timing = true;
+  b->timing_stride = enable;
   return LLAMPC_OK;
 }
 
@@ -525,6 +533,7 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
   int rc = check_plan_in(b, in);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(b->mu);
+  if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
   DeviceGuard g(b->device);
   hipStream_t s = b->stream;
   if (cost_out && in->do_lookahead && (rc = ensure_cost(b, (size_t)b->n * in->C))) return rc;
@@ -542,6 +551,33 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
   if (d_cost)
     HIP_TRY(hipMemcpyAsync(cost_out, d_cost, (size_t)b->n * in->C * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  *out = *b->h_out;
+  return LLAMPC_OK;
+}
+
+int llampc_plan_async(llampc_bank* b, const llampc_plan_in* in) {
+  if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
+  int rc = check_plan_in(b, in);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
+  DeviceGuard g(b->device);
+  hipStream_t s = b->stream;
+  llampc_plan_in din;
+  if ((rc = stage_inputs(b, in, &din, s))) return rc;
+  if ((rc = plan_launch(b, din, b->d_out, nullptr, nullptr, nullptr, s))) return rc;
+  HIP_TRY(hipMemcpyAsync(b->h_out, b->d_out, sizeof(llampc_plan_out), hipMemcpyDeviceToHost, s));
+  b->async_pending = true;
+  return LLAMPC_OK;
+}
+
+int llampc_plan_wait(llampc_bank* b, llampc_plan_out* out) {
+  if (!b || !out) return fail(LLAMPC_E_ARG, "bank/out is NULL");
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (!b->async_pending) return fail(LLAMPC_E_STATE, "no async tick outstanding");
+  DeviceGuard g(b->device);
+  b->async_pending = false;
+  HIP_TRY(hipStreamSynchronize(b->stream));
   *out = *b->h_out;
   return LLAMPC_OK;
 }

@@ -79,6 +79,8 @@ _SIGNATURES = {
     "llampc_bank_reset": (C.c_int, [C.c_void_p]),
     "llampc_bank_window": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int32)]),
     "llampc_bank_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "llampc_plan_async": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "llampc_plan_wait": (C.c_int, [C.c_void_p, C.c_void_p]),
     "llampc_bank_timing": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "llampc_bank_timing_read": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int64)]),
     "llampc_lookback": (C.c_int, [C.c_void_p, _dp, _dp, _dp, C.c_double, C.c_int32, C.c_int32, _dp,

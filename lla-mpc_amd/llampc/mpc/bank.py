@@ -164,26 +164,32 @@ class ModelBank:
         return dict(best_model=bm.value, best_cand=bcand.value, best_cost=bcost.value, costs=costs,
                     best_cand_per_model=bc)
 
-    def plan_raw(self, x_prev, u_prev, x_now, U, xref, uprev, Ts=0.02, K=10, integrator="rk4",
-                 do_lookback=True, do_lookahead=True, current_model=0, nan_policy=nat.NAN_FIRST,
-                 cost=None, return_errors=False, return_window_mean=False, return_costs=False):
-        """The fused tick (llampc_plan): returns (PlanOut, errors, window_mean, costs)."""
+    def _plan_in(self, x_prev, u_prev, x_now, U, xref, uprev, Ts, K, integrator, do_lookback,
+                 do_lookahead, current_model, nan_policy, cost):
         U = nat.f64(U)
         if U.ndim == 2:
             U = U.reshape(1, *U.shape)
-        C_, H = U.shape[0], U.shape[1]
         keep = []
         ptr = lambda a: (keep.append(nat.f64(a)), nat.dptr(keep[-1]))[1] if a is not None else None
         pin = nat.PlanIn()
         pin.x_prev, pin.u_prev, pin.x_now = ptr(x_prev), ptr(u_prev), ptr(x_now)
         pin.U, pin.xref, pin.uprev = ptr(U), ptr(xref), ptr(uprev)
-        pin.C, pin.H, pin.K = C_, H, int(K)
+        pin.C, pin.H, pin.K = U.shape[0], U.shape[1], int(K)
         pin.integrator = nat.INTEGRATORS[integrator]
         pin.do_lookback, pin.do_lookahead = int(bool(do_lookback)), int(bool(do_lookahead))
         pin.nan_policy = int(nan_policy)
         pin.current_model = int(current_model)
         pin.Ts = float(Ts)
         pin.cost = cost if cost is not None else nat.cost_struct()
+        return pin, keep
+
+    def plan_raw(self, x_prev, u_prev, x_now, U, xref, uprev, Ts=0.02, K=10, integrator="rk4",
+                 do_lookback=True, do_lookahead=True, current_model=0, nan_policy=nat.NAN_FIRST,
+                 cost=None, return_errors=False, return_window_mean=False, return_costs=False):
+        """The fused tick (llampc_plan): returns (PlanOut, errors, window_mean, costs)."""
+        pin, keep = self._plan_in(x_prev, u_prev, x_now, U, xref, uprev, Ts, K, integrator,
+                                  do_lookback, do_lookahead, current_model, nan_policy, cost)
+        C_ = pin.C
         err = np.empty(self.n) if return_errors else None
         wm = np.empty(self.n) if return_window_mean else None
         costs = np.empty((self.n, C_)) if return_costs else None
@@ -191,3 +197,18 @@ class ModelBank:
         nat.check(nat.load().llampc_plan(self.handle, nat.C.byref(pin), nat.C.byref(out), nat.dptr(err),
                                          nat.dptr(wm), nat.dptr(costs)))
         return out, err, wm, costs
+
+    def plan_async(self, x_prev, u_prev, x_now, U, xref, uprev, Ts=0.02, K=10, integrator="rk4",
+                   do_lookback=True, do_lookahead=True, current_model=0, nan_policy=nat.NAN_FIRST,
+                   cost=None):
+        """Enqueue one tick (llampc_plan_async): inputs are staged before return, the tick
+        runs on the bank's stream; ``plan_wait()`` returns its PlanOut.  Independent banks
+        (e.g. one per track) overlap on the device."""
+        pin, keep = self._plan_in(x_prev, u_prev, x_now, U, xref, uprev, Ts, K, integrator,
+                                  do_lookback, do_lookahead, current_model, nan_policy, cost)
+        nat.check(nat.load().llampc_plan_async(self.handle, nat.C.byref(pin)))
+
+    def plan_wait(self):
+        out = nat.PlanOut()
+        nat.check(nat.load().llampc_plan_wait(self.handle, nat.C.byref(out)))
+        return out

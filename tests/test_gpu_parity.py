@@ -500,3 +500,39 @@ def test_lookahead_out_of_domain_fallback(nat):
         r = b.lookahead(x0, U, xref, np.zeros(2), Ts=TS, return_costs=True)
     traj = O.rollout_rk4(shared(), tuple(p), x0, U, TS, approx=True)
     close(r["costs"].ravel(), O.mpc_cost(traj, U, xref, np.zeros(2), Q, R, P), RTOL_ROLL)
+
+
+def test_plan_async_two_banks(nat):
+    """llampc_plan_async / llampc_plan_wait: two banks (two tracks) in flight together give
+    the same records as the blocking llampc_plan; a second async tick on a busy bank and a
+    wait without a tick are refused (LLAMPC_E_STATE)."""
+    from llampc import _native
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    H, W = 20, 3
+    banks = [ModelBank(generate_bank(700, seed=k), W=W, device=0) for k in (0, 1)]
+    refs = [ModelBank(generate_bank(700, seed=k), W=W, device=0) for k in (0, 1)]
+    try:
+        for t in range(1, W + 3):
+            U = u[:, t:t + H].T[None]
+            xref = s[:2, t:t + H + 1] + 0.01 * np.arange(2)[:, None]
+            args = (s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1])
+            for b in banks:
+                b.plan_async(*args, K=5, current_model=2)
+            with pytest.raises(RuntimeError):
+                banks[0].plan_async(*args, K=5)
+            outs = [b.plan_wait() for b in banks]
+            for o, r in zip(outs, refs):
+                want = r.plan_raw(*args, K=5, current_model=2)[0]
+                a, w = _native.plan_out_to_dict(o), _native.plan_out_to_dict(want)
+                for k in a:
+                    if isinstance(a[k], np.ndarray):
+                        np.testing.assert_array_equal(a[k], w[k])
+                    else:
+                        assert a[k] == w[k] or (a[k] != a[k] and w[k] != w[k]), k
+        with pytest.raises(RuntimeError):
+            banks[0].plan_wait()
+    finally:
+        for b in banks + refs:
+            b.close()
