@@ -328,12 +328,12 @@ def concurrent_tracks(args, ticks=1000, warm=50):
 def lpm_of(n, C):
     """Lanes per rollout the library picks (mirror of kernels.hip lookahead_lpm)."""
     G = 1
-    while G < C and G < 64:
+    while G < C and G < 256:
         G <<= 1
     env = os.environ.get("LLAMPC_LPM")
-    if env == "1" or (env == "2" and G <= 32):
+    if env == "1" or (env == "2" and G <= 128):
         return int(env)
-    return 2 if (n * G <= 32768 and G <= 32) else 1
+    return 2 if (n * G <= 32768 and G <= 128) else 1
 
 
 def pmc_traffic(args):

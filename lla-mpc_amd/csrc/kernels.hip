@@ -394,13 +394,35 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     }
   }
   LA_STAMP(blk, 2);
-  // per-model argmin over its candidates: xor-shuffles across the model's G*LPM lanes
-  for (int off = (G * LPM) >> 1; off >= LPM; off >>= 1) {
+  // per-model argmin over its candidates: xor-shuffles across the model's lanes inside a
+  // wave, then (a model spanning 2 or 4 waves: G*LPM in {128, 256}) across its waves in LDS
+  const int span = G * LPM;
+  for (int off = (span < 64 ? span : 64) >> 1; off >= LPM; off >>= 1) {
     const double ov = __shfl_xor(bv, off, 64);
     const int64_t oc = __shfl_xor(bc, off, 64);
     if (less_nan_last(ov, oc, bv, bc)) {
       bv = ov;
       bc = oc;
+    }
+  }
+  int par = 0;
+  if (span > 64) {                                  // block-uniform
+    double* sv = sc.sv + 4 * par;
+    int64_t* si = sc.si + 4 * par;
+    par ^= 1;
+    if ((threadIdx.x & 63) == 0) {
+      sv[threadIdx.x >> 6] = bv;
+      si[threadIdx.x >> 6] = bc;
+    }
+    __syncthreads();
+    const int w0 = (int)(threadIdx.x / span) * (span / 64);
+    bv = sv[w0];
+    bc = si[w0];
+    for (int k = 1; k < span / 64; ++k) {
+      if (less_nan_last(sv[w0 + k], si[w0 + k], bv, bc)) {
+        bv = sv[w0 + k];
+        bc = si[w0 + k];
+      }
     }
   }
   if (live && g == 0 && sub == 0) {
@@ -410,7 +432,6 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   // per-block argmin over (model, candidate) in flattened order (goff+n)*C + c
   int64_t key = (live && bc != kNoIndex) ? (a.goff + n) * C + bc : kNoIndex;
   double v = (key == kNoIndex) ? __builtin_nan("") : bv;
-  int par = 0;
   block_min1<0>(v, key, sc, par);
   const int nfs = block_sum(nf, sc.sn);
   if (threadIdx.x == 0) {
@@ -832,9 +853,11 @@ __global__ __launch_bounds__(kBlock) void integrate_kernel(const double* x0, con
 // ------------------------------------------------------------------------------------
 int lookback_blocks(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
 
+// Lanes (candidate slots) per model: the power of two >= C, at most one block (256); a
+// model's candidates beyond G run sequentially in its lanes (cpl = ceil(C / G)).
 int lookahead_group(int32_t C) {
   int G = 1;
-  while (G < C && G < 64) G <<= 1;
+  while (G < C && G < kBlock) G <<= 1;
   return G;
 }
 
@@ -846,10 +869,10 @@ int lookahead_lpm(int64_t n, int32_t C, int32_t integrator) {
   const int G = lookahead_group(C);
   if (const char* e = getenv("LLAMPC_LPM")) {     // benchmarking override
     const int v = atoi(e);
-    if (v == 1 || (v == 2 && G <= 32)) return v;
+    if (v == 1 || (v == 2 && 2 * G <= kBlock)) return v;
   }
   const int64_t lanes = n * G;
-  return (lanes <= 32768 && G <= 32) ? 2 : 1;
+  return (lanes <= 32768 && 2 * G <= kBlock) ? 2 : 1;
 }
 
 int lookahead_blocks(int64_t n, int32_t C, int lpm) {

@@ -4,3 +4,4 @@ from llampc.mpc.plan import PlanResult, plan  # noqa: F401
 from llampc.mpc.planner import ConstantSpeed  # noqa: F401
 from llampc.mpc.controller import (LLAMPC, CandidateGenerator, ExponentialSmoother,  # noqa: F401
                                    MuEstimator, update_friction, FRICTION_CASES)
+from llampc.mpc.nmpc import setupNLP  # noqa: F401

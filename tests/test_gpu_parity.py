@@ -198,12 +198,13 @@ def test_lookahead_rk4_rollout_and_cost_vs_golden(nat):
     close(traj, g["traj"], RTOL_ROLL)
 
 
-@pytest.mark.parametrize("C,H", [(1, 20), (3, 7), (64, 20), (100, 5), (130, 40)])
-def test_lookahead_candidate_group_shapes(nat, C, H):
-    """C=1 (lane per model), non-power-of-two C, C = 64 (one model per wave), C > 64 (lanes
-    loop over candidates), LDS staging on (small C*H) and off (C*H*16 > 48 KB)."""
+@pytest.mark.parametrize("C,H,N", [(1, 20, 300), (3, 7, 300), (64, 20, 300), (100, 5, 300),
+                                   (130, 40, 300), (1000, 12, 3)])
+def test_lookahead_candidate_group_shapes(nat, C, H, N):
+    """C=1 (lane per model), non-power-of-two C, C = 64 (one model per wave), 64 < C <= 256
+    (a model spans 2 or 4 waves: per-model argmin across waves in LDS), C > 256 (lanes loop
+    over candidates), LDS staging on (small C*H) and off (C*H*16 > 48 KB)."""
     from llampc.mpc import ModelBank, generate_bank
-    N = 300
     p = generate_bank(N, seed=C)
     rng = np.random.RandomState(C)
     x0 = np.array([0.2, 0.1, -0.7, 1.5, 0.02, 0.3])
@@ -536,3 +537,43 @@ def test_plan_async_two_banks(nat):
     finally:
         for b in banks + refs:
             b.close()
+
+
+def test_setupnlp_solve_sampling(nat):
+    """setupNLP.solve drop-in (sampling over the NLP transcription on the GPU): the returned
+    (umpc, fval, xmpc) are consistent with the oracle's NLP restatement — xmpc is the Euler
+    trajectory of umpc, fval its objective (nmpc.py:44-111) — umpc meets the bounds and the
+    steering-rate limits, and fval is no worse than holding uprev.  IPOPT's own optimum is
+    parity unpinned (casadi absent)."""
+    from llampc.models import Dynamic
+    from llampc.mpc.nmpc import setupNLP
+    from llampc.mpc.planner import ConstantSpeed
+    from llampc.params import ORCA
+    from llampc.tracks import ETHZ
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    p = ORCA(control="pwm")
+    H, Ts = 20, TS
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    model = Dynamic(**p)
+    nlp = setupNLP(H, Ts, Q, P, R, p, model, ETHZ())
+    track = ETHZ()
+    x0, uprev, projidx = s[:, 10].copy(), u[:, 9].copy(), 0
+    bank6 = tuple(np.array([p[k]]) for k in O.BANK_ORDER)
+    for tick in range(3):
+        xref, projidx, _ = ConstantSpeed(x0[:2], x0[3], track, H, Ts, projidx, curr_mu=0.9, scale=0.9)
+        umpc, fval, xmpc, viol = nlp.solve(x0=x0, xref=xref[:2, :], uprev=uprev)
+        assert umpc.shape == (2, H) and xmpc.shape == (6, H + 1) and viol == 0.0
+        assert np.all(umpc >= np.array(p["min_inputs"])[:, None] - 1e-15)
+        assert np.all(umpc <= np.array(p["max_inputs"])[:, None] + 1e-15)
+        dd = np.diff(np.concatenate([uprev[1:2], umpc[1]]))
+        assert np.all(np.abs(dd) <= 5.0 * Ts * (1 + 1e-12))
+        traj = O.rollout_euler_nlp(shared(), bank6, x0, umpc.T[None], Ts)
+        close(xmpc, traj[:, 0, :].T, RTOL_STEP * 10)
+        close(fval, O.mpc_cost(traj, umpc.T[None], xref, uprev, Q, R, P)[0], RTOL_ROLL)
+        hold = np.tile(uprev, (H, 1))[None]
+        jh = O.mpc_cost(O.rollout_euler_nlp(shared(), bank6, x0, hold, Ts), hold, xref, uprev, Q, R, P)[0]
+        assert fval <= jh * (1 + 1e-12)
+        xn, _ = O.sim_continuous(O.Vehicle.from_params(O.orca_params()), x0, umpc[:, :1], [0, Ts])
+        x0, uprev = xn[:, -1], umpc[:, 0].copy()
+    nlp.close()

@@ -252,3 +252,18 @@ def test_div6_correctly_rounded():
         r = F(v) - 6 * F(q)
         assert float(r) == r                       # the FMA residual is exact
         assert float(F(q) + r * y) == v / 6.0, v
+
+
+def test_setupnlp_interface_cpu():
+    """llampc.mpc.nmpc.setupNLP keeps nmpc.py:16's constructor; construction touches no
+    device (one instance per bank model, rt.py:195-202); track_cons=True is refused."""
+    from llampc.models import Dynamic
+    from llampc.mpc.nmpc import setupNLP
+    from llampc.params import ORCA
+    p = ORCA(control="pwm")
+    m = Dynamic(**p)
+    nlps = [setupNLP(20, 0.02, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, m, None) for _ in range(50)]
+    assert all(n._bank is None for n in nlps)
+    assert nlps[0].rate[0] == (None, None) and np.allclose(nlps[0].rate[1], (-0.1, 0.1))
+    with pytest.raises(NotImplementedError):
+        setupNLP(20, 0.02, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, m, None, track_cons=True)
