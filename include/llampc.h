@@ -83,6 +83,13 @@ typedef struct llampc_cost {
   int32_t reserved;
 } llampc_cost;
 
+/* Look-ahead reference.  GIVEN: one shared xref [2][H+1] (ConstantSpeed with mu-hat,
+ * rt.py:280).  RACELINE: every model tracks its own ConstantSpeed
+ * reference (planner.py:12-67) with mu_n = (Df_n + Dr_n) / (9.81 mass), evaluated on the
+ * device from the table of llampc_bank_set_raceline; xref then points to the shared start
+ * {s0 = arc length after the projection (planner.py:25-33), v0, scale, 0}. */
+enum llampc_xref_mode { LLAMPC_XREF_GIVEN = 0, LLAMPC_XREF_RACELINE = 1 };
+
 /* One tick's inputs.  Pointers are HOST pointers for llampc_plan and DEVICE pointers
  * for llampc_plan_device. */
 typedef struct llampc_plan_in {
@@ -90,7 +97,8 @@ typedef struct llampc_plan_in {
   const double* u_prev;   /* [2]  u_{t-1}                                          */
   const double* x_now;    /* [6]  x_t (look-back target, look-ahead start)          */
   const double* U;        /* [C][H][2] candidate control sequences                 */
-  const double* xref;     /* [2][H+1] reference (planner.py:12-67 output)          */
+  const double* xref;     /* [2][H+1] reference (planner.py:12-67 output); with
+                             xref_mode RACELINE: [4] {s0, v0, scale, 0} (see below)  */
   const double* uprev;    /* [2]  last applied input for du_0 (nmpc.py:65-66)      */
   int32_t C, H;
   int32_t K;              /* top-K size, <= LLAMPC_KMAX                            */
@@ -98,7 +106,7 @@ typedef struct llampc_plan_in {
   int32_t do_lookback;    /* 0: skip the look-back (first tick, rt.py:347)         */
   int32_t do_lookahead;   /* 0: skip the look-ahead                                */
   int32_t nan_policy;
-  int32_t reserved;
+  int32_t xref_mode;      /* LLAMPC_XREF_GIVEN (0) or LLAMPC_XREF_RACELINE (1)      */
   int64_t current_model;  /* global index used while the window fills (rt.py:264)  */
   double Ts;
   llampc_cost cost;
@@ -175,6 +183,15 @@ int llampc_lookahead(llampc_bank* bank, const double* x0, const double* U, int32
                      const llampc_cost* cost, double Ts, int32_t integrator,
                      double* cost_out, int32_t* best_cand_out, int64_t* best_model,
                      int32_t* best_cand, double* best_cost);
+
+/* Attach (replace) the raceline library used by LLAMPC_XREF_RACELINE: natural cubic
+ * splines over the arc length (pycubicspline.py:17-182, track.py:52-83): knots [n]
+ * (Spline2D.s, ascending from 0), xy [2][4][n-1] (x(s) then y(s); rows a, b, c, d per
+ * segment), speed [M][4][n-1] (one speed profile per friction), mus [M] ascending.
+ * 2 <= n <= 850 (knots and x/y rows are staged in 60 KB of LDS), 1 <= M <= 64.  Copied
+ * to the device. */
+int llampc_bank_set_raceline(llampc_bank* bank, const double* knots, int32_t n, const double* xy,
+                             const double* speed, const double* mus, int32_t M);
 
 /* ---- fused tick ------------------------------------------------------------------ */
 /* Host pointers; blocking.  err_out [n], wmean_out [n], cost_out [n][C] may be NULL. */

@@ -136,6 +136,10 @@ struct llampc_bank {
   bool timing = false;
   int64_t timing_stride = 1;       // bracket every stride-th launch
   bool async_pending = false;      // llampc_plan_async issued, llampc_plan_wait not yet
+  double* d_rl = nullptr;          // raceline table: knots | xy | speed | mus
+  int32_t rl_n = 0, rl_M = 0;
+  double* d_xref_pm = nullptr;     // per-model references [n][H][2] (RACELINE ticks)
+  size_t xref_pm_cap = 0;
   int64_t timing_seen[3] = {0, 0, 0};
 };
 
@@ -167,6 +171,19 @@ int ensure_cost(llampc_bank* b, size_t count) {
   return LLAMPC_OK;
 }
 
+int ensure_xref_pm(llampc_bank* b, const llampc_plan_in* in) {
+  if (!in->do_lookahead || in->xref_mode != LLAMPC_XREF_RACELINE) return LLAMPC_OK;
+  const size_t count = (size_t)b->n * 2 * in->H;
+  if (count <= b->xref_pm_cap) return LLAMPC_OK;
+  if (b->d_xref_pm) (void)hipFree(b->d_xref_pm);
+  b->d_xref_pm = nullptr;
+  b->xref_pm_cap = 0;
+  int rc = dev_alloc(&b->d_xref_pm, count);
+  if (rc) return rc;
+  b->xref_pm_cap = count;
+  return LLAMPC_OK;
+}
+
 int check_plan_in(const llampc_bank* b, const llampc_plan_in* in) {
   if (!in) return fail(LLAMPC_E_ARG, "plan input is NULL");
   if (in->do_lookback && (in->K < 1 || in->K > LLAMPC_KMAX))
@@ -180,6 +197,10 @@ int check_plan_in(const llampc_bank* b, const llampc_plan_in* in) {
       return fail(LLAMPC_E_ARG, "look-ahead needs x_now, U, xref and uprev");
     if (in->integrator < LLAMPC_RK4 || in->integrator > LLAMPC_RK6)
       return fail(LLAMPC_E_ARG, "unknown integrator %d", in->integrator);
+    if (in->xref_mode != LLAMPC_XREF_GIVEN && in->xref_mode != LLAMPC_XREF_RACELINE)
+      return fail(LLAMPC_E_ARG, "unknown xref_mode %d", in->xref_mode);
+    if (in->xref_mode == LLAMPC_XREF_RACELINE && !b->d_rl)
+      return fail(LLAMPC_E_STATE, "xref_mode RACELINE needs llampc_bank_set_raceline first");
     if ((b->n + 1) * (int64_t)in->C <= 0 || b->n > INT64_MAX / std::max(1, in->C) - 1)
       return fail(LLAMPC_E_ARG, "n*C overflows");
   }
@@ -221,6 +242,7 @@ void timing_free(llampc_bank* b) {
 // Advances the window bookkeeping when a look-back runs.
 int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out, double* d_err,
                 double* d_wmean, double* d_cost, hipStream_t s) {
+  if (int rc = ensure_xref_pm(b, &in)) return rc;
   const bool lb = in.do_lookback != 0;
   const bool la = in.do_lookahead != 0;
   int32_t count = b->count;
@@ -272,6 +294,17 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
     lal.pv = b->d_pv;
     lal.pidx = b->d_pidx;
     lal.pnf = b->d_pnf;
+    lal.xref_mode = in.xref_mode;
+    if (in.xref_mode == LLAMPC_XREF_RACELINE) {
+      const size_t m = (size_t)b->rl_n - 1;
+      lal.rl.knots = b->d_rl;
+      lal.rl.xy = b->d_rl + b->rl_n;
+      lal.rl.speed = lal.rl.xy + 8 * m;
+      lal.rl.mus = lal.rl.speed + 4 * m * b->rl_M;
+      lal.rl.n = b->rl_n;
+      lal.rl.M = b->rl_M;
+      lal.xref_pm = b->d_xref_pm;       // sized by ensure_xref_pm before the launch
+    }
   }
   FinalLaunch f{};
   f.out = d_out;
@@ -318,7 +351,12 @@ int stage_inputs(llampc_bank* b, const llampc_plan_in* in, llampc_plan_in* dev_i
   if (in->x_now) std::memcpy(h + 8, in->x_now, 6 * sizeof(double));
   if (in->uprev) std::memcpy(h + 14, in->uprev, 2 * sizeof(double));
   if (in->do_lookahead) {
-    std::memcpy(h + 16, in->xref, 2 * (H + 1) * sizeof(double));
+    if (in->xref_mode == LLAMPC_XREF_RACELINE) {       // {s0, v0, scale, 0} (<= 2(H+1) slots)
+      std::memset(h + 16, 0, 2 * (H + 1) * sizeof(double));
+      std::memcpy(h + 16, in->xref, 3 * sizeof(double));
+    } else {
+      std::memcpy(h + 16, in->xref, 2 * (H + 1) * sizeof(double));
+    }
     std::memcpy(h + 16 + 2 * (H + 1), in->U, 2 * C * H * sizeof(double));
   }
   HIP_TRY(hipMemcpyAsync(b->d_in, h, total * sizeof(double), hipMemcpyHostToDevice, s));
@@ -415,7 +453,8 @@ int llampc_bank_destroy(llampc_bank* b) {
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     void* dptrs[] = {b->d_params, b->d_ring, b->d_am_val, b->d_am_idx, b->d_tk_val, b->d_tk_idx,
                      b->d_pv, b->d_pidx, b->d_pnf, b->d_best_cand, b->d_best_cost, b->d_in,
-                     b->d_out, b->d_err, b->d_wmean, b->d_cost, b->d_tickets};
+                     b->d_out, b->d_err, b->d_wmean, b->d_cost, b->d_tickets, b->d_rl,
+                     b->d_xref_pm};
     for (void* p : dptrs)
       if (p) (void)hipFree(p);
     if (b->h_in) (void)hipHostFree(b->h_in);
@@ -552,6 +591,36 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
     HIP_TRY(hipMemcpyAsync(cost_out, d_cost, (size_t)b->n * in->C * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   *out = *b->h_out;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_set_raceline(llampc_bank* b, const double* knots, int32_t n, const double* xy,
+                             const double* speed, const double* mus, int32_t M) {
+  if (!b || !knots || !xy || !speed || !mus) return fail(LLAMPC_E_ARG, "NULL argument");
+  if (n < 2 || M < 1 || M > 64) return fail(LLAMPC_E_ARG, "n=%d (>= 2) M=%d (1..64)", n, M);
+  if (raceline_lds_bytes(n) > 60 * 1024)
+    return fail(LLAMPC_E_ARG, "raceline of %d knots exceeds the 60 KB LDS stage", n);
+  for (int32_t i = 1; i < n; ++i)
+    if (!(knots[i] > knots[i - 1])) return fail(LLAMPC_E_ARG, "knots must increase (at %d)", i);
+  for (int32_t i = 1; i < M; ++i)
+    if (!(mus[i] >= mus[i - 1])) return fail(LLAMPC_E_ARG, "mus must be ascending (at %d)", i);
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  const size_t m = (size_t)n - 1;
+  const size_t total = (size_t)n + 8 * m + 4 * m * M + M;
+  if (b->d_rl) (void)hipFree(b->d_rl);
+  b->d_rl = nullptr;
+  b->rl_n = b->rl_M = 0;
+  int rc = dev_alloc(&b->d_rl, total);
+  if (rc) return rc;
+  double* d = b->d_rl;
+  HIP_TRY(hipMemcpy(d, knots, n * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d + n, xy, 8 * m * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d + n + 8 * m, speed, 4 * m * M * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d + n + 8 * m + 4 * m * M, mus, M * sizeof(double), hipMemcpyHostToDevice));
+  b->rl_n = n;
+  b->rl_M = M;
   return LLAMPC_OK;
 }
 

@@ -20,6 +20,7 @@
 #include <algorithm>
 
 #include "kernels.hpp"
+#include "raceline.hpp"
 #include "merge.hpp"
 
 namespace llampc {
@@ -287,16 +288,38 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
 // candidates c = g + j*G, j < cpl, run sequentially in its G*LPM lanes.
 //   LDS from kScratchBytes: xref as [k][2]; U as [k][c][2] when staged.
 // ------------------------------------------------------------------------------------
-template <int INTEG, bool STAGE, int LPM>
+template <int INTEG, bool STAGE, int LPM, int XM>
 __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int blk, int G, int cpl,
                                                 unsigned char* smem, const Scratch& sc) {
   LA_STAMP(blk, 0);
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);
   double* su = sx + 2 * (a.H + 1);
   const int H = a.H, C = a.C;
-  for (int e = threadIdx.x; e <= H; e += kBlock) {
-    sx[2 * e] = a.xref[e];
-    sx[2 * e + 1] = a.xref[(H + 1) + e];
+  // XM = 1 (per-model raceline reference): knots [n] and the x/y spline rows [2][4][n-1]
+  // after the (optional) U staging; a.xref holds the shared start {s0, v0, scale}
+  double* rl_knots = su + (STAGE ? 2 * C * H : 0);
+  double* rl_xy = rl_knots + a.rl.n;
+  if (XM) {
+    const int nk = a.rl.n, nxy = 8 * (a.rl.n - 1);
+    for (int e = threadIdx.x; e < nk; e += kBlock) rl_knots[e] = a.rl.knots[e];
+    for (int e = threadIdx.x; e < nxy; e += kBlock) rl_xy[e] = a.rl.xy[e];
+    __syncthreads();
+    // one thread per model of this block walks ConstantSpeed into xref_pm[m][H][2]
+    const int mpb = kBlock / (G * LPM);
+    const int64_t m = (int64_t)blk * mpb + threadIdx.x;
+    if ((int)threadIdx.x < mpb && m < a.n) {
+      const double mu = (a.params[2 * a.n + m] + a.params[5 * a.n + m]) / (9.81 * a.veh.mass);
+      RaceRef rr;
+      rr.init(a.rl, rl_knots, mu, a.xref[0], a.xref[1], a.xref[2], a.Ts);
+      double* out = a.xref_pm + m * 2 * H;
+      for (int k = 0; k < H; ++k) rr.step(a.rl, rl_knots, rl_xy, out[2 * k], out[2 * k + 1]);
+    }
+    __threadfence_block();
+  } else {
+    for (int e = threadIdx.x; e <= H; e += kBlock) {
+      sx[2 * e] = a.xref[e];
+      sx[2 * e + 1] = a.xref[(H + 1) + e];
+    }
   }
   if (STAGE) {
     for (int e = threadIdx.x; e < C * H; e += kBlock) {
@@ -355,6 +378,8 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       double track = 0.0, act = 0.0;
       double p0 = up0, p1 = up1;
       bool feas = true;
+      double xr0 = 0.0, xr1 = 0.0;
+      const double* xpm = XM ? a.xref_pm + n * 2 * H : nullptr;   // this model's reference
       for (int k = 0; k < H; ++k) {
         double ua, ud;
         if (STAGE) {
@@ -373,13 +398,20 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
         }
         const Input u = make_input_fast(ua, ud, K);
         step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K);
-        const double e0 = x[0] - sx[2 * (k + 1)], e1 = x[1] - sx[2 * (k + 1) + 1];
+        if (XM) {
+          xr0 = xpm[2 * k];
+          xr1 = xpm[2 * k + 1];
+        } else {
+          xr0 = sx[2 * (k + 1)];
+          xr1 = sx[2 * (k + 1) + 1];
+        }
+        const double e0 = x[0] - xr0, e1 = x[1] - xr1;
         track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
         act = act + (d0 * (q.R[0] * d0 + q.R[1] * d1) + d1 * (q.R[2] * d0 + q.R[3] * d1));
         p0 = ua;
         p1 = ud;
       }
-      const double e0 = x[0] - sx[2 * H], e1 = x[1] - sx[2 * H + 1];   // nmpc.py:48
+      const double e0 = x[0] - xr0, e1 = x[1] - xr1;                   // nmpc.py:48 (xref_H)
       const double term = e0 * (q.P[0] * e0 + q.P[1] * e1) + e1 * (q.P[2] * e0 + q.P[3] * e1);
       double J = (term + track) + act;                                // nmpc.py:111
       if (!feas) J = __builtin_inf();
@@ -637,7 +669,7 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
 // (lb_final) while look-ahead blocks still run; the last block overall completes the
 // llampc_plan_out record (final_select).
 // ------------------------------------------------------------------------------------
-template <int INTEG, bool STAGE, int LPM>
+template <int INTEG, bool STAGE, int LPM, int XM>
 __global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
                                                       FinalLaunch fin, int G, int cpl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -648,7 +680,7 @@ __global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, Lookahe
     if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
     if (fin.full) lb_final(fin, smem, sc);
   } else {
-    lookahead_block<INTEG, STAGE, LPM>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
+    lookahead_block<INTEG, STAGE, LPM, XM>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
   }
   const unsigned expected = (unsigned)fin.nb_la + (fin.nb_lb > 0 ? 1u : 0u);
   if (!ticket_last(&fin.tickets[1], expected, flag)) return;
@@ -882,6 +914,8 @@ int lookahead_blocks(int64_t n, int32_t C, int lpm) {
 
 constexpr size_t kStageLimit = 48 * 1024;
 
+size_t raceline_lds_bytes(int32_t n) { return 8 * (size_t)n + 64 * (size_t)(n - 1); }
+
 size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u) {
   const size_t base = kScratchBytes + 16 * (size_t)(H + 1);
   const size_t ub = 16 * (size_t)C * H;
@@ -901,8 +935,12 @@ int lookback_blocks_r(int64_t n, int R) { return (int)((n + (int64_t)kBlock * R 
 template <int INTEG, bool STAGE, int LPM>
 static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
                           int G, int cpl, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, LPM>), dim3(f.nb_lb + f.nb_la), dim3(kBlock), lds, s,
-                     lb, la, f, G, cpl);
+  if (la.xref_mode == LLAMPC_XREF_RACELINE)
+    hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, LPM, 1>), dim3(f.nb_lb + f.nb_la), dim3(kBlock), lds, s,
+                       lb, la, f, G, cpl);
+  else
+    hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, LPM, 0>), dim3(f.nb_lb + f.nb_la), dim3(kBlock), lds, s,
+                       lb, la, f, G, cpl);
 }
 
 template <int INTEG, bool STAGE>
@@ -934,7 +972,12 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
     integ = la->integrator;
     lpm = lookahead_lpm(la->n, la->C, integ);
     f.nb_la = lookahead_blocks(la->n, la->C, lpm);
-    lds = std::max(lds, lookahead_lds_bytes(la->C, la->H, &stage));
+    if (la->xref_mode == LLAMPC_XREF_RACELINE) {  // knots + x/y rows in LDS; U from global
+      stage = false;
+      lds = std::max(lds, kScratchBytes + 16 * (size_t)(la->H + 1) + raceline_lds_bytes(la->rl.n));
+    } else {
+      lds = std::max(lds, lookahead_lds_bytes(la->C, la->H, &stage));
+    }
   }
   f.do_lb = lb != nullptr;
   f.do_la = la != nullptr;

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "dyn.hpp"
+#include "raceline.hpp"
 #include "llampc.h"
 
 namespace llampc {
@@ -44,6 +45,9 @@ struct LookaheadLaunch {
   double* cost_out;                      // [n][C] or null
   int32_t* best_cand;  double* best_cost; // [n]
   double* pv;  int64_t* pidx;  int32_t* pnf;  // [blocks]
+  int32_t xref_mode;                     // LLAMPC_XREF_*; RACELINE: xref = {s0, v0, scale}
+  RacelineK rl;
+  double* xref_pm;                       // RACELINE: per-model reference [n][H][2]
 };
 
 // What the ticket winners of the plan launch need (see plan_kernel).
@@ -63,6 +67,7 @@ int lookahead_group(int32_t C);
 int lookahead_lpm(int64_t n, int32_t C, int32_t integrator);
 int lookahead_blocks(int64_t n, int32_t C, int lpm);
 size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u);
+size_t raceline_lds_bytes(int32_t n);
 
 // The whole tick in ONE launch: look-back blocks (if lb), look-ahead blocks (if la), and
 // the completion stages run by ticket winners; writes f.out.  f.nb_* / f.do_* are set here.

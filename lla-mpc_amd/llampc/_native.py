@@ -18,6 +18,7 @@ WMAX = 128
 RK4, EULER_NLP, RK6 = 0, 1, 2
 INTEGRATORS = {"rk4": RK4, "euler_nlp": EULER_NLP, "rk6": RK6}
 NAN_FIRST, NAN_IGNORE = 0, 1
+XREF_GIVEN, XREF_RACELINE = 0, 1
 OP_FORCES, OP_DERIV = 0, 1
 E_ARG, E_HIP, E_NODEV, E_STATE, E_OOM = -1, -2, -3, -4, -5
 
@@ -49,7 +50,7 @@ class PlanIn(C.Structure):
     _fields_ = [("x_prev", _dp), ("u_prev", _dp), ("x_now", _dp), ("U", _dp), ("xref", _dp),
                 ("uprev", _dp), ("C", C.c_int32), ("H", C.c_int32), ("K", C.c_int32),
                 ("integrator", C.c_int32), ("do_lookback", C.c_int32), ("do_lookahead", C.c_int32),
-                ("nan_policy", C.c_int32), ("reserved", C.c_int32), ("current_model", C.c_int64),
+                ("nan_policy", C.c_int32), ("xref_mode", C.c_int32), ("current_model", C.c_int64),
                 ("Ts", C.c_double), ("cost", Cost)]
 
 
@@ -79,6 +80,7 @@ _SIGNATURES = {
     "llampc_bank_reset": (C.c_int, [C.c_void_p]),
     "llampc_bank_window": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int32)]),
     "llampc_bank_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "llampc_bank_set_raceline": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, _dp, _dp, C.c_int32]),
     "llampc_plan_async": (C.c_int, [C.c_void_p, C.c_void_p]),
     "llampc_plan_wait": (C.c_int, [C.c_void_p, C.c_void_p]),
     "llampc_bank_timing": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),

@@ -164,8 +164,20 @@ class ModelBank:
         return dict(best_model=bm.value, best_cand=bcand.value, best_cost=bcost.value, costs=costs,
                     best_cand_per_model=bc)
 
+    def set_raceline(self, track):
+        """Attach ``track``'s raceline library (llampc_bank_set_raceline) for
+        xref_mode='raceline' ticks: every model then tracks its own ConstantSpeed reference
+        with mu_n = (Df_n + Dr_n) / (9.81 m) (SURVEY.md §8f #1)."""
+        knots, xy, speed, mus = track.device_table()
+        nat.check(nat.load().llampc_bank_set_raceline(self.handle, nat.dptr(knots), len(knots), nat.dptr(xy),
+                                                      nat.dptr(speed), nat.dptr(mus), len(mus)))
+        self.raceline = track
+
     def _plan_in(self, x_prev, u_prev, x_now, U, xref, uprev, Ts, K, integrator, do_lookback,
-                 do_lookahead, current_model, nan_policy, cost):
+                 do_lookahead, current_model, nan_policy, cost, raceline_start=None):
+        """raceline_start = (s0, v0, scale): xref_mode RACELINE (xref is then unused)."""
+        if raceline_start is not None:
+            xref = np.array([*map(float, raceline_start), 0.0])
         U = nat.f64(U)
         if U.ndim == 2:
             U = U.reshape(1, *U.shape)
@@ -181,14 +193,17 @@ class ModelBank:
         pin.current_model = int(current_model)
         pin.Ts = float(Ts)
         pin.cost = cost if cost is not None else nat.cost_struct()
+        pin.xref_mode = nat.XREF_RACELINE if raceline_start is not None else nat.XREF_GIVEN
         return pin, keep
 
     def plan_raw(self, x_prev, u_prev, x_now, U, xref, uprev, Ts=0.02, K=10, integrator="rk4",
                  do_lookback=True, do_lookahead=True, current_model=0, nan_policy=nat.NAN_FIRST,
-                 cost=None, return_errors=False, return_window_mean=False, return_costs=False):
+                 cost=None, return_errors=False, return_window_mean=False, return_costs=False,
+                 raceline_start=None):
         """The fused tick (llampc_plan): returns (PlanOut, errors, window_mean, costs)."""
         pin, keep = self._plan_in(x_prev, u_prev, x_now, U, xref, uprev, Ts, K, integrator,
-                                  do_lookback, do_lookahead, current_model, nan_policy, cost)
+                                  do_lookback, do_lookahead, current_model, nan_policy, cost,
+                                  raceline_start)
         C_ = pin.C
         err = np.empty(self.n) if return_errors else None
         wm = np.empty(self.n) if return_window_mean else None
@@ -200,12 +215,13 @@ class ModelBank:
 
     def plan_async(self, x_prev, u_prev, x_now, U, xref, uprev, Ts=0.02, K=10, integrator="rk4",
                    do_lookback=True, do_lookahead=True, current_model=0, nan_policy=nat.NAN_FIRST,
-                   cost=None):
+                   cost=None, raceline_start=None):
         """Enqueue one tick (llampc_plan_async): inputs are staged before return, the tick
         runs on the bank's stream; ``plan_wait()`` returns its PlanOut.  Independent banks
         (e.g. one per track) overlap on the device."""
         pin, keep = self._plan_in(x_prev, u_prev, x_now, U, xref, uprev, Ts, K, integrator,
-                                  do_lookback, do_lookahead, current_model, nan_policy, cost)
+                                  do_lookback, do_lookahead, current_model, nan_policy, cost,
+                                  raceline_start)
         nat.check(nat.load().llampc_plan_async(self.handle, nat.C.byref(pin)))
 
     def plan_wait(self):

@@ -61,11 +61,13 @@ def result_from_out(o: nat.PlanOut, U=None, **extra) -> PlanResult:
 def plan(bank: ModelBank, x_t, u_prev, x_prev, xref, U_cand, uprev=None, Ts=0.02, K=10,
          current_model=0, integrator="rk4", cost=None, nan_policy=nat.NAN_FIRST,
          do_lookback=True, return_errors=False, return_window_mean=False,
-         return_costs=False) -> PlanResult:
+         return_costs=False, raceline_start=None) -> PlanResult:
     """One tick.  x_t [6]; (x_prev [6], u_prev [2]) the previous transition (pass
     do_lookback=False on the first tick, rt.py:347); xref [2, H+1]; U_cand [C, H, 2];
     uprev [2] is the input applied last (defaults to u_prev), used for du_0
-    (nmpc.py:65-66); current_model is used while the window fills (rt.py:264)."""
+    (nmpc.py:65-66); current_model is used while the window fills (rt.py:264).
+    raceline_start = (s0, v0, scale) (planner.raceline_start, the bank's set_raceline track):
+    per-model references from the device raceline lookup instead of the shared xref."""
     U = np.asarray(U_cand, dtype=np.float64)
     if U.ndim == 2:
         U = U[None]
@@ -74,7 +76,8 @@ def plan(bank: ModelBank, x_t, u_prev, x_prev, xref, U_cand, uprev=None, Ts=0.02
         x_prev if do_lookback else np.zeros(6), u_prev if do_lookback else np.zeros(2), x_t, U, xref,
         uprev, Ts=Ts, K=K, integrator=integrator, do_lookback=do_lookback, do_lookahead=True,
         current_model=current_model, nan_policy=nan_policy, cost=cost, return_errors=return_errors,
-        return_window_mean=return_window_mean, return_costs=return_costs)
+        return_window_mean=return_window_mean, return_costs=return_costs,
+        raceline_start=raceline_start)
     return result_from_out(o, U, lookback_err=err,
                            window_mean=wm if (wm is not None and o.window_full) else None,
                            costs=costs)

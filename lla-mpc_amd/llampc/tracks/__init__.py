@@ -34,6 +34,14 @@ class Raceline:
         # (rt.py:287 uses 656 for ETHZ; 440 for ETHZMobil, rt.py:288 / nrt_avg_runs.py:354)
         self.lap_projidx = {"ETHZ": 656, "ETHZMobil": 440}.get(name, self.raceline.shape[1] - 44)
 
+    def device_table(self):
+        """(knots [n], xy [2, 4, n-1], speed [M, 4, n-1], mus [M]) for
+        llampc_bank_set_raceline: the raceline and speed-profile spline coefficients."""
+        knots = np.asarray(self.spline.s, dtype=np.float64)
+        xy = np.stack([self.spline.sx.coefficients(), self.spline.sy.coefficients()])
+        speed = np.stack([sp.coefficients() for sp in self.spline_v])
+        return knots, np.ascontiguousarray(xy), np.ascontiguousarray(speed), np.asarray(self.mus, dtype=np.float64)
+
     def project_fast(self, x, y, raceline):
         """track.py:147-160: nearest segment of the polyline ``raceline`` [2, m]."""
         proj, dist = project_segments(np.array([x, y], dtype=np.float64), raceline[:, :-1], raceline[:, 1:])

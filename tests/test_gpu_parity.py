@@ -577,3 +577,47 @@ def test_setupnlp_solve_sampling(nat):
         xn, _ = O.sim_continuous(O.Vehicle.from_params(O.orca_params()), x0, umpc[:, :1], [0, Ts])
         x0, uprev = xn[:, -1], umpc[:, 0].copy()
     nlp.close()
+
+
+@pytest.mark.parametrize("track_name,start", [("ETHZ", "projected"), ("ETHZ", "lap_end"), ("ETHZMobil", "projected")])
+def test_lookahead_raceline_per_model_xref(nat, track_name, start):
+    """xref_mode RACELINE: every model's look-ahead tracks its own
+    ConstantSpeed reference with mu_n = (Df_n + Dr_n) / (9.81 m), evaluated on the device
+    from the raceline splines — against the oracle's ConstantSpeed loop (planner.py:34-65,
+    pinned by tests/golden/planner.npz) per model.  Wide bank: mu_n below, inside and above
+    the profile range; 'lap_end' starts 3 cm before the lap length (the mod-L wrap)."""
+    from llampc.mpc import ModelBank, generate_bank, plan
+    from llampc.mpc.planner import raceline_start
+    from llampc.tracks import ETHZ, ETHZMobil
+    tr = ETHZ() if track_name == "ETHZ" else ETHZMobil()
+    td = np.load(os.path.join(os.path.dirname(__file__), "..", "lla-mpc_amd", "llampc", "tracks", "data", "tracks.npz"))
+    ref = O.RacelineRef(td[f"{track_name}_x"], td[f"{track_name}_y"], td[f"{track_name}_speeds"], td[f"{track_name}_mus"])
+    N, C, H, scale = 192, 2, 20, 0.9
+    p = generate_bank(N, seed=21, sigma=0.45)
+    d = golden("dyn_slice.npz")
+    x0 = d["states"][:, 30].copy()
+    if track_name == "ETHZMobil":
+        x0[:3] = [tr.x_init, tr.y_init, tr.psi_init]
+    rng = np.random.RandomState(4)
+    U = np.stack([rng.uniform(0.2, 0.8, (C, H)), rng.uniform(-0.2, 0.2, (C, H))], axis=-1)
+    uprev = U[0, 0]
+    if start == "lap_end":
+        s0 = float(tr.length) - 0.03
+    else:
+        s0, _ = raceline_start(x0, tr, 0)
+    v0 = float(x0[3])
+    mass = O.orca_params()["mass"]
+    mu = (p[2] + p[5]) / (9.81 * mass)
+    assert mu.min() < ref.mus[0] and mu.max() > ref.mus[-1]
+    traj = O.rollout_rk4(shared(), tuple(p), x0, U, TS)
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    cref = np.empty((N, C))
+    for n in range(N):
+        xr, _ = O.constant_speed_from(s0, x0[:2], v0, ref, H, TS, scale, mu[n])
+        cref[n] = O.mpc_cost(traj[:, n * C:(n + 1) * C], U, xr, uprev, Q, R, P)
+    with ModelBank(p, device=0) as b:
+        b.set_raceline(tr)
+        res = plan(b, x0, uprev, x0, None, U, uprev=uprev, Ts=TS, do_lookback=False,
+                   return_costs=True, raceline_start=(s0, v0, scale))
+    close(res.costs, cref, RTOL_ROLL)
+    assert res.global_best[0] * C + res.global_best[1] == int(np.argmin(np.where(np.isnan(cref), np.inf, cref).ravel()))
