@@ -347,7 +347,7 @@ __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::F
 // One look-ahead step on the fast path.
 //  RK4 (rk6.py:58-66): the four stages as a (not unrolled) loop over ONE rhs_fast, with
 //    the stage combinations as FMAs by per-stage weights — the same roundings as rk4_step:
-//    acc = k | acc + 2k (fma(w, k, acc * wb), wb in {0, 1}), y = x + k/2 | x + k
+//    acc = k | acc + 2k (fma(w, k, acc) from acc = 0, w in {1, 2}), y = x + k/2 | x + k
 //    (fma(c, k, x), c in {1/2, 1}); the final sum divided by 6 through fm::div6
 //    (correctly rounded, = x / 6.0).
 //  NLP Euler (nmpc.py:58-60): x + Ts f_nlp(x, u).
@@ -367,12 +367,12 @@ __device__ __forceinline__ void step_fast(const VehK& v, const Tire& t, const St
     for (int st = 0;; ++st) {
       rhs_fast<Form::Ref, LPM>(v, t, sk, y, u, d, K);
       if (st == 3) break;
-      const double w = st == 0 ? 1.0 : 2.0, wb = st == 0 ? 0.0 : 1.0;
+      const double w = st == 0 ? 1.0 : 2.0;       // acc = 0 + 1*k (= k exactly), acc + 2k
       const double c = st == 2 ? 1.0 : 0.5;
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const double k = h * d[i];
-        acc[i] = fma(w, k, acc[i] * wb);
+        acc[i] = fma(w, k, acc[i]);
         y[i] = fma(c, k, x[i]);
       }
     }

@@ -286,7 +286,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
 // Look-ahead body.  Lane layout inside a block: sub = lane % LPM (LPM = 2: the lane pair
 // of one rollout, front/rear chain), cl = lane / LPM; G candidate-lanes per model (power of two); a model's
 // candidates c = g + j*G, j < cpl, run sequentially in its G*LPM lanes.
-//   LDS from kScratchBytes: xref as [k][2]; U as [k][c][2] when staged.
+//   LDS from kScratchBytes: xref as [k][2]; U as [k][c][4] (pwm, delta, sin, cos) when staged.
 // ------------------------------------------------------------------------------------
 template <int INTEG, bool STAGE, int LPM, int XM>
 __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int blk, int G, int cpl,
@@ -297,7 +297,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   const int H = a.H, C = a.C;
   // XM = 1 (per-model raceline reference): knots [n] and the x/y spline rows [2][4][n-1]
   // after the (optional) U staging; a.xref holds the shared start {s0, v0, scale}
-  double* rl_knots = su + (STAGE ? 2 * C * H : 0);
+  double* rl_knots = su + (STAGE ? 4 * C * H : 0);
   double* rl_xy = rl_knots + a.rl.n;
   if (XM) {
     const int nk = a.rl.n, nxy = 8 * (a.rl.n - 1);
@@ -322,10 +322,21 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     }
   }
   if (STAGE) {
+    // [k][c] -> (pwm, delta, sin delta, cos delta): the steering's sincos depends only on the
+    // shared candidates, so it is formed once per block here (same evaluation as
+    // make_input_fast: the fast core on its domain, the general function off it)
+    const fm::FmK K = fm::FmK::load();
     for (int e = threadIdx.x; e < C * H; e += kBlock) {
       const int c = e / H, k = e - c * H;
-      su[2 * (k * C + c)] = a.U[2 * e];
-      su[2 * (k * C + c) + 1] = a.U[2 * e + 1];
+      const double dl = a.U[2 * e + 1];
+      double sd, cd;
+      if (fm::sincos_fast_ok(dl)) fm::sincos_fast(dl, &sd, &cd, K);
+      else LL_SINCOS(dl, &sd, &cd);
+      double* o = su + 4 * (k * C + c);
+      o[0] = a.U[2 * e];
+      o[1] = dl;
+      o[2] = sd;
+      o[3] = cd;
     }
   }
   __syncthreads();
@@ -382,12 +393,19 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       const double* xpm = XM ? a.xref_pm + n * 2 * H : nullptr;   // this model's reference
       for (int k = 0; k < H; ++k) {
         double ua, ud;
+        Input u;
         if (STAGE) {
-          ua = su[2 * (k * C + c)];
-          ud = su[2 * (k * C + c) + 1];
+          const double* o = su + 4 * (k * C + c);
+          ua = o[0];
+          ud = o[1];
+          u.a = ua;
+          u.d = ud;
+          u.sd = o[2];
+          u.cd = o[3];
         } else {
           ua = a.U[2 * ((int64_t)c * H + k)];
           ud = a.U[2 * ((int64_t)c * H + k) + 1];
+          u = make_input_fast(ua, ud, K);
         }
         const double d0 = ua - p0, d1 = ud - p1;          // nmpc.py:65-68
         if (q.enforce) {                                  // nmpc.py:102-105
@@ -396,7 +414,6 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
           if (q.dmax[0] >= 0) feas = feas && d0 <= q.dmax[0] && -d0 <= q.dmax[0];
           if (q.dmax[1] >= 0) feas = feas && d1 <= q.dmax[1] && -d1 <= q.dmax[1];
         }
-        const Input u = make_input_fast(ua, ud, K);
         step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K);
         if (XM) {
           xr0 = xpm[2 * k];
@@ -918,7 +935,7 @@ size_t raceline_lds_bytes(int32_t n) { return 8 * (size_t)n + 64 * (size_t)(n - 
 
 size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u) {
   const size_t base = kScratchBytes + 16 * (size_t)(H + 1);
-  const size_t ub = 16 * (size_t)C * H;
+  const size_t ub = 32 * (size_t)C * H;           // (pwm, delta, sin delta, cos delta)
   *stage_u = base + ub <= kStageLimit;
   return *stage_u ? base + ub : base;
 }
