@@ -92,6 +92,16 @@ def make_ticks(args, T, seed=0):
 _DEV = [0]
 
 
+def max_over_ranks(x: float) -> float:
+    """MAX of a host scalar over the process group (device tensor under nccl, host under gloo)."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", _DEV[0]) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def torch_device_index():
     return _DEV[0]
 
@@ -141,10 +151,18 @@ def main():
         world = int(os.environ.get("WORLD_SIZE", "1"))
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
-    _DEV[0] = local
+    # LLAMPC_DIST_BACKEND=gloo + LLAMPC_SAME_DEVICE=1: rehearsal of the N-rank flow on a
+    # one-GPU box (records gathered over gloo on the host, merged by the same device kernel)
+    backend = os.environ.get("LLAMPC_DIST_BACKEND", "nccl")
+    dev_index = 0 if os.environ.get("LLAMPC_SAME_DEVICE") else local
+    torch.cuda.set_device(dev_index)
+    _DEV[0] = dev_index
+    local = dev_index
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     from llampc import _native as nat
     from llampc.mpc import generate_bank
     from llampc.mpc.sharded import ShardedBank
@@ -183,9 +201,7 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+        el = max_over_ranks(el)
     ms = el / args.steps * 1e3
 
     avg = (ctypes.c_double * 3)()
@@ -198,8 +214,8 @@ def main():
     merged = sb.fetch(stream)          # result of the last tick (all ranks identical)
 
     extra = {}
-    if not args.no_extra and rank == 0:
-        extra = extras(args, sb, stream, world)
+    if not args.no_extra:              # every rank: the C=64 extra ticks run the collective
+        extra = extras(args, sb, stream, world, rank)
 
     if rank == 0:
         steps_per_tick = N_total * C * H + N_total
@@ -249,9 +265,10 @@ def main():
         dist.destroy_process_group()
 
 
-def extras(args, sb, stream, world):
-    """Rank-0 extras: C=64 throughput on the same bank, and synchronous per-tick latency
-    through the host-pointer API (PCIe-inclusive; never the headline value)."""
+def extras(args, sb, stream, world, rank=0):
+    """Extras reported by rank 0: C=64 throughput on the same bank (run on EVERY rank — each
+    tick includes the all-gather), and, at world 1, synchronous per-tick latency through the
+    host-pointer API and BASELINE config 5 (PCIe-inclusive; never the headline value)."""
     import torch
     out = {}
     H = args.H
@@ -270,6 +287,8 @@ def extras(args, sb, stream, world):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / n * 1e3
     Nt = args.n_per_gpu * world
+    if world > 1:
+        ms = max_over_ranks(ms)
     out["C64"] = {"ms_per_step": ms, "value": (Nt * 64 * H + Nt) / (ms / 1e3)}
     if world == 1:
         pk = make_ticks(args, 1)[0]

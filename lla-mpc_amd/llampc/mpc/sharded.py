@@ -110,8 +110,15 @@ class ShardedBank:
                                          None, None, None, s.cuda_stream))
         if self.world > 1:
             import torch.distributed as dist
-            with torch.cuda.stream(s):
-                dist.all_gather_into_tensor(self.d_all, self.d_local, group=self.group)
+            if self.backend == "nccl":
+                with torch.cuda.stream(s):
+                    dist.all_gather_into_tensor(self.d_all, self.d_local, group=self.group)
+            else:                          # gloo (CPU rehearsal): gather on the host
+                s.synchronize()
+                parts = [torch.empty(nat.PLAN_OUT_BYTES, dtype=torch.uint8) for _ in range(self.world)]
+                dist.all_gather(parts, self.d_local.cpu(), group=self.group)
+                with torch.cuda.stream(s):
+                    self.d_all.copy_(torch.cat(parts).to(self.d_all.device), non_blocking=False)
             nat.check(lib.llampc_merge_device(self.d_all.data_ptr(), self.world, pin.nan_policy,
                                               self.d_merged.data_ptr(), self.device, s.cuda_stream))
         return s
