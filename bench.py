@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--W", type=int, default=10)
     ap.add_argument("--K", type=int, default=10)
     ap.add_argument("--track", default="ETHZ", choices=["ETHZ", "ETHZMobil"])
+    ap.add_argument("--scenario", default=None, choices=["gradual", "sudden"],
+                    help="friction change of the tick inputs (default: gradual on ETHZ, sudden on "
+                         "ETHZMobil, BASELINE configs 2/3)")
     ap.add_argument("--ticks", type=int, default=64, help="distinct resident tick inputs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -70,8 +73,12 @@ def make_ticks(args, T, seed=0):
     track = ETHZ() if args.track == "ETHZ" else ETHZMobil()
     gen = CandidateGenerator(args.C, args.H, seed=2)
     H, Ts = args.H, 0.02
-    k0 = 100                                    # ticks into the decay
-    Df, Dr = p["Df"] * (1 - 1 / 2600.) ** k0, p["Dr"] * (1 - 1 / 2600.) ** k0
+    scenario = getattr(args, "scenario", None) or ("sudden" if args.track == "ETHZMobil" else "gradual")
+    if scenario == "gradual":
+        k0 = 100                                # ticks into the decay
+        Df, Dr = p["Df"] * (1 - 1 / 2600.) ** k0, p["Dr"] * (1 - 1 / 2600.) ** k0
+    else:                                       # config 3: the 9-tick drop x21/22 (rt.py:132-141)
+        Df, Dr = p["Df"], p["Dr"]
     packs, projidx = [], 0
     for t in range(T + 1):
         u = u_rec[:, t % u_rec.shape[1]]
@@ -84,8 +91,12 @@ def make_ticks(args, T, seed=0):
             U = gen(None, u)
             packs.append(np.concatenate([x, u, x_next, u, xref.ravel(), U.ravel()]))
         x = x_next
-        Df -= Df / 2600.
-        Dr -= Dr / 2600.
+        if scenario == "gradual":
+            Df -= Df / 2600.
+            Dr -= Dr / 2600.
+        elif 2 <= t < 11:                       # nine ticks of D -= D/22 (rt.py:132-140)
+            Df -= Df / 22.
+            Dr -= Dr / 22.
     return np.stack(packs[:T])
 
 
@@ -238,10 +249,11 @@ def main():
             "value": value, "unit": "model-rollout-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (RK6-plant states under gradual friction decay, recorded ETHZ controls, "
+            "data": "synthetic (RK6-plant states under the friction change of config.workload, recorded ETHZ controls, "
                     "ConstantSpeed xref; seeded Pacejka bank)",
             "config": {"workload": f"{args.track} LLA-MPC tick: look-back W={W} K={K} + look-ahead H={H} "
-                                   f"C={C}, gradual friction", "N_models_total": N_total,
+                                   f"C={C}, {args.scenario or ('sudden' if args.track == 'ETHZMobil' else 'gradual')} friction",
+                       "N_models_total": N_total,
                        "N_models_per_gpu": N_local, "H": H, "C": C, "W": W, "K": K, "Ts": 0.02,
                        "track": args.track, "parallelism": f"bank-shard x{world}" + (" + 1 RCCL all-gather/tick" if world > 1 else "")},
             "roofline": roof,

@@ -267,3 +267,23 @@ def test_setupnlp_interface_cpu():
     assert nlps[0].rate[0] == (None, None) and np.allclose(nlps[0].rate[1], (-0.1, 0.1))
     with pytest.raises(NotImplementedError):
         setupNLP(20, 0.02, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, m, None, track_cons=True)
+
+
+def test_raceline_npz_reader_reference_format(tmp_path):
+    """Raceline.from_raceline_npz reads the reference's raceline file layout
+    (ethz.py:59-96 keys x, y, speed, time, speeds, mus) into the same splines and device
+    tables as the packaged library; a file without ``speeds`` gets one profile."""
+    from llampc.tracks import ETHZ, Raceline
+    ref = ETHZ()
+    n = ref.raceline.shape[1]
+    f = tmp_path / "ethz_raceline_long_.npz"
+    np.savez(f, x=ref.x_raceline, y=ref.y_raceline, speed=ref.v_raceline[0], time=np.arange(n) * 0.02,
+             speeds=ref.v_raceline, mus=ref.mus)
+    tr = Raceline.from_raceline_npz(f, name="ETHZ", track_width=0.37, psi_init=-np.pi / 4, lap_projidx=656)
+    for a, b in zip(tr.device_table(), ref.device_table()):
+        np.testing.assert_array_equal(a, b)
+    assert tr.length == ref.length and tr.lap_projidx == 656
+    f2 = tmp_path / "single.npz"
+    np.savez(f2, x=ref.x_raceline, y=ref.y_raceline, speed=ref.v_raceline[3], time=np.arange(n) * 0.02)
+    one = Raceline.from_raceline_npz(f2)
+    assert one.v_raceline.shape == (1, n) and list(one.mus) == [1.0]
