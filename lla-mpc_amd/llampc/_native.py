@@ -47,8 +47,11 @@ _dp = C.POINTER(C.c_double)
 
 
 class PlanIn(C.Structure):
-    _fields_ = [("x_prev", _dp), ("u_prev", _dp), ("x_now", _dp), ("U", _dp), ("xref", _dp),
-                ("uprev", _dp), ("C", C.c_int32), ("H", C.c_int32), ("K", C.c_int32),
+    # the pointer members are declared void* (same C layout as llampc_plan_in's const
+    # double*): the host assigns raw addresses, which is ~10x cheaper than ctypes casts
+    _fields_ = [("x_prev", C.c_void_p), ("u_prev", C.c_void_p), ("x_now", C.c_void_p),
+                ("U", C.c_void_p), ("xref", C.c_void_p), ("uprev", C.c_void_p),
+                ("C", C.c_int32), ("H", C.c_int32), ("K", C.c_int32),
                 ("integrator", C.c_int32), ("do_lookback", C.c_int32), ("do_lookahead", C.c_int32),
                 ("nan_policy", C.c_int32), ("xref_mode", C.c_int32), ("current_model", C.c_int64),
                 ("Ts", C.c_double), ("cost", Cost)]
@@ -173,6 +176,17 @@ def vehicle(lf, lr, mass, Iz, Cm1, Cm2, Cr0, Cr2, input_acc=False, approx=False)
     nz = lambda v: 0.0 if v is None else float(v)
     return Vehicle(float(lf), float(lr), float(mass), float(Iz), nz(Cm1), nz(Cm2), nz(Cr0), nz(Cr2),
                    int(bool(input_acc)), int(bool(approx)))
+
+
+_DEFAULT_COST = None
+
+
+def default_cost() -> Cost:
+    """cost_struct() with its defaults, built once (a fresh copy per call)."""
+    global _DEFAULT_COST
+    if _DEFAULT_COST is None:
+        _DEFAULT_COST = cost_struct()
+    return Cost.from_buffer_copy(_DEFAULT_COST)
 
 
 def cost_struct(Q=None, R=None, P=None, umin=(-0.1, -0.35), umax=(1.0, 0.35),

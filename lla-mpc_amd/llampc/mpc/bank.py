@@ -181,18 +181,26 @@ class ModelBank:
         U = nat.f64(U)
         if U.ndim == 2:
             U = U.reshape(1, *U.shape)
-        keep = []
-        ptr = lambda a: (keep.append(nat.f64(a)), nat.dptr(keep[-1]))[1] if a is not None else None
+        # one packed array, one address lookup (~1 us each in NumPy): pointers = base + offsets
+        parts = [np.zeros(6) if x_prev is None else x_prev, np.zeros(2) if u_prev is None else u_prev,
+                 x_now, uprev, xref, U]
+        flat = [np.asarray(a, dtype=np.float64).ravel() for a in parts]
+        pack = np.concatenate(flat)
+        keep = [pack]
+        base, off = pack.ctypes.data, 0
+        ptrs = []
+        for a in flat:
+            ptrs.append(base + 8 * off)
+            off += a.size
         pin = nat.PlanIn()
-        pin.x_prev, pin.u_prev, pin.x_now = ptr(x_prev), ptr(u_prev), ptr(x_now)
-        pin.U, pin.xref, pin.uprev = ptr(U), ptr(xref), ptr(uprev)
+        pin.x_prev, pin.u_prev, pin.x_now, pin.uprev, pin.xref, pin.U = ptrs
         pin.C, pin.H, pin.K = U.shape[0], U.shape[1], int(K)
         pin.integrator = nat.INTEGRATORS[integrator]
         pin.do_lookback, pin.do_lookahead = int(bool(do_lookback)), int(bool(do_lookahead))
         pin.nan_policy = int(nan_policy)
         pin.current_model = int(current_model)
         pin.Ts = float(Ts)
-        pin.cost = cost if cost is not None else nat.cost_struct()
+        pin.cost = cost if cost is not None else nat.default_cost()
         pin.xref_mode = nat.XREF_RACELINE if raceline_start is not None else nat.XREF_GIVEN
         return pin, keep
 

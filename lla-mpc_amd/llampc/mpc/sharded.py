@@ -85,7 +85,7 @@ class ShardedBank:
         [x_prev 6 | u_prev 2 | x_now 6 | uprev 2 | xref 2(H+1) | U 2CH] (float64)."""
         base = pack.data_ptr()
         pin = nat.PlanIn()
-        dp = lambda off: C.cast(C.c_void_p(base + 8 * off), nat._dp)
+        dp = lambda off: base + 8 * off
         pin.x_prev, pin.u_prev, pin.x_now, pin.uprev = dp(0), dp(6), dp(8), dp(14)
         pin.xref, pin.U = dp(16), dp(16 + 2 * (H + 1))
         pin.C, pin.H, pin.K = C_, H, K
@@ -94,7 +94,7 @@ class ShardedBank:
         pin.nan_policy = nan_policy
         pin.current_model = current_model
         pin.Ts = Ts
-        pin.cost = cost if cost is not None else nat.cost_struct()
+        pin.cost = cost if cost is not None else nat.default_cost()
         pin._pack = pack                   # keep the device buffer alive
         self._nan_policy = nan_policy
         return pin
