@@ -262,7 +262,8 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
   const double yy = fma(c.lw, om, c.sg * vy);
   const double a2 = fm::atan2_fast(yy, den, K);
   const double z = c.B * fma(-c.sg, a2, dsel);
-  ok = ok && fm::atan2_fast_ok(yy, den) && fm::atan_fast_ok(z);
+  // non-short-circuit: a && here compiles to a divergent branch inside the stage
+  ok = (int)ok & (int)fm::atan2_fast_ok(yy, den) & (int)fm::atan_fast_ok(z);
   return c.D * fm::sin_wide(c.C * fm::atan_fast(z, K), K);
 }
 
@@ -272,6 +273,7 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
 struct StageK {
   Chain ch[2];
   double fw;
+  double k1, k2, k0, k3;   // Frx = (k1 - k2 vx) a - k0 - k3 vx^2; input_acc: (mass, 0, 0, 0)
   bool sok;
 };
 
@@ -282,7 +284,13 @@ __device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int s
   s.ch[0] = make_chain(v, t, front);
   s.ch[1] = make_chain(v, t, false);
   s.fw = front ? 1.0 : 0.0;
-  s.sok = chain_static_ok(s.ch[0]) && ((LPM == 2) || chain_static_ok(s.ch[1]));
+  // dynamic.py:141 (input_acc: mass * a) as the :146 form with (mass, 0, 0, 0): equal for
+  // finite vx (a non-finite vx is outside the chain domain -> the general rhs)
+  s.k1 = v.input_acc ? v.mass : v.Cm1;
+  s.k2 = v.input_acc ? 0.0 : v.Cm2;
+  s.k0 = v.input_acc ? 0.0 : v.Cr0;
+  s.k3 = v.input_acc ? 0.0 : v.Cr2;
+  s.sok = chain_static_ok(s.ch[0]) && ((LPM == 2) || chain_static_ok(s.ch[1])) && !v.approx;
   return s;
 }
 
@@ -302,7 +310,7 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const Tire& t, const Sta
     vx = 0.05;
   }
   const double den = (F == Form::Ref) ? fabs(vx) : vx;
-  bool ok = sk.sok && !v.approx && fm::sincos_fast_ok(x[2]);
+  bool ok = (int)sk.sok & (int)fm::sincos_fast_ok(x[2]);   // sok includes !approx
   double Ffy, Fry;
   if (LPM == 2) {
     const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, ok, K);
@@ -317,8 +325,7 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const Tire& t, const Sta
   }
   double sp, cp;
   fm::sincos_fast(x[2], &sp, &cp, K);
-  const double Frx = v.input_acc ? v.mass * u.a
-                                 : (v.Cm1 - v.Cm2 * vx) * u.a - v.Cr0 - v.Cr2 * (vx * vx);
+  const double Frx = (sk.k1 - sk.k2 * vx) * u.a - sk.k0 - sk.k3 * (vx * vx);
   dx[0] = vx * cp - vy * sp;
   dx[1] = vx * sp + vy * cp;
   dx[2] = om;

@@ -408,11 +408,12 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
           u = make_input_fast(ua, ud, K);
         }
         const double d0 = ua - p0, d1 = ud - p1;          // nmpc.py:65-68
-        if (q.enforce) {                                  // nmpc.py:102-105
-          feas = feas && ua <= q.umax[0] && ua >= q.umin[0] && ud <= q.umax[1] &&
-                 ud >= q.umin[1];
-          if (q.dmax[0] >= 0) feas = feas && d0 <= q.dmax[0] && -d0 <= q.dmax[0];
-          if (q.dmax[1] >= 0) feas = feas && d1 <= q.dmax[1] && -d1 <= q.dmax[1];
+        if (q.enforce) {                                  // nmpc.py:102-105 (branch-free:
+          // |d| <= dmax is false for NaN like the two one-sided tests; dmax < 0 disables)
+          feas = (int)feas & (int)(ua <= q.umax[0]) & (int)(ua >= q.umin[0]) &
+                 (int)(ud <= q.umax[1]) & (int)(ud >= q.umin[1]) &
+                 ((int)(q.dmax[0] < 0) | (int)(fabs(d0) <= q.dmax[0])) &
+                 ((int)(q.dmax[1] < 0) | (int)(fabs(d1) <= q.dmax[1]));
         }
         step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K);
         if (XM) {

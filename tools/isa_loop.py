@@ -1,6 +1,7 @@
 """Instruction mix of the innermost loop(s) containing a marker instruction in one kernel
 of a hipcc -S listing (diagnostic).  usage: isa_loop.py file.s kernel_substr marker"""
 import collections
+import os
 import re
 import sys
 
@@ -27,6 +28,9 @@ for st in starts:
                 loops.append((labels[m.group(1)], i, body))
     loops.sort(key=lambda t: t[1] - t[0])
     print(name[:90], 'loops with marker:', len(loops))
+    dump = os.environ.get("ISA_DUMP")
+    if dump and loops:
+        open(dump, "w").write("\n".join(loops[0][2]))
     for lo, hi, body in loops[:3]:
         ins = [b.strip().split()[0] for b in body if b.startswith('\t') and not b.strip().startswith(('.', ';'))]
         c = collections.Counter(ins)
