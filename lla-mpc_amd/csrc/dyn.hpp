@@ -294,11 +294,13 @@ __device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int s
   return s;
 }
 
-// dx/dt on the fast path, falling back to the general rhs<F> for out-of-domain lanes.
+// dx/dt on the fast path.  No fallback here: `bad` |= "an operand of this lane left a fast
+// core's domain (or the bank uses linear tires)"; the caller re-runs such rollouts with the
+// general evaluation (lookahead_block), so the stage has no branch at all.
 template <Form F, int LPM>
-__device__ __forceinline__ void rhs_fast(const VehK& v, const Tire& t, const StageK& sk,
-                                         const double* x, const Input& u, double* dx,
-                                         const fm::FmK& K) {
+__device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const double* x,
+                                         const Input& u, double* dx, const fm::FmK& K,
+                                         bool& bad) {
   double vx = x[3], vy = x[4], om = x[5];
   double d = u.d, sd = u.sd, cd = u.cd;
   if (F == Form::Nlp && vx < 0.05) {      // dynamic.py:208-212 (vmin clamp)
@@ -316,13 +318,11 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const Tire& t, const Sta
     const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, ok, K);
     Ffy = dpp_bcast<kPair0>(r);
     Fry = dpp_bcast<kPair1>(r);
-    const int oi = ok;                    // the pair shares one state: both or neither
-    ok = __builtin_amdgcn_mov_dpp(oi, kPair0, 0xF, 0xF, false) &
-         __builtin_amdgcn_mov_dpp(oi, kPair1, 0xF, 0xF, false);
   } else {
     Ffy = chain_fast(sk.ch[0], den, vy, om, d, ok, K);
     Fry = chain_fast(sk.ch[1], den, vy, om, 0.0, ok, K);
   }
+  bad = (int)bad | (int)!ok;
   double sp, cp;
   fm::sincos_fast(x[2], &sp, &cp, K);
   const double Frx = (sk.k1 - sk.k2 * vx) * u.a - sk.k0 - sk.k3 * (vx * vx);
@@ -332,62 +332,57 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const Tire& t, const Sta
   dx[3] = v.inv_mass * (Frx - Ffy * sd) + vy * om;
   dx[4] = v.inv_mass * (Fry + Ffy * cd) - vx * om;
   dx[5] = v.inv_Iz * (Ffy * v.lf * cd - Fry * v.lr);
-  // Out-of-domain lanes (and linear-tire banks): the general evaluation.  One copy per
-  // kernel (the stage loop below is not unrolled), normally skipped wave-uniformly.
-  if (__builtin_expect(__any(!ok), 0)) {
-    if (!ok) rhs<F>(v, t, x, u, dx);
-  }
 }
 
-__device__ __forceinline__ Input make_input_fast(double a, double d, const fm::FmK& K) {
+__device__ __forceinline__ Input make_input_fast(double a, double d, const fm::FmK& K,
+                                                 bool& bad) {
   Input u;
   u.a = a;
   u.d = d;
   fm::sincos_fast(d, &u.sd, &u.cd, K);
-  const bool ok = fm::sincos_fast_ok(d);
-  if (__builtin_expect(__any(!ok), 0)) {
-    if (!ok) LL_SINCOS(d, &u.sd, &u.cd);
-  }
+  bad = (int)bad | (int)!fm::sincos_fast_ok(d);
   return u;
 }
 
 // One look-ahead step on the fast path.
-//  RK4 (rk6.py:58-66): the four stages as a (not unrolled) loop over ONE rhs_fast, with
-//    the stage combinations as FMAs by per-stage weights — the same roundings as rk4_step:
-//    acc = k | acc + 2k (fma(w, k, acc) from acc = 0, w in {1, 2}), y = x + k/2 | x + k
-//    (fma(c, k, x), c in {1/2, 1}); the final sum divided by 6 through fm::div6
-//    (correctly rounded, = x / 6.0).
+//  RK4 (rk6.py:58-66): four explicit stages with rk4_step's roundings — acc = k, acc + 2k,
+//    acc + 2k (FMAs by exact weights), y = x + k/2, x + k/2, x + k, and the final sum divided
+//    by 6 through fm::div6 (correctly rounded, = x / 6.0).
 //  NLP Euler (nmpc.py:58-60): x + Ts f_nlp(x, u).
 //  RK6 (rk6.py:13-28): the general rk6_step, one lane per rollout (LPM must be 1).
 template <int INTEG, int LPM>
 __device__ __forceinline__ void step_fast(const VehK& v, const Tire& t, const StageK& sk,
                                           double* x, const Input& u, double h,
-                                          const fm::FmK& K) {
+                                          const fm::FmK& K, bool& bad) {
   if (INTEG == 0) {
     double y[6], d[6], acc[6];
+    rhs_fast<Form::Ref, LPM>(v, sk, x, u, d, K, bad);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-      y[i] = x[i];
-      acc[i] = 0.0;
+      const double k = h * d[i];
+      acc[i] = k;
+      y[i] = fma(0.5, k, x[i]);
     }
-#pragma unroll 1
-    for (int st = 0;; ++st) {
-      rhs_fast<Form::Ref, LPM>(v, t, sk, y, u, d, K);
-      if (st == 3) break;
-      const double w = st == 0 ? 1.0 : 2.0;       // acc = 0 + 1*k (= k exactly), acc + 2k
-      const double c = st == 2 ? 1.0 : 0.5;
+    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, bad);
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const double k = h * d[i];
-        acc[i] = fma(w, k, acc[i]);
-        y[i] = fma(c, k, x[i]);
-      }
+    for (int i = 0; i < 6; ++i) {
+      const double k = h * d[i];
+      acc[i] = fma(2.0, k, acc[i]);
+      y[i] = fma(0.5, k, x[i]);
     }
+    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, bad);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double k = h * d[i];
+      acc[i] = fma(2.0, k, acc[i]);
+      y[i] = x[i] + k;
+    }
+    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, bad);
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = x[i] + fm::div6(acc[i] + h * d[i], K);
   } else if (INTEG == 1) {
     double d[6];
-    rhs_fast<Form::Nlp, LPM>(v, t, sk, x, u, d, K);
+    rhs_fast<Form::Nlp, LPM>(v, sk, x, u, d, K, bad);
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = x[i] + h * d[i];
   } else {

@@ -282,6 +282,73 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
   }
 }
 
+// One (model, candidate) rollout over H steps and its NLP objective (nmpc.py:44-111).
+// FAST: the branch-free stage (dyn.hpp step_fast); `bad` |= any operand of this lane outside
+// the fast cores' domains.  !FAST: the general evaluation (rk4_step / euler / rk6 with the
+// general transcendentals) — the re-run of bad lanes, so every lane's result depends on its
+// own operands only.  Returns J (+inf when infeasible).
+template <int INTEG, bool STAGE, int LPM, int XM, bool FAST>
+__device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64_t n,
+                                          const double* sx, const double* su, const VehK& veh,
+                                          const Tire& t, const StageK& sk, const CostK& q,
+                                          double Ts, double up0, double up1, const fm::FmK& K,
+                                          bool& bad) {
+  const int H = a.H, C = a.C;
+  double x[6];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) x[m] = a.x0[m];
+  double track = 0.0, act = 0.0;
+  double p0 = up0, p1 = up1;
+  bool feas = true;
+  double xr0 = 0.0, xr1 = 0.0;
+  const double* xpm = XM ? a.xref_pm + n * 2 * H : nullptr;   // this model's reference
+  for (int k = 0; k < H; ++k) {
+    double ua, ud;
+    Input u;
+    if (STAGE) {                        // sincos(delta) staged with the fast/general rule
+      const double* o = su + 4 * (k * C + c);
+      ua = o[0];
+      ud = o[1];
+      u.a = ua;
+      u.d = ud;
+      u.sd = o[2];
+      u.cd = o[3];
+    } else {
+      ua = a.U[2 * ((int64_t)c * H + k)];
+      ud = a.U[2 * ((int64_t)c * H + k) + 1];
+      if (FAST) u = make_input_fast(ua, ud, K, bad);
+      else u = make_input(ua, ud);
+    }
+    const double d0 = ua - p0, d1 = ud - p1;          // nmpc.py:65-68
+    if (q.enforce) {                                  // nmpc.py:102-105 (branch-free:
+      // |d| <= dmax is false for NaN like the two one-sided tests; dmax < 0 disables)
+      feas = (int)feas & (int)(ua <= q.umax[0]) & (int)(ua >= q.umin[0]) &
+             (int)(ud <= q.umax[1]) & (int)(ud >= q.umin[1]) &
+             ((int)(q.dmax[0] < 0) | (int)(fabs(d0) <= q.dmax[0])) &
+             ((int)(q.dmax[1] < 0) | (int)(fabs(d1) <= q.dmax[1]));
+    }
+    if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, bad);
+    else step<INTEG>(veh, t, x, u, Ts);
+    if (XM) {
+      xr0 = xpm[2 * k];
+      xr1 = xpm[2 * k + 1];
+    } else {
+      xr0 = sx[2 * (k + 1)];
+      xr1 = sx[2 * (k + 1) + 1];
+    }
+    const double e0 = x[0] - xr0, e1 = x[1] - xr1;
+    track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
+    act = act + (d0 * (q.R[0] * d0 + q.R[1] * d1) + d1 * (q.R[2] * d0 + q.R[3] * d1));
+    p0 = ua;
+    p1 = ud;
+  }
+  const double e0 = x[0] - xr0, e1 = x[1] - xr1;                   // nmpc.py:48 (xref_H)
+  const double term = e0 * (q.P[0] * e0 + q.P[1] * e1) + e1 * (q.P[2] * e0 + q.P[3] * e1);
+  double J = (term + track) + act;                                // nmpc.py:111
+  if (!feas) J = __builtin_inf();
+  return J;
+}
+
 // ------------------------------------------------------------------------------------
 // Look-ahead body.  Lane layout inside a block: sub = lane % LPM (LPM = 2: the lane pair
 // of one rollout, front/rear chain), cl = lane / LPM; G candidate-lanes per model (power of two); a model's
@@ -383,56 +450,17 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     for (int j = 0; j < cpl; ++j) {
       const int c = g + j * G;
       if (c >= C) break;
-      double x[6];
-#pragma unroll
-      for (int m = 0; m < 6; ++m) x[m] = a.x0[m];
-      double track = 0.0, act = 0.0;
-      double p0 = up0, p1 = up1;
-      bool feas = true;
-      double xr0 = 0.0, xr1 = 0.0;
-      const double* xpm = XM ? a.xref_pm + n * 2 * H : nullptr;   // this model's reference
-      for (int k = 0; k < H; ++k) {
-        double ua, ud;
-        Input u;
-        if (STAGE) {
-          const double* o = su + 4 * (k * C + c);
-          ua = o[0];
-          ud = o[1];
-          u.a = ua;
-          u.d = ud;
-          u.sd = o[2];
-          u.cd = o[3];
-        } else {
-          ua = a.U[2 * ((int64_t)c * H + k)];
-          ud = a.U[2 * ((int64_t)c * H + k) + 1];
-          u = make_input_fast(ua, ud, K);
-        }
-        const double d0 = ua - p0, d1 = ud - p1;          // nmpc.py:65-68
-        if (q.enforce) {                                  // nmpc.py:102-105 (branch-free:
-          // |d| <= dmax is false for NaN like the two one-sided tests; dmax < 0 disables)
-          feas = (int)feas & (int)(ua <= q.umax[0]) & (int)(ua >= q.umin[0]) &
-                 (int)(ud <= q.umax[1]) & (int)(ud >= q.umin[1]) &
-                 ((int)(q.dmax[0] < 0) | (int)(fabs(d0) <= q.dmax[0])) &
-                 ((int)(q.dmax[1] < 0) | (int)(fabs(d1) <= q.dmax[1]));
-        }
-        step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K);
-        if (XM) {
-          xr0 = xpm[2 * k];
-          xr1 = xpm[2 * k + 1];
-        } else {
-          xr0 = sx[2 * (k + 1)];
-          xr1 = sx[2 * (k + 1) + 1];
-        }
-        const double e0 = x[0] - xr0, e1 = x[1] - xr1;
-        track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
-        act = act + (d0 * (q.R[0] * d0 + q.R[1] * d1) + d1 * (q.R[2] * d0 + q.R[3] * d1));
-        p0 = ua;
-        p1 = ud;
+      bool bad = false;
+      double J = rollout<INTEG, STAGE, LPM, XM, true>(a, c, n, sx, su, veh, t, sk, q, Ts, up0, up1, K, bad);
+      if (LPM == 2) {                   // the pair shares one rollout: re-run both or neither
+        const int bi = bad;
+        bad = __builtin_amdgcn_mov_dpp(bi, kPair0, 0xF, 0xF, false) |
+              __builtin_amdgcn_mov_dpp(bi, kPair1, 0xF, 0xF, false);
       }
-      const double e0 = x[0] - xr0, e1 = x[1] - xr1;                   // nmpc.py:48 (xref_H)
-      const double term = e0 * (q.P[0] * e0 + q.P[1] * e1) + e1 * (q.P[2] * e0 + q.P[3] * e1);
-      double J = (term + track) + act;                                // nmpc.py:111
-      if (!feas) J = __builtin_inf();
+      if (__builtin_expect(__any(bad), 0)) {
+        bool unused = false;
+        if (bad) J = rollout<INTEG, STAGE, LPM, XM, false>(a, c, n, sx, su, veh, t, sk, q, Ts, up0, up1, K, unused);
+      }
       if (sub == 0) {
         if (a.cost_out) a.cost_out[n * C + c] = J;
         nf += !isfinite(J);

@@ -40,16 +40,16 @@ __global__ void chain(const double* in, double* out, long long* cyc, int iters, 
       }
       if (OP == 15) {                                               // full RK4 step, LPM=4
         double xs[6] = {x, 0.2, 0.3 + x * 0.01, 1.5, 0.05, 0.3};
-        const Input u = make_input_fast(0.5, 0.05 + 1e-3 * x, K);
+        bool bad = false; const Input u = make_input_fast(0.5, 0.05 + 1e-3 * x, K, bad);
         const StageK sk = make_stage<2>(vk, t, threadIdx.x & 1);
-        step_fast<0, 2>(vk, t, sk, xs, u, 0.02, K);
+        step_fast<0, 2>(vk, t, sk, xs, u, 0.02, K, bad);
         x = xs[0] * 0.5 + xs[3] * 1e-3;
       }
       if (OP == 16) {                                               // full RK4 step, LPM=1
         double xs[6] = {x, 0.2, 0.3 + x * 0.01, 1.5, 0.05, 0.3};
-        const Input u = make_input_fast(0.5, 0.05 + 1e-3 * x, K);
+        bool bad = false; const Input u = make_input_fast(0.5, 0.05 + 1e-3 * x, K, bad);
         const StageK sk = make_stage<1>(vk, t, 0);
-        step_fast<0, 1>(vk, t, sk, xs, u, 0.02, K);
+        step_fast<0, 1>(vk, t, sk, xs, u, 0.02, K, bad);
         x = xs[0] * 0.5 + xs[3] * 1e-3;
       }
       if (OP == 17) x = fm::atan2_fast(x * 0.3, 1.0 + x * x, K);

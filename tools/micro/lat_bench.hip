@@ -72,6 +72,26 @@ __global__ void chain(const double* in, double* out, long long* cyc, int iters) 
       if (OP == 11) x = 1.0 + __builtin_amdgcn_rcp(x);
       if (OP == 12) { for (int j = 0; j < 16; ++j) x = (x > k2) ? x * k1 : x + k2; }  // 16 cmp+cndmask+op
       if (OP == 13) x = rint(x * k1) + k2;
+      if (OP == 20) {                                  // 64 dependent fp64 FMAs
+#pragma unroll
+        for (int j = 0; j < 64; ++j) x = fma(x, k1, c[j % 22]);
+      }
+      if (OP == 21) {                                  // 8 independent chains x 8 FMAs
+        double y[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) y[q] = x + q;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) y[q] = fma(y[q], k1, c[(j + q) % 22]);
+        x = ((y[0] + y[1]) + (y[2] + y[3])) + ((y[4] + y[5]) + (y[6] + y[7]));
+      }
+      if (OP == 22) {                                  // 2 independent chains x 32 FMAs
+        double y0 = x, y1 = x + 1;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) { y0 = fma(y0, k1, c[j % 22]); y1 = fma(y1, k1, c[(j + 5) % 22]); }
+        x = y0 + y1;
+      }
       v[i] = x;
     }
   }
@@ -114,5 +134,8 @@ int main() {
   R(10, "div IEEE", 1)
   R(11, "rcp only", 1)
   R(13, "rint", 1)
+  run<20, 1>("64 dep fma (per fma)", din, dout, dcyc, 64);
+  run<21, 1>("8x8 indep fma (per fma)", din, dout, dcyc, 71);
+  run<22, 1>("2x32 fma (per fma)", din, dout, dcyc, 65);
   return 0;
 }
