@@ -316,15 +316,25 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const 
   double Ffy, Fry;
   if (LPM == 2) {
     const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, ok, K);
+#ifdef LLAMPC_ABL_NODPP   // diagnostic ablation builds only
+    Ffy = r;
+    Fry = r * 0.5;
+#else
     Ffy = dpp_bcast<kPair0>(r);
     Fry = dpp_bcast<kPair1>(r);
+#endif
   } else {
     Ffy = chain_fast(sk.ch[0], den, vy, om, d, ok, K);
     Fry = chain_fast(sk.ch[1], den, vy, om, 0.0, ok, K);
   }
   bad = (int)bad | (int)!ok;
   double sp, cp;
+#ifdef LLAMPC_ABL_NOPSI   // diagnostic ablation builds only
+  sp = x[2] * 0.5;
+  cp = x[2] * 0.25;
+#else
   fm::sincos_fast(x[2], &sp, &cp, K);
+#endif
   const double Frx = (sk.k1 - sk.k2 * vx) * u.a - sk.k0 - sk.k3 * (vx * vx);
   dx[0] = vx * cp - vy * sp;
   dx[1] = vx * sp + vy * cp;

@@ -207,7 +207,7 @@ constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 4 
 // issue slots per use — 2.5x on a Horner chain in the one-wave-per-SIMD regime.
 struct FmK {
   double at[22], sw[11], sq[7], cq[7];
-  double pio2, pio2t, two_pi, cw0, cw1, cw2, sixth, six;
+  double pio2, pio2t, two_pi, cw0, cw1, cw2, sixth, six, rmagic;
 
   __device__ __forceinline__ static void pin(double& x) { asm volatile("" : "+v"(x)); }
   __device__ __forceinline__ static FmK load() {
@@ -231,14 +231,18 @@ struct FmK {
     k.cw2 = kPio2Lo;
     k.sixth = 1.0 / 6.0;
     k.six = 6.0;
+    k.rmagic = 0x1.8p52;
     pin(k.pio2); pin(k.pio2t); pin(k.two_pi); pin(k.cw0); pin(k.cw1); pin(k.cw2);
-    pin(k.sixth); pin(k.six);
+    pin(k.sixth); pin(k.six); pin(k.rmagic);
     return k;
   }
 };
 
 template <int N>
 __device__ __forceinline__ double horner(const double* c, double s) {
+#ifdef LLAMPC_ABL_NOPOLY  // diagnostic ablation builds only
+  return fma(c[1], s, c[0]);
+#endif
   double p = c[N - 1];
 #pragma unroll
   for (int i = N - 2; i >= 0; --i) p = fma(p, s, c[i]);
@@ -247,6 +251,9 @@ __device__ __forceinline__ double horner(const double* c, double s) {
 
 // num / den, den in [2^-1001, 2^1000]: reciprocal + two Newton steps + residual.
 __device__ __forceinline__ double div_fast(double num, double den) {
+#ifdef LLAMPC_ABL_NODIV   // diagnostic ablation builds only (tools/micro/ablate.sh)
+  return num * den;
+#endif
   double r = __builtin_amdgcn_rcp(den);
   double e = fma(-den, r, 1.0);
   r = fma(r, e, r);
@@ -307,11 +314,14 @@ __device__ __forceinline__ double sin_wide(double a, const FmK& K) {
 // fix-up with integer sign flips.
 __device__ __host__ __forceinline__ bool sincos_fast_ok(double a) { return fabs(a) <= kSinCosMax; }
 __device__ __forceinline__ void sincos_fast(double a, double* s, double* c, const FmK& K) {
-  const double k = rint(a * K.two_pi);
+  // k = round(a 2/pi) by adding 1.5*2^52 (|a 2/pi| < 2^51 on the domain): the integer lands
+  // in the mantissa's low bits, so the quadrant is the low word — no v_rndne / v_cvt
+  const double t = fma(a, K.two_pi, K.rmagic);
+  const double k = t - K.rmagic;
   double r = fma(-k, K.cw0, a);
   r = fma(-k, K.cw1, r);
   r = fma(-k, K.cw2, r);
-  const int q = (int)k;
+  const int q = __double2loint(t);
   const double s1 = r * r;
   const double sr = fma(r * s1, horner<7>(K.sq, s1), r);
   const double cr = fma(s1 * s1, horner<7>(K.cq, s1), fma(-0.5, s1, 1.0));

@@ -32,6 +32,14 @@ namespace llampc {
 __device__ unsigned long long g_stamps[64][8][2];
 __device__ unsigned int g_stamp_launch;
 __device__ unsigned long long g_la_stamps[8][8][2];   // first 8 look-ahead blocks, last launch
+__device__ unsigned long long g_lb_stamps[8][8][2];   // first 8 look-back blocks, last launch
+#define LB_STAMP(blk, slot)                                                              \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && (blk) < 8) {                                                 \
+      g_lb_stamps[blk][slot][0] = __builtin_amdgcn_s_memtime();                          \
+      g_lb_stamps[blk][slot][1] = __builtin_amdgcn_s_memrealtime();                      \
+    }                                                                                    \
+  } while (0)
 #define LA_STAMP(blk, slot)                                                              \
   do {                                                                                   \
     if (threadIdx.x == 0 && (blk) < 8) {                                                 \
@@ -54,6 +62,9 @@ __device__ unsigned long long g_la_stamps[8][8][2];   // first 8 look-ahead bloc
 #define LA_STAMP(blk, slot) \
   do {                      \
   } while (0)
+#define LB_STAMP(blk, slot) \
+  do {                      \
+  } while (0)
 #endif
 
 namespace {
@@ -63,22 +74,80 @@ __device__ __forceinline__ bool kless(double av, int64_t ai, double bv, int64_t 
   return NAN_FIRST ? less_nan_first(av, ai, bv, bi) : less_nan_last(av, ai, bv, bi);
 }
 
-template <int NAN_FIRST>
-__device__ __forceinline__ void wave_min(double& v, int64_t& i) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double ov = __shfl_xor(v, off, 64);
-    const int64_t oi = __shfl_xor(i, off, 64);
-    if (kless<NAN_FIRST>(ov, oi, v, i)) {
-      v = ov;
-      i = oi;
-    }
+// Cross-lane moves within rows of 16 lanes (DPP; a disabled source lane returns the lane's
+// own value).  xor 1 / xor 2 = quad_perm [1,0,3,2] / [2,3,0,1]; rotate by 4 / 8 in a row.
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppRor4 = 0x124, kDppRor8 = 0x128;
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  return __hiloint2double(dpp_i<CTRL>(__double2hiint(v)), dpp_i<CTRL>(__double2loint(v)));
+}
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp_l(int64_t v) {
+  const uint64_t u = (uint64_t)v;
+  const uint64_t lo = (uint32_t)dpp_i<CTRL>((int)(uint32_t)u), hi = (uint32_t)dpp_i<CTRL>((int)(u >> 32));
+  return (int64_t)(lo | (hi << 32));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ int64_t readlane_l(int64_t v, int l) {
+  const uint64_t u = (uint64_t)v;
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(u >> 32), l);
+  return (int64_t)(lo | (hi << 32));
+}
+
+template <int NAN_FIRST, int CTRL>
+__device__ __forceinline__ void min_step(double& v, int64_t& i) {
+  const double ov = dpp_d<CTRL>(v);
+  const int64_t oi = dpp_l<CTRL>(i);
+  if (kless<NAN_FIRST>(ov, oi, v, i)) {
+    v = ov;
+    i = oi;
   }
 }
 
-__device__ __forceinline__ int block_sum(int x, int32_t* sn) {
+// Wave-wide min of (v, i) under kless<NAN_FIRST>, the result in every lane.  ALL 64 lanes
+// must be active (converged code).  DPP butterfly inside each row of 16 lanes, then the four
+// row results combined from readlanes — no LDS round trips (the __shfl_xor form cost ~4k
+// cycles per block reduction, SQ stamps).
+template <int NAN_FIRST>
+__device__ __forceinline__ void wave_min(double& v, int64_t& i) {
+  min_step<NAN_FIRST, kDppXor1>(v, i);
+  min_step<NAN_FIRST, kDppXor2>(v, i);
+  min_step<NAN_FIRST, kDppRor4>(v, i);
+  min_step<NAN_FIRST, kDppRor8>(v, i);
+  double bv = readlane_d(v, 0);
+  int64_t bi = readlane_l(i, 0);
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  for (int r = 16; r < 64; r += 16) {
+    const double rv = readlane_d(v, r);
+    const int64_t ri = readlane_l(i, r);
+    if (kless<NAN_FIRST>(rv, ri, bv, bi)) {
+      bv = rv;
+      bi = ri;
+    }
+  }
+  v = bv;
+  i = bi;
+}
+
+__device__ __forceinline__ int wave_sum(int x) {
+  x += dpp_i<kDppXor1>(x);
+  x += dpp_i<kDppXor2>(x);
+  x += dpp_i<kDppRor4>(x);
+  x += dpp_i<kDppRor8>(x);
+  return __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 16) +
+         __builtin_amdgcn_readlane(x, 32) + __builtin_amdgcn_readlane(x, 48);
+}
+
+__device__ __forceinline__ int block_sum(int x, int32_t* sn) {
+  x = wave_sum(x);
   if ((threadIdx.x & 63) == 0) sn[threadIdx.x >> 6] = x;
   __syncthreads();
   int s = 0;
@@ -207,8 +276,11 @@ __device__ __forceinline__ bool ticket_last(unsigned* t, unsigned expected, int*
 // mean in NumPy's pairwise order; then the block's argmin and its SORTED top-K list.
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk, const Scratch& sc) {
+  LB_STAMP(blk, 0);
   const int64_t base = (int64_t)blk * kBlock * a.R;
-  const Input u = make_input(a.u_prev[0], a.u_prev[1]);
+  const fm::FmK K = fm::FmK::load();
+  bool ubad = false;
+  const Input uf = make_input_fast(a.u_prev[0], a.u_prev[1], K, ubad);
   double wm0 = 0.0;                     // R == 1 keeps the window mean in a register
   for (int r = 0; r < a.R; ++r) {
     const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
@@ -217,7 +289,18 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
 #pragma unroll
     for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
     const Tire t = load_tire(a.params, a.n, n);
-    rk4_step(a.veh, t, x, u, a.Ts);                       // model.py:32-40, one RK4 step
+    // model.py:32-40, one RK4 step: the fast stage; a lane whose operands leave the fast
+    // cores' domains redoes the step with the general functions (as the look-ahead does)
+    bool bad = ubad;
+    const StageK sk = make_stage<1>(a.veh, t, 0);
+    step_fast<0, 1>(a.veh, t, sk, x, uf, a.Ts, K, bad);
+    if (__builtin_expect(__any(bad), 0)) {
+      if (bad) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
+        rk4_step(a.veh, t, x, make_input(a.u_prev[0], a.u_prev[1]), a.Ts);
+      }
+    }
     double s = 0.0;                                       // rt.py:349 mean over 4 states
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -234,6 +317,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
       if (r == 0) wm0 = wm;
     }
   }
+  LB_STAMP(blk, 1);
   if (!a.full) return;  // launch-uniform
 
   // the block's argmin (rt.py:359 semantics) over its 256*R models
@@ -255,6 +339,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     a.am_val[blk] = v;
     a.am_idx[blk] = i;
   }
+  LB_STAMP(blk, 2);
   // sorted top-K of the block (rt.py:360 argsort order): K rounds of "next larger key"
   double lv = 0.0;
   int64_t li = -1;
@@ -280,6 +365,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     lv = cv;
     li = ci;
   }
+  LB_STAMP(blk, 3);
 }
 
 // One (model, candidate) rollout over H steps and its NLP objective (nmpc.py:44-111).
@@ -517,6 +603,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     a.pidx[blk] = key;
     a.pnf[blk] = nfs;
   }
+  LA_STAMP(blk, 3);
 }
 
 struct Ent {
@@ -620,6 +707,24 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
   const int tid = threadIdx.x;
   llampc_plan_out* o = f.out;
   const bool lb = f.do_lb && f.full;
+  // Every load that does not depend on the look-ahead reduction is issued first, so the
+  // tail costs two dependent round trips, not three: the look-back result lb_final left in
+  // the record (top-K ids, lb_best) and then those models' best candidates.
+  const int64_t idk = (lb && tid < LLAMPC_KMAX) ? o->topk[tid] : -1;
+  const int64_t lbi = (tid == 0 && lb) ? o->lb_best : -1;
+  const int64_t sel = lbi >= 0 ? lbi : f.current_model;
+  const bool owned = sel >= f.goff && sel < f.goff + f.n;
+  const bool have = lb && tid < LLAMPC_KMAX && idk >= 0 && f.do_la;
+  int32_t kcand = -1, scand = -1;
+  double kcost = __builtin_nan(""), scost = __builtin_nan("");
+  if (have) {
+    kcand = f.best_cand[idk - f.goff];
+    kcost = f.best_cost[idk - f.goff];
+  }
+  if (tid == 0 && owned && f.do_la) {
+    scand = f.best_cand[sel - f.goff];
+    scost = f.best_cost[sel - f.goff];
+  }
   double lav = __builtin_nan("");
   int64_t lai = kNoIndex;
   int nf = 0;
@@ -633,16 +738,8 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
         lai = pi;
       }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double ov = __shfl_xor(lav, off, 64);
-      const int64_t oi = __shfl_xor(lai, off, 64);
-      nf += __shfl_xor(nf, off, 64);
-      if (less_nan_last(ov, oi, lav, lai)) {
-        lav = ov;
-        lai = oi;
-      }
-    }
+    wave_min<0>(lav, lai);              // converged: every lane of the block is here
+    nf = wave_sum(nf);
     if ((tid & 63) == 0) {
       sc.sv[4 + (tid >> 6)] = lav;
       sc.si[4 + (tid >> 6)] = lai;
@@ -664,17 +761,14 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
   STAMP(4);
   if (tid < LLAMPC_KMAX) {
     const int k = tid;
-    const int64_t id = lb ? o->topk[k] : -1;
     if (!lb) {
       o->topk[k] = -1;
       o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = __builtin_nan("");
     }
-    const bool have = lb && id >= 0 && f.do_la;
-    o->topk_cand[k] = have ? f.best_cand[id - f.goff] : -1;
-    o->topk_cost[k] = have ? f.best_cost[id - f.goff] : __builtin_nan("");
+    o->topk_cand[k] = kcand;
+    o->topk_cost[k] = kcost;
   }
   if (tid == 0) {
-    const int64_t lbi = lb ? o->lb_best : -1;
     if (!lb) {
       o->lb_best = -1;
       o->lb_best_val = __builtin_nan("");
@@ -684,12 +778,10 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
     o->K = f.K;
     o->n_nonfinite = nf;
     o->reserved = 0;
-    const int64_t sel = lbi >= 0 ? lbi : f.current_model;
-    const bool owned = sel >= f.goff && sel < f.goff + f.n;
     o->sel_model = sel;
     o->sel_owned = owned;
-    o->sel_cand = (owned && f.do_la) ? f.best_cand[sel - f.goff] : -1;
-    o->sel_cost = (owned && f.do_la) ? f.best_cost[sel - f.goff] : __builtin_nan("");
+    o->sel_cand = scand;
+    o->sel_cost = scost;
     if (f.do_la && lai != kNoIndex) {
       o->la_best_model = lai / f.C;
       o->la_best_cand = (int32_t)(lai % f.C);
@@ -1047,6 +1139,9 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
 }
 
 #ifdef LLAMPC_STAMPS
+extern "C" int llampc_debug_lb_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lb_stamps), sizeof(g_lb_stamps)) == hipSuccess ? 0 : -2;
+}
 extern "C" int llampc_debug_la_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_stamps), sizeof(g_la_stamps)) == hipSuccess ? 0 : -2;
 }

@@ -22,6 +22,7 @@ fn(st)
 a = np.frombuffer(st, dtype=np.uint64).reshape(8, 8, 2).astype(np.int64)
 t0 = a[:, 0, 1].min()
 for blk in range(8):
-    mt, rt = a[blk, :5, 0], a[blk, :5, 1]
-    print(f"la block {blk}: start +{(rt[0]-t0)/100:.2f}us | phases(cycles) staging {mt[1]-mt[0]}, rollout {mt[2]-mt[1]}, "
-          f"reduce {mt[3]-mt[2]}, ticket {mt[4]-mt[3]} | total {(rt[4]-rt[0])/100:.2f}us  clk {(mt[4]-mt[0])/max(1,rt[4]-rt[0])*100:.0f}MHz")
+    mt, rt = a[blk, :4, 0], a[blk, :4, 1]
+    clk = (mt[3] - mt[0]) / max(1, rt[3] - rt[0]) * 100       # s_memrealtime ticks at 100 MHz
+    print(f"la block {blk}: start +{(rt[0]-t0)/100:.2f}us | cycles: staging {mt[1]-mt[0]}, rollout {mt[2]-mt[1]} "
+          f"({(mt[2]-mt[1])/20:.0f}/step), reduce {mt[3]-mt[2]} | {(rt[3]-rt[0])/100:.2f}us  clock {clk:.0f} MHz")

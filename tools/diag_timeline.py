@@ -1,0 +1,47 @@
+"""Diagnostic (not product): one tick's timeline from the stamps build — look-ahead blocks
+(first 8: start, end of staging, end of rollout, end of reduction) and the completion stages
+(lb_final, final_select) on the same s_memrealtime (100 MHz) clock."""
+import ctypes, os, sys
+import numpy as np
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["LLAMPC_HIP_LIB"] = os.path.join(REPO, "lla-mpc_amd/llampc/_lib/libllampc_hip_stamps.so")
+sys.path[:0] = [REPO, os.path.join(REPO, "lla-mpc_amd")]
+from llampc import _native as nat
+from llampc.mpc import ModelBank, generate_bank
+lib = nat.load()
+d = np.load(os.path.join(REPO, "tests/golden/dyn_slice.npz"))
+s, u = d["states"], d["inputs"]
+N, H = int(sys.argv[1]) if len(sys.argv) > 1 else 10000, 20
+LB_ONLY = len(sys.argv) > 2 and sys.argv[2] == "lb"
+b = ModelBank(generate_bank(N, 0), W=10, device=0)
+xref = s[:2, :H + 1]
+U = np.tile(u[:, 0], (H, 1))[None]
+for t in range(1, 30):
+    b.plan_raw(s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1], do_lookahead=not LB_ONLY)
+la = (ctypes.c_ulonglong * (8 * 8 * 2))()
+lib.llampc_debug_la_stamps.argtypes = [ctypes.c_void_p]
+lib.llampc_debug_la_stamps(la)
+fs = (ctypes.c_ulonglong * (64 * 8 * 2))()
+nl = ctypes.c_uint()
+lib.llampc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+lib.llampc_debug_stamps(fs, ctypes.byref(nl))
+A = np.frombuffer(la, dtype=np.uint64).reshape(8, 8, 2).astype(np.int64)[:, :4, 1]
+lb = (ctypes.c_ulonglong * (8 * 8 * 2))()
+lib.llampc_debug_lb_stamps.argtypes = [ctypes.c_void_p]
+lib.llampc_debug_lb_stamps(lb)
+B = np.frombuffer(lb, dtype=np.uint64).reshape(8, 8, 2).astype(np.int64)
+F = np.frombuffer(fs, dtype=np.uint64).reshape(64, 8, 2).astype(np.int64)
+l = (nl.value - 1) & 63
+R = F[l, :6, 1]
+B0 = np.frombuffer(lb, dtype=np.uint64).reshape(8, 8, 2).astype(np.int64)
+t0 = B0[:, 0, 1].min() if LB_ONLY else A[:, 0].min()
+us = lambda x: (x - t0) / 100.0
+print(f"launches {nl.value}; times in us from the first look-ahead block start")
+print(f"look-ahead blocks: start {us(A[:,0].min()):.2f}..{us(A[:,0].max()):.2f}, staging end ..{us(A[:,1].max()):.2f}, "
+      f"rollout end {us(A[:,2].min()):.2f}..{us(A[:,2].max()):.2f}, reduce end ..{us(A[:,3].max()):.2f}")
+for k in range(8):
+    print(f"look-back block {k}: start {us(B[k,0,1]):.2f}, step+ring+mean end {us(B[k,1,1]):.2f}, "
+          f"argmin end {us(B[k,2,1]):.2f}, top-K end {us(B[k,3,1]):.2f}  "
+          f"(cycles {B[k,1,0]-B[k,0,0]}, {B[k,2,0]-B[k,1,0]}, {B[k,3,0]-B[k,2,0]})")
+print(f"lb_final: {us(R[0]):.2f} -> {us(R[1]):.2f} -> {us(R[2]):.2f}")
+print(f"final_select: {us(R[3]):.2f} -> {us(R[4]):.2f} -> {us(R[5]):.2f}")
