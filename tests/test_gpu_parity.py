@@ -482,7 +482,8 @@ def test_lookahead_out_of_domain_fallback(nat):
     Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
     cases = [np.array([0.2, 0.1, -0.7, 1.5, 0.02, 0.3]),
              np.array([0.2, 0.1, 3.0e6, 1.5, 0.02, 0.3]),           # huge yaw: sincos fallback
-             np.array([0.0, 0.0, 0.4, 0.0, 0.0, 0.0])]              # standing start
+             np.array([0.0, 0.0, 0.4, 0.0, 0.0, 0.0]),              # standing start
+             np.array([0.2, 0.1, -0.7, 2.5, 0.1, 40.0])]            # spinning start
     for x0 in cases:
         with np.errstate(all="ignore"):
             traj = O.rollout_rk4(shared(), tuple(p), x0, U, TS)
