@@ -252,19 +252,46 @@ __device__ __host__ __forceinline__ Chain make_chain(const VehK& v, const Tire& 
 
 // Static part of the fast chain's domain: |C atan(.)| <= |C| pi/2 must stay inside
 // sin_wide's |a| <= 3 (|C| <= 1.9 -> 2.985; NaN -> false).
-__device__ __host__ __forceinline__ bool chain_static_ok(const Chain& c) { return fabs(c.C) <= 1.9; }
+// Static part of the domain: |C| <= 1.9 (sin_wide's range), finite B and D (so a NaN in
+// the chain always comes from a NaN state or input, which reaches the rollout's result).
+__device__ __host__ __forceinline__ bool chain_static_ok(const Chain& c) {
+  return (int)(fabs(c.C) <= 1.9) & (int)(fabs(c.B) <= 1e300) & (int)(fabs(c.D) <= 1e300) &
+         (int)(fabs(c.lw) <= 1e300);
+}
+
+// Running extremes of the fast cores' operands over a rollout (or a look-back step): the
+// domain is judged once at the end instead of per stage (a compare + mask OR per operand
+// cost ~15 issue slots per stage).  hi = max of the atan2 divisors max(|y|, x) and of the
+// atan divisors max(|z|, 1); lo = min of the atan2 divisors; ps = max |psi|.  ok(): every
+// operand inside the fast domains (atan2: hi in [2^-1000, 2^999] implies |y| + x in
+// [2^-1000, 2^1000]; atan: |z| <= 2^999; sincos: |psi| <= kSinCosMax).  fmax/fmin skip a
+// NaN operand, but a NaN operand comes from a NaN state, input or parameter and reaches the
+// lane's result (the caller also requires a finite result).
+struct Dom {
+  double hi, lo, ps;
+  __device__ __forceinline__ void init() {
+    hi = 0.0;
+    lo = __builtin_inf();
+    ps = 0.0;
+  }
+  __device__ __forceinline__ bool ok() const {
+    return (int)(hi <= 0x1p999) & (int)(lo >= 0x1p-1000) & (int)(ps <= fm::kSinCosMax);
+  }
+};
 
 // F = D sin(C atan(B slip)) with slip = dsel - atan2(yy, den) for the front tire
 // (dsel = delta) and atan2(yy, den) for the rear (dsel = 0); yy = lf om + vy | lr om - vy
-// (dynamic.py:149-152 / :215-220).  `ok` &= the lane's dynamic domain.
+// (dynamic.py:149-152 / :215-220).  The divisors go to the lane's Dom.
 __device__ __forceinline__ double chain_fast(const Chain& c, double den, double vy, double om,
-                                             double dsel, bool& ok, const fm::FmK& K) {
+                                             double dsel, Dom& dm, const fm::FmK& K) {
   const double yy = fma(c.lw, om, c.sg * vy);
-  const double a2 = fm::atan2_fast(yy, den, K);
+  double h2, hz;
+  const double a2 = fm::atan2_fast(yy, den, K, h2);
   const double z = c.B * fma(-c.sg, a2, dsel);
-  // non-short-circuit: a && here compiles to a divergent branch inside the stage
-  ok = (int)ok & (int)fm::atan2_fast_ok(yy, den) & (int)fm::atan_fast_ok(z);
-  return c.D * fm::sin_wide(c.C * fm::atan_fast(z, K), K);
+  const double at = fm::atan_fast(z, K, hz);
+  dm.lo = fmin(dm.lo, h2);
+  dm.hi = fmax(dm.hi, fmax(h2, hz));
+  return c.D * fm::sin_wide(c.C * at, K);
 }
 
 // Per-rollout constants of the fast stage.  ch[0] is this lane's chain (LPM = 2) or the
@@ -294,13 +321,13 @@ __device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int s
   return s;
 }
 
-// dx/dt on the fast path.  No fallback here: `bad` |= "an operand of this lane left a fast
-// core's domain (or the bank uses linear tires)"; the caller re-runs such rollouts with the
-// general evaluation (lookahead_block), so the stage has no branch at all.
+// dx/dt on the fast path.  No fallback and no domain test here: the operands go to `dm`;
+// the caller judges dm (and sk.sok) once and re-runs an out-of-domain lane's rollout with
+// the general evaluation (lookahead_block), so the stage has no branch at all.
 template <Form F, int LPM>
 __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const double* x,
                                          const Input& u, double* dx, const fm::FmK& K,
-                                         bool& bad) {
+                                         Dom& dm) {
   double vx = x[3], vy = x[4], om = x[5];
   double d = u.d, sd = u.sd, cd = u.cd;
   if (F == Form::Nlp && vx < 0.05) {      // dynamic.py:208-212 (vmin clamp)
@@ -312,10 +339,10 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const 
     vx = 0.05;
   }
   const double den = (F == Form::Ref) ? fabs(vx) : vx;
-  bool ok = (int)sk.sok & (int)fm::sincos_fast_ok(x[2]);   // sok includes !approx
+  dm.ps = fmax(dm.ps, fabs(x[2]));
   double Ffy, Fry;
   if (LPM == 2) {
-    const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, ok, K);
+    const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
 #ifdef LLAMPC_ABL_NODPP   // diagnostic ablation builds only
     Ffy = r;
     Fry = r * 0.5;
@@ -324,10 +351,9 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const 
     Fry = dpp_bcast<kPair1>(r);
 #endif
   } else {
-    Ffy = chain_fast(sk.ch[0], den, vy, om, d, ok, K);
-    Fry = chain_fast(sk.ch[1], den, vy, om, 0.0, ok, K);
+    Ffy = chain_fast(sk.ch[0], den, vy, om, d, dm, K);
+    Fry = chain_fast(sk.ch[1], den, vy, om, 0.0, dm, K);
   }
-  bad = (int)bad | (int)!ok;
   double sp, cp;
 #ifdef LLAMPC_ABL_NOPSI   // diagnostic ablation builds only
   sp = x[2] * 0.5;
@@ -363,36 +389,36 @@ __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::F
 template <int INTEG, int LPM>
 __device__ __forceinline__ void step_fast(const VehK& v, const Tire& t, const StageK& sk,
                                           double* x, const Input& u, double h,
-                                          const fm::FmK& K, bool& bad) {
+                                          const fm::FmK& K, Dom& dm) {
   if (INTEG == 0) {
     double y[6], d[6], acc[6];
-    rhs_fast<Form::Ref, LPM>(v, sk, x, u, d, K, bad);
+    rhs_fast<Form::Ref, LPM>(v, sk, x, u, d, K, dm);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const double k = h * d[i];
       acc[i] = k;
       y[i] = fma(0.5, k, x[i]);
     }
-    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, bad);
+    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, dm);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const double k = h * d[i];
       acc[i] = fma(2.0, k, acc[i]);
       y[i] = fma(0.5, k, x[i]);
     }
-    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, bad);
+    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, dm);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const double k = h * d[i];
       acc[i] = fma(2.0, k, acc[i]);
       y[i] = x[i] + k;
     }
-    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, bad);
+    rhs_fast<Form::Ref, LPM>(v, sk, y, u, d, K, dm);
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = x[i] + fm::div6(acc[i] + h * d[i], K);
   } else if (INTEG == 1) {
     double d[6];
-    rhs_fast<Form::Nlp, LPM>(v, sk, x, u, d, K, bad);
+    rhs_fast<Form::Nlp, LPM>(v, sk, x, u, d, K, dm);
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = x[i] + h * d[i];
   } else {

@@ -286,21 +286,34 @@ __device__ __host__ __forceinline__ bool atan2_fast_ok(double y, double x) {
   const double s = fabs(y) + x;
   return s >= 0x1p-1000 && s <= 0x1p1000;
 }
-__device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K) {
+// hi = max(|y|, x), the divisor: hi in [2^-1000, 2^999] lies inside the domain (the
+// rollout checks its running extremes once, dyn.hpp Dom).
+__device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K, double& hi) {
   const double ay = fabs(y);
-  const double r = atan_core_k(div_fast(fmin(ay, x), fmax(ay, x)), K);
+  hi = fmax(ay, x);
+  const double r = atan_core_k(div_fast(fmin(ay, x), hi), K);
   const double o = (ay > x) ? (K.pio2 - r) + K.pio2t : r;
   return copysign(o, y);
+}
+__device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K) {
+  double hi;
+  return atan2_fast(y, x, K, hi);
 }
 
 // atan(z) on the domain |z| <= 2^1000: the reciprocal branch as a division by max(|z|, 1)
 // (exact when |z| <= 1).
 __device__ __host__ __forceinline__ bool atan_fast_ok(double z) { return fabs(z) <= 0x1p1000; }
-__device__ __forceinline__ double atan_fast(double z, const FmK& K) {
+// hz = max(|z|, 1), the divisor: hz <= 2^1000 is the domain.
+__device__ __forceinline__ double atan_fast(double z, const FmK& K, double& hz) {
   const double az = fabs(z);
-  const double r = atan_core_k(div_fast(fmin(az, 1.0), fmax(az, 1.0)), K);
+  hz = fmax(az, 1.0);
+  const double r = atan_core_k(div_fast(fmin(az, 1.0), hz), K);
   const double o = (az > 1.0) ? (K.pio2 - r) + K.pio2t : r;
   return copysign(o, z);
+}
+__device__ __forceinline__ double atan_fast(double z, const FmK& K) {
+  double hz;
+  return atan_fast(z, K, hz);
 }
 
 // sin(a) for |a| <= kSinWideMax, one polynomial (the Pacejka argument C*atan(.) is

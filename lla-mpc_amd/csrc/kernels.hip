@@ -270,6 +270,16 @@ __device__ __forceinline__ bool ticket_last(unsigned* t, unsigned expected, int*
   return *flag != 0;
 }
 
+__device__ __forceinline__ double sq_err4(const double* x, const double* xn) {
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double e = x[j] - xn[j];
+    s += e * e;
+  }
+  return s;
+}
+
 // ------------------------------------------------------------------------------------
 // Look-back body: one block = 256*R models (R models per lane, coalesced in r).
 // RK4 step from (x_{t-1}, u_{t-1}), 4-state MSE against x_t, in-place ring write, window
@@ -291,21 +301,20 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     const Tire t = load_tire(a.params, a.n, n);
     // model.py:32-40, one RK4 step: the fast stage; a lane whose operands leave the fast
     // cores' domains redoes the step with the general functions (as the look-ahead does)
-    bool bad = ubad;
     const StageK sk = make_stage<1>(a.veh, t, 0);
-    step_fast<0, 1>(a.veh, t, sk, x, uf, a.Ts, K, bad);
+    Dom dm;
+    dm.init();
+    step_fast<0, 1>(a.veh, t, sk, x, uf, a.Ts, K, dm);
+    double s = sq_err4(x, a.x_now);                       // rt.py:349 mean over 4 states
+    // the domain once per step; a NaN operand reaches x[0..3] (the stage-4 chains feed x[3])
+    bool bad = (int)ubad | (int)!sk.sok | (int)!dm.ok() | (int)!(s <= __DBL_MAX__);
     if (__builtin_expect(__any(bad), 0)) {
       if (bad) {
 #pragma unroll
         for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
         rk4_step(a.veh, t, x, make_input(a.u_prev[0], a.u_prev[1]), a.Ts);
+        s = sq_err4(x, a.x_now);
       }
-    }
-    double s = 0.0;                                       // rt.py:349 mean over 4 states
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const double e = x[j] - a.x_now[j];
-      s += e * e;
     }
     const double err = s / 4;
     if (a.err_out) a.err_out[n] = err;
@@ -388,6 +397,8 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   bool feas = true;
   double xr0 = 0.0, xr1 = 0.0;
   const double* xpm = XM ? a.xref_pm + n * 2 * H : nullptr;   // this model's reference
+  Dom dm;                               // FAST: the operands' running extremes
+  dm.init();
   for (int k = 0; k < H; ++k) {
     double ua, ud;
     Input u;
@@ -413,7 +424,7 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
              ((int)(q.dmax[0] < 0) | (int)(fabs(d0) <= q.dmax[0])) &
              ((int)(q.dmax[1] < 0) | (int)(fabs(d1) <= q.dmax[1]));
     }
-    if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, bad);
+    if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, dm);
     else step<INTEG>(veh, t, x, u, Ts);
     if (XM) {
       xr0 = xpm[2 * k];
@@ -431,6 +442,10 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   const double e0 = x[0] - xr0, e1 = x[1] - xr1;                   // nmpc.py:48 (xref_H)
   const double term = e0 * (q.P[0] * e0 + q.P[1] * e1) + e1 * (q.P[2] * e0 + q.P[3] * e1);
   double J = (term + track) + act;                                // nmpc.py:111
+  // the domain, once per rollout: a NaN operand reaches x[0..1] (every chain output feeds
+  // the later stages' positions, the last stage's feeds vx, vy, omega only through a NaN
+  // state that the position update already carries), so a non-finite J is re-run too
+  if (FAST) bad = (int)bad | (int)!sk.sok | (int)!dm.ok() | (int)!(fabs(J) <= __DBL_MAX__);
   if (!feas) J = __builtin_inf();
   return J;
 }
