@@ -400,7 +400,8 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
   if (!out) return fail(LLAMPC_E_ARG, "out is NULL");
   *out = nullptr;
   if (!params || !veh) return fail(LLAMPC_E_ARG, "params/veh is NULL");
-  if (n < 1) return fail(LLAMPC_E_ARG, "n=%lld must be >= 1", (long long)n);
+  if (n < 1 || n > INT32_MAX)   // the kernels rank models by a 32-bit local index
+    return fail(LLAMPC_E_ARG, "n=%lld must be in [1, 2^31-1]", (long long)n);
   if (W < 1 || W > LLAMPC_WMAX) return fail(LLAMPC_E_ARG, "W=%d outside [1, %d]", W, LLAMPC_WMAX);
   if (global_offset < 0) return fail(LLAMPC_E_ARG, "global_offset < 0");
   int ndev = 0;
@@ -424,12 +425,12 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
   if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
   b->own_stream = true;
-  const int lbb = lookback_blocks(n);
+  const int64_t lbl = (int64_t)lookback_blocks(n) * (kBlock / 64);   // look-back lists (waves)
   const int64_t lab = n;                 // worst case: one model per block (wave-role, G=64)
   if ((rc = dev_alloc(&b->d_params, 6 * (size_t)n)) || (rc = dev_alloc(&b->d_ring, (size_t)W * n)) ||
-      (rc = dev_alloc(&b->d_am_val, lbb)) || (rc = dev_alloc(&b->d_am_idx, lbb)) ||
-      (rc = dev_alloc(&b->d_tk_val, (size_t)lbb * LLAMPC_KMAX)) ||
-      (rc = dev_alloc(&b->d_tk_idx, (size_t)lbb * LLAMPC_KMAX)) || (rc = dev_alloc(&b->d_pv, lab)) ||
+      (rc = dev_alloc(&b->d_am_val, lbl)) || (rc = dev_alloc(&b->d_am_idx, lbl)) ||
+      (rc = dev_alloc(&b->d_tk_val, (size_t)lbl * LLAMPC_KMAX)) ||
+      (rc = dev_alloc(&b->d_tk_idx, (size_t)lbl * LLAMPC_KMAX)) || (rc = dev_alloc(&b->d_pv, lab)) ||
       (rc = dev_alloc(&b->d_pidx, lab)) || (rc = dev_alloc(&b->d_pnf, lab)) ||
       (rc = dev_alloc(&b->d_best_cand, n)) || (rc = dev_alloc(&b->d_best_cost, n)) ||
       (rc = dev_alloc(&b->d_err, n)) || (rc = dev_alloc(&b->d_wmean, n)) ||

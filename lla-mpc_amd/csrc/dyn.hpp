@@ -451,6 +451,15 @@ __device__ __host__ __forceinline__ bool key_less(bool nan_first, double av, int
   return nan_first ? less_nan_first(av, ai, bv, bi) : less_nan_last(av, ai, bv, bi);
 }
 
+// Branch-free forms of the two orders for per-lane loops on the device (the if/else forms
+// above compile to nested divergent branches).
+template <int NAN_FIRST, typename I>
+__device__ __forceinline__ bool less_bf(double av, I ai, double bv, I bi) {
+  const int an = av != av, bn = bv != bv, na = an ^ 1, nb = bn ^ 1;
+  const int first = NAN_FIRST ? (an & nb) : (na & bn);
+  return first | ((na & nb) & (int)(av < bv)) | (((an & bn) | (int)(av == bv)) & (int)(ai < bi));
+}
+
 constexpr int64_t kNoIndex = INT64_MAX;   // sentinel index: sorts after every real key
                                           // (value +inf under NaN-first, NaN under NaN-last)
 

@@ -249,15 +249,16 @@ __device__ __forceinline__ double horner(const double* c, double s) {
   return p;
 }
 
-// num / den, den in [2^-1001, 2^1000]: reciprocal + two Newton steps + residual.
+// num / den, den in [2^-1001, 2^1000]: reciprocal + one Newton step + residual.  With the
+// reciprocal's relative error e0, r has e0^2 and the corrected quotient e0^4 + 1/2 ulp:
+// one step is enough for any e0 <= 2^-14 (v_rcp_f64 is far better; the atan2/atan ULP
+// tests, whose every call divides, bound the result).
 __device__ __forceinline__ double div_fast(double num, double den) {
 #ifdef LLAMPC_ABL_NODIV   // diagnostic ablation builds only (tools/micro/ablate.sh)
   return num * den;
 #endif
   double r = __builtin_amdgcn_rcp(den);
-  double e = fma(-den, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-den, r, 1.0);
+  const double e = fma(-den, r, 1.0);
   r = fma(r, e, r);
   const double q = num * r;
   return fma(r, fma(-den, q, num), q);

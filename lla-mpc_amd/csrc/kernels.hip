@@ -137,6 +137,46 @@ __device__ __forceinline__ void wave_min(double& v, int64_t& i) {
   i = bi;
 }
 
+// Branch-free ordered picks over a wave (all 64 lanes active).  A lane's candidate is
+// (v, li) with li a local model index (order = global index order); a lane without one holds
+// li = kNoLocal (and v = NaN, or +inf under NaN-first).  The value min runs on v_min_f64
+// (IEEE minNum: NaN only when every lane is NaN), the tie-break on u32 mins — no compare of
+// (value, index) pairs and no divergent branch.
+constexpr uint32_t kNoLocal = 0xFFFFFFFFu;
+__device__ __forceinline__ double wave_min_f64(double v) {
+  v = fmin(v, dpp_d<kDppXor1>(v));
+  v = fmin(v, dpp_d<kDppXor2>(v));
+  v = fmin(v, dpp_d<kDppRor4>(v));
+  v = fmin(v, dpp_d<kDppRor8>(v));
+  return fmin(fmin(readlane_d(v, 0), readlane_d(v, 16)), fmin(readlane_d(v, 32), readlane_d(v, 48)));
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+  x = min(x, (uint32_t)dpp_i<kDppXor1>((int)x));
+  x = min(x, (uint32_t)dpp_i<kDppXor2>((int)x));
+  x = min(x, (uint32_t)dpp_i<kDppRor4>((int)x));
+  x = min(x, (uint32_t)dpp_i<kDppRor8>((int)x));
+  const uint32_t a = min((uint32_t)__builtin_amdgcn_readlane((int)x, 0), (uint32_t)__builtin_amdgcn_readlane((int)x, 16));
+  const uint32_t b = min((uint32_t)__builtin_amdgcn_readlane((int)x, 32), (uint32_t)__builtin_amdgcn_readlane((int)x, 48));
+  return min(a, b);
+}
+// NaN-last order (argsort): the smallest value, ties (and all-NaN) -> the lowest li.
+__device__ __forceinline__ void wave_pick_nl(double& v, uint32_t& li) {
+  const double m = wave_min_f64(v);
+  const int c = (int)(li != kNoLocal) & ((int)(v == m) | ((int)(m != m) & (int)(v != v)));
+  li = wave_min_u32(c ? li : kNoLocal);
+  v = m;
+}
+// NaN-first order (np.argmin): the lowest li holding NaN if there is one.
+__device__ __forceinline__ void wave_pick_nf(double& v, uint32_t& li) {
+  const int isn = (int)(li != kNoLocal) & (int)(v != v);
+  if (__any(isn)) {                     // wave-uniform
+    li = wave_min_u32(isn ? li : kNoLocal);
+    v = __builtin_nan("");
+  } else {
+    wave_pick_nl(v, li);
+  }
+}
+
 __device__ __forceinline__ int wave_sum(int x) {
   x += dpp_i<kDppXor1>(x);
   x += dpp_i<kDppXor2>(x);
@@ -210,6 +250,8 @@ __device__ __forceinline__ double window_mean(const double* ring, int64_t ld, in
 // G17): [0,64) sv[2][4] double | [64,128) si[2][4] int64 | [128,144) sn[4] int32 |
 // pad to 160 | role-specific region from 160.
 constexpr int kScratchBytes = 160;
+constexpr int kWaves = kBlock / 64;     // look-back lists per block (one per wave)
+constexpr int kListsPerLane = 8;        // lb_final: lists per lane of the merging wave
 
 struct Scratch {
   double* sv;
@@ -329,50 +371,51 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
   LB_STAMP(blk, 1);
   if (!a.full) return;  // launch-uniform
 
-  // the block's argmin (rt.py:359 semantics) over its 256*R models
-  int par = 0;
+  // per WAVE (a list): the argmin (rt.py:359 semantics) and the sorted top-K (rt.py:360
+  // argsort order) of its 64*R models with branch-free wave picks — no LDS round trip, no
+  // barrier (a block-wide (value, index) min per round cost ~4k cycles); lb_final merges
+  // the kWaves lists of every block.  Local index n < 2^32 (bank size check in the C-ABI).
+  const int lane = threadIdx.x & 63;
+  const int64_t list = (int64_t)blk * kWaves + (threadIdx.x >> 6);
   double v = a.nan_first ? __builtin_inf() : __builtin_nan("");
-  int64_t i = kNoIndex;
+  uint32_t li = kNoLocal;
   for (int r = 0; r < a.R; ++r) {
     const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
     if (n >= a.n) break;
     const double w = (a.R == 1) ? wm0 : a.wm_buf[n];
-    if (key_less(a.nan_first, w, a.goff + n, v, i)) {
-      v = w;
-      i = a.goff + n;
-    }
+    const bool t = a.nan_first ? less_bf<1>(w, (uint32_t)n, v, li) : less_bf<0>(w, (uint32_t)n, v, li);
+    v = t ? w : v;
+    li = t ? (uint32_t)n : li;
   }
-  if (a.nan_first) block_min1<1>(v, i, sc, par);
-  else block_min1<0>(v, i, sc, par);
-  if (threadIdx.x == 0) {
-    a.am_val[blk] = v;
-    a.am_idx[blk] = i;
+  if (a.nan_first) wave_pick_nf(v, li);
+  else wave_pick_nl(v, li);
+  if (lane == 0) {
+    a.am_val[list] = v;
+    a.am_idx[list] = li == kNoLocal ? kNoIndex : a.goff + li;
   }
   LB_STAMP(blk, 2);
-  // sorted top-K of the block (rt.py:360 argsort order): K rounds of "next larger key"
+  // K rounds of "next key after the previous pick" (NaN last, ties -> lower index)
   double lv = 0.0;
-  int64_t li = -1;
+  uint32_t ll = kNoLocal;
   for (int k = 0; k < a.K; ++k) {
     double cv = __builtin_nan("");
-    int64_t ci = kNoIndex;
+    uint32_t cl = kNoLocal;
     for (int r = 0; r < a.R; ++r) {
       const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
       if (n >= a.n) break;
       const double w = (a.R == 1) ? wm0 : a.wm_buf[n];
-      const int64_t gi = a.goff + n;
-      if (li >= 0 && !less_nan_last(lv, li, w, gi)) continue;
-      if (less_nan_last(w, gi, cv, ci)) {
-        cv = w;
-        ci = gi;
-      }
+      const uint32_t ln = (uint32_t)n;
+      const bool t = (int)(k == 0 || less_bf<0>(lv, ll, w, ln)) & (int)less_bf<0>(w, ln, cv, cl);
+      cv = t ? w : cv;
+      cl = t ? ln : cl;
     }
-    block_min1<0>(cv, ci, sc, par);
-    if (threadIdx.x == 0) {
-      a.tk_val[(int64_t)blk * a.K + k] = cv;
-      a.tk_idx[(int64_t)blk * a.K + k] = ci;
+    wave_pick_nl(cv, cl);
+    if (lane == 0) {
+      a.tk_val[list * a.K + k] = cv;
+      a.tk_idx[list * a.K + k] = cl == kNoLocal ? kNoIndex : a.goff + cl;
     }
     lv = cv;
-    li = ci;
+    ll = cl;
   }
   LB_STAMP(blk, 3);
 }
@@ -643,7 +686,7 @@ __device__ __forceinline__ Ent merge_path_at(const Ent* A, const Ent* B, int K, 
   return ent_less(A[i], B[j]) ? A[i] : B[j];
 }
 
-// Tree-merge L sorted K-lists in LDS (buf0 holds them; buf1 same size); every output
+// Tree-merge L sorted K-lists in LDS (the cross-shard merge_kernel) (buf0 holds them; buf1 same size); every output
 // element of a level is computed by its own thread.  Returns the buffer holding the merged
 // list (first K entries).
 __device__ __forceinline__ Ent* tree_merge(Ent* buf0, Ent* buf1, int L, int K) {
@@ -673,47 +716,89 @@ __device__ __forceinline__ Ent* tree_merge(Ent* buf0, Ent* buf1, int L, int K) {
 // final     (last block overall): look-ahead best over the block partials, the selected
 //           model's choice, each top-K model's best candidate; completes the record.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* smem, const Scratch& sc) {
+__device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* smem) {
   STAMP(0);
   const int tid = threadIdx.x;
-  const int M = f.nb_lb * f.K;
-  Ent* buf0 = reinterpret_cast<Ent*>(smem + kScratchBytes);
-  Ent* buf1 = buf0 + M;
-  for (int e = tid; e < M; e += kBlock) buf0[e] = Ent{f.tk_val[e], f.tk_idx[e]};
+  const int L = f.nb_lb * kWaves;          // one sorted K-list + argmin per look-back wave
+  const int K = f.K;
+  Ent* buf = reinterpret_cast<Ent*>(smem + kScratchBytes);
+  for (int e = tid; e < L * K; e += kBlock) buf[e] = Ent{f.tk_val[e], f.tk_idx[e]};
+  __syncthreads();
+  STAMP(1);
+  if (tid >= 64) return;                   // one wave merges; the caller re-converges
+  const int lane = tid;
+  auto local = [&](int64_t id) { return id == kNoIndex ? kNoLocal : (uint32_t)(id - f.goff); };
+  // argmin over the lists' argmins (rt.py:359)
   double v = f.nan_first ? __builtin_inf() : __builtin_nan("");
-  int64_t i = kNoIndex;
-  for (int b = tid; b < f.nb_lb; b += kBlock) {
-    const int64_t bi = f.am_idx[b];
+  uint32_t li = kNoLocal;
+  for (int b = lane; b < L; b += 64) {
     const double bv = f.am_val[b];
-    if (bi != kNoIndex && key_less(f.nan_first, bv, bi, v, i)) {
-      v = bv;
-      i = bi;
+    const uint32_t bl = local(f.am_idx[b]);
+    const bool t = (int)(bl != kNoLocal) &
+                   (int)(f.nan_first ? less_bf<1>(bv, bl, v, li) : less_bf<0>(bv, bl, v, li));
+    v = t ? bv : v;
+    li = t ? bl : li;
+  }
+  if (f.nan_first) wave_pick_nf(v, li);
+  else wave_pick_nl(v, li);
+  // top-K: K rounds of a wave pick over the list heads.  Lane owns lists lane + 64 j
+  // (j < kListsPerLane); its read positions are 8-bit fields of one register.
+  uint64_t pos = 0;
+  double hv;
+  uint32_t hl;
+  int hj;
+  auto head = [&]() {
+    hv = __builtin_nan("");
+    hl = kNoLocal;
+    hj = 0;
+#pragma unroll
+    for (int j = 0; j < kListsPerLane; ++j) {
+      const int l = lane + 64 * j;
+      const int p = (int)((pos >> (8 * j)) & 0xFF);
+      if (l < L && p < K) {
+        const Ent e = buf[l * K + p];
+        const uint32_t el = local(e.i);
+        const bool t = (int)(el != kNoLocal) & (int)less_bf<0>(e.v, el, hv, hl);
+        hv = t ? e.v : hv;
+        hl = t ? el : hl;
+        hj = t ? j : hj;
+      }
+    }
+  };
+  head();
+  double kv = __builtin_nan("");
+  uint32_t kl = kNoLocal;
+  for (int k = 0; k < K; ++k) {
+    double m = hv;
+    uint32_t w = hl;
+    wave_pick_nl(m, w);
+    if (lane == k) {
+      kv = m;
+      kl = w;
+    }
+    if (w == kNoLocal) break;              // wave-uniform: every list is exhausted
+    if (hl == w) {                         // the owner (local indices are unique)
+      pos += 1ull << (8 * hj);
+      head();
     }
   }
-  int par = 0;
-  if (f.nan_first) block_min1<1>(v, i, sc, par);   // its barrier also publishes buf0
-  else block_min1<0>(v, i, sc, par);
-  STAMP(1);
-  const Ent* r = tree_merge(buf0, buf1, f.nb_lb, f.K);
   STAMP(2);
   llampc_plan_out* o = f.out;
-  if (tid < LLAMPC_KMAX) {
-    const int k = tid;
-    const int64_t id = k < f.K ? r[k].i : kNoIndex;
-    if (id != kNoIndex) {
-      const int64_t li = id - f.goff;
-      o->topk[k] = id;
-      o->topk_val[k] = r[k].v;
-      o->topk_Df[k] = f.params[2 * f.n + li];
-      o->topk_Dr[k] = f.params[5 * f.n + li];
+  if (lane < LLAMPC_KMAX) {
+    const int k = lane;
+    if (k < K && kl != kNoLocal) {
+      o->topk[k] = f.goff + kl;
+      o->topk_val[k] = kv;
+      o->topk_Df[k] = f.params[2 * f.n + kl];
+      o->topk_Dr[k] = f.params[5 * f.n + kl];
     } else {
       o->topk[k] = -1;
       o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = __builtin_nan("");
     }
   }
-  if (tid == 0) {
-    o->lb_best = i == kNoIndex ? -1 : i;
-    o->lb_best_val = i == kNoIndex ? __builtin_nan("") : v;
+  if (lane == 0) {
+    o->lb_best = li == kNoLocal ? -1 : f.goff + li;
+    o->lb_best_val = li == kNoLocal ? __builtin_nan("") : v;
   }
 }
 
@@ -831,7 +916,7 @@ __global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, Lookahe
   if ((int)blockIdx.x < fin.nb_lb) {
     lookback_block(lb, blockIdx.x, sc);
     if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
-    if (fin.full) lb_final(fin, smem, sc);
+    if (fin.full) lb_final(fin, smem);
   } else {
     lookahead_block<INTEG, STAGE, LPM, XM>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
   }
@@ -1078,8 +1163,12 @@ size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u) {
 
 // Models per look-back lane: keep the block lists small enough for the in-LDS tree merge
 // (nb_lb * K <= 640 entries = 20 KB for both buffers).
+// Models per lane: lb_final holds blocks * kWaves * K entries in LDS and merges at most
+// 64 * kListsPerLane lists; R grows once blocks * K would pass 640 (40 KB of LDS) or the
+// blocks 64 * kListsPerLane / kWaves.
 int lookback_r(int64_t n, int32_t K) {
-  const int64_t per = (int64_t)kBlock * 640 / std::max(1, K);   // models per list budget
+  const int64_t blocks = std::min<int64_t>(640 / std::max(1, K), 64 * kListsPerLane / kWaves);
+  const int64_t per = (int64_t)kBlock * std::max<int64_t>(1, blocks);   // models per R step
   return (int)std::max<int64_t>(1, (n + per - 1) / per);
 }
 
@@ -1116,7 +1205,7 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
     lbv = *lb;
     lbv.R = lookback_r(lb->n, std::max(1, lb->K));
     f.nb_lb = lookback_blocks_r(lb->n, lbv.R);
-    if (lb->full) lds = std::max(lds, kScratchBytes + 2 * (size_t)f.nb_lb * lb->K * sizeof(Ent));
+    if (lb->full) lds = std::max(lds, kScratchBytes + (size_t)f.nb_lb * kWaves * lb->K * sizeof(Ent));
   }
   if (la) {
     lav = *la;

@@ -31,8 +31,8 @@ struct LookbackLaunch {
   int32_t R;             // models per lane (set by launch_plan)
   double* err_out;       // [n] or null
   double* wm_buf;        // [n] window means (always written when the window is full)
-  double* am_val;  int64_t* am_idx;   // [blocks]
-  double* tk_val;  int64_t* tk_idx;   // [blocks][K]
+  double* am_val;  int64_t* am_idx;   // [blocks * kWaves] (one per look-back wave)
+  double* tk_val;  int64_t* tk_idx;   // [blocks * kWaves][K]
 };
 
 struct LookaheadLaunch {

@@ -172,6 +172,38 @@ def test_lookback_nan_semantics(nat):
             np.testing.assert_array_equal(r["topk"], e.argsort(kind="stable")[:10])
 
 
+@pytest.mark.parametrize("N,K", [(200_000, 10), (200_000, 1), (60_000, 32)])
+def test_lookback_selection_ties_nans_many_lists(nat, N, K):
+    """The look-back selection at sizes where each lane ranks several models (R > 1) and
+    lb_final merges hundreds of per-wave lists (up to its 512-list cap at K = 1), with exact
+    ties (duplicated models: equal errors -> lower index first, the stable argsort) and NaN
+    models (argmin: first NaN under NaN-first; argsort: NaN last).  Expected indices come from
+    the kernel's own errors (the selection is exact); the errors match the oracle."""
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    p = generate_bank(N, seed=5)
+    e0 = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), s[:, 0], u[:, 0], TS), s[:, 1])
+    best = int(np.argmin(e0))
+    dup = np.array([i for i in (best + 7, best + 3001, best + 45_000, N - 1, 3) if 0 <= i < N and i != best])
+    p[:, dup] = p[:, [best]]                      # exact ties with the best model
+    p[2, [11, N // 2]] = np.nan                  # NaN models
+    with np.errstate(all="ignore"):
+        e = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), s[:, 0], u[:, 0], TS), s[:, 1])
+    for policy in (0, 1):
+        with ModelBank(p, W=1, device=0) as b:
+            r = b.lookback(s[:, 0], u[:, 0], s[:, 1], Ts=TS, K=K, nan_policy=policy, return_errors=True)
+        g = r["errors"]
+        close(g, e, RTOL_STEP)
+        assert np.array_equal(np.isnan(g), np.isnan(e))
+        assert np.all(g[dup] == g[best])
+        if policy == 0:
+            assert r["best"] == int(np.argmin(g)) == 11
+        else:
+            assert r["best"] == int(np.nanargmin(g))
+        np.testing.assert_array_equal(r["topk"][:K], g.argsort(kind="stable")[:K])
+
+
 # ----------------------------------------------------------------- look-ahead (a8-a10)
 def test_lookahead_rk4_rollout_and_cost_vs_golden(nat):
     from llampc import _native
