@@ -169,7 +169,9 @@ def main():
     torch.cuda.set_device(dev_index)
     _DEV[0] = dev_index
     local = dev_index
-    if world > 1:
+    # LLAMPC_FORCE_EXCHANGE=1 (diagnostic, under torch.distributed.run with one rank): the
+    # tick runs the collective + device merge of the N > 1 path on a 1-rank group
+    if world > 1 or os.environ.get("LLAMPC_FORCE_EXCHANGE"):
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
         else:
@@ -206,6 +208,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+    t_issue = time.perf_counter() - t0       # host time to enqueue the K ticks
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -255,13 +258,14 @@ def main():
                                    f"C={C}, {args.scenario or ('sudden' if args.track == 'ETHZMobil' else 'gradual')} friction",
                        "N_models_total": N_total,
                        "N_models_per_gpu": N_local, "H": H, "C": C, "W": W, "K": K, "Ts": 0.02,
-                       "track": args.track, "parallelism": f"bank-shard x{world}" + (" + 1 RCCL all-gather/tick" if world > 1 else "")},
+                       "track": args.track, "parallelism": f"bank-shard x{world}" + (" + 1 RCCL all-gather/tick" if sb.exchange else "")},
             "roofline": roof,
             "valu": {"bound": "fp64-valu", "achieved_gflops": valu_gf, "peak_tflops": FP64_VALU_PEAK_TFLOPS,
                      "frac": valu_gf / (FP64_VALU_PEAK_TFLOPS * 1e3) if valu_gf else None,
                      "flops_per_model_step": FLOPS_PER_MODEL_STEP,
                      "note": "plain flops only; the 29 fp64 transcendentals per RK4 step are excluded"},
             "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0])},
+            "host_issue_us_per_step": t_issue / args.steps * 1e6,
             "lpm": lpm_of(N_local, C),
             "result_check": {"sel_model": merged.best_model, "window_full": merged.window_full,
                              "sel_cand": merged.best_cand, "n_nonfinite": merged.n_nonfinite},
@@ -272,7 +276,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     sb.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

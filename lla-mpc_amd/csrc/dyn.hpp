@@ -238,8 +238,24 @@ __device__ __forceinline__ double dpp_bcast(double v) {
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
-// quad_perm broadcasts within lane pairs: [0,0,2,2] = 0xA0, [1,1,3,3] = 0xF5.
+// quad_perm broadcasts within lane pairs: [0,0,2,2] = 0xA0, [1,1,3,3] = 0xF5; within a
+// quad: lane q to all four = 0x00, 0x55, 0xAA, 0xFF; xor-1 / xor-2 swaps = 0xB1, 0x4E.
 constexpr int kPair0 = 0xA0, kPair1 = 0xF5;
+constexpr int kQuad0 = 0x00, kQuad1 = 0x55, kQuad2 = 0xAA, kQuad3 = 0xFF;
+constexpr int kQuadX1 = 0xB1, kQuadX2 = 0x4E;
+
+// Polynomial scheme of the fast chain: Horner.  Estrin (-DLLAMPC_CHAIN_EST=1, A/B builds)
+// shortens the chain's dependency depth but adds instructions, and the stage is issue-
+// bound even at LPM 4 (measured: 4.7 shader cycles per instruction at one wave per SIMD;
+// Estrin +1 us per tick at LPM 2 and 4).
+template <int LPM>
+struct ChainEst {
+#ifdef LLAMPC_CHAIN_EST
+  static constexpr bool value = LLAMPC_CHAIN_EST != 0;
+#else
+  static constexpr bool value = false;
+#endif
+};
 
 // One tire's constants in this lane: front (lw = lf, sg = +1) or rear (lw = lr, sg = -1).
 struct Chain {
@@ -282,16 +298,56 @@ struct Dom {
 // F = D sin(C atan(B slip)) with slip = dsel - atan2(yy, den) for the front tire
 // (dsel = delta) and atan2(yy, den) for the rear (dsel = 0); yy = lf om + vy | lr om - vy
 // (dynamic.py:149-152 / :215-220).  The divisors go to the lane's Dom.
+template <bool EST>
 __device__ __forceinline__ double chain_fast(const Chain& c, double den, double vy, double om,
                                              double dsel, Dom& dm, const fm::FmK& K) {
   const double yy = fma(c.lw, om, c.sg * vy);
   double h2, hz;
-  const double a2 = fm::atan2_fast(yy, den, K, h2);
+  const double a2 = fm::atan2_fast<EST>(yy, den, K, h2);
   const double z = c.B * fma(-c.sg, a2, dsel);
-  const double at = fm::atan_fast(z, K, hz);
+  const double at = fm::atan_fast<EST>(z, K, hz);
   dm.lo = fmin(dm.lo, h2);
   dm.hi = fmax(dm.hi, fmax(h2, hz));
-  return c.D * fm::sin_wide(c.C * at, K);
+  return c.D * fm::sin_wide<EST>(c.C * at, K);
+}
+
+// LPM = 4: the quad's lanes run ONE instruction stream — lanes 0/1 the front/rear chain,
+// lanes 2/3 the same chains (wasted) up to the final sine, whose argument is theirs:
+// lane 2 sin(psi), lane 3 cos(psi), so sincos(psi) costs no polynomial of its own.
+// psi = r + k pi (2k = nearest even integer to psi 2/pi, 3-part Cody-Waite by pi/2, |r| <=
+// pi/2); sin psi = sin((-1)^k r), cos psi = sin((-1)^k (pi/2 - |r|)).  Per lane:
+// c.C = C (lanes 0/1) or 0 (2/3), c.D = D or 1, ra = the |r| mask of the high word (lane 3
+// clears the sign), pm = 0 / 1 / -1 and po = 0 / 0 / pi/2 place the angle argument
+// po + pm r' (exactly 0 in lanes 0/1, so their argument is C atan(.) as at LPM 1/2).
+__device__ __forceinline__ double chain_fold(const Chain& c, double den, double vy, double om,
+                                             double dsel, double psi, int ra, double pm,
+                                             double po, Dom& dm, const fm::FmK& K) {
+  constexpr bool EST = ChainEst<4>::value;
+  const double t2 = fma(psi, K.two_pi, K.rmagic2);       // 2^53 (1.5 + 2k 2^-53): ulp 2
+  const double k2 = t2 - K.rmagic2;
+  double r = fma(-k2, K.cw0, psi);
+  r = fma(-k2, K.cw1, r);
+  r = fma(-k2, K.cw2, r);
+  const double rr = __hiloint2double(__double2hiint(r) & ra, __double2loint(r));
+  const double pa = fma(pm, rr, po);
+  const int fs = __double2loint(t2) << 31;               // (-1)^k on the argument
+  const double arg_psi = __hiloint2double(__double2hiint(pa) ^ fs, __double2loint(pa));
+#ifdef LLAMPC_FOLD_MASK   // A/B: lanes 2/3 masked off (exec) during the chain's atans
+  double at = 0.0;
+  if (pm == 0.0) {
+#else
+  double at;
+  {
+#endif
+    const double yy = fma(c.lw, om, c.sg * vy);
+    double h2, hz;
+    const double a2 = fm::atan2_fast<EST>(yy, den, K, h2);
+    const double z = c.B * fma(-c.sg, a2, dsel);
+    at = fm::atan_fast<EST>(z, K, hz);
+    dm.lo = fmin(dm.lo, h2);
+    dm.hi = fmax(dm.hi, fmax(h2, hz));
+  }
+  return c.D * fm::sin_wide<EST>(fma(c.C, at, arg_psi), K);
 }
 
 // Per-rollout constants of the fast stage.  ch[0] is this lane's chain (LPM = 2) or the
@@ -301,23 +357,32 @@ struct StageK {
   Chain ch[2];
   double fw;
   double k1, k2, k0, k3;   // Frx = (k1 - k2 vx) a - k0 - k3 vx^2; input_acc: (mass, 0, 0, 0)
+  double pm, po;           // LPM = 4: the angle argument of chain_fold
+  int ra;
   bool sok;
 };
 
 template <int LPM>
 __device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int sub) {
-  const bool front = (LPM == 1) || sub == 0;
+  const bool front = (LPM == 1) || (sub & 1) == 0;
   StageK s;
   s.ch[0] = make_chain(v, t, front);
   s.ch[1] = make_chain(v, t, false);
   s.fw = front ? 1.0 : 0.0;
+  s.pm = sub == 2 ? 1.0 : (sub == 3 ? -1.0 : 0.0);
+  s.po = sub == 3 ? fm::kPio2 : 0.0;
+  s.ra = sub == 3 ? 0x7FFFFFFF : -1;
   // dynamic.py:141 (input_acc: mass * a) as the :146 form with (mass, 0, 0, 0): equal for
   // finite vx (a non-finite vx is outside the chain domain -> the general rhs)
   s.k1 = v.input_acc ? v.mass : v.Cm1;
   s.k2 = v.input_acc ? 0.0 : v.Cm2;
   s.k0 = v.input_acc ? 0.0 : v.Cr0;
   s.k3 = v.input_acc ? 0.0 : v.Cr2;
-  s.sok = chain_static_ok(s.ch[0]) && ((LPM == 2) || chain_static_ok(s.ch[1])) && !v.approx;
+  s.sok = chain_static_ok(s.ch[0]) && ((LPM >= 2) || chain_static_ok(s.ch[1])) && !v.approx;
+  if (LPM == 4 && sub >= 2) {   // lanes 2/3: the chain's sine takes the psi argument alone
+    s.ch[0].C = 0.0;
+    s.ch[0].D = 1.0;
+  }
   return s;
 }
 
@@ -341,8 +406,22 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const 
   const double den = (F == Form::Ref) ? fabs(vx) : vx;
   dm.ps = fmax(dm.ps, fabs(x[2]));
   double Ffy, Fry;
+  if (LPM == 4) {
+    const double r = chain_fold(sk.ch[0], den, vy, om, d * sk.fw, x[2], sk.ra, sk.pm, sk.po, dm, K);
+    Ffy = dpp_bcast<kQuad0>(r);
+    Fry = dpp_bcast<kQuad1>(r);
+    const double sp = dpp_bcast<kQuad2>(r), cp = dpp_bcast<kQuad3>(r);
+    const double Frx = (sk.k1 - sk.k2 * vx) * u.a - sk.k0 - sk.k3 * (vx * vx);
+    dx[0] = vx * cp - vy * sp;
+    dx[1] = vx * sp + vy * cp;
+    dx[2] = om;
+    dx[3] = v.inv_mass * (Frx - Ffy * sd) + vy * om;
+    dx[4] = v.inv_mass * (Fry + Ffy * cd) - vx * om;
+    dx[5] = v.inv_Iz * (Ffy * v.lf * cd - Fry * v.lr);
+    return;
+  }
   if (LPM == 2) {
-    const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
+    const double r = chain_fast<ChainEst<2>::value>(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
 #ifdef LLAMPC_ABL_NODPP   // diagnostic ablation builds only
     Ffy = r;
     Fry = r * 0.5;
@@ -351,8 +430,8 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const 
     Fry = dpp_bcast<kPair1>(r);
 #endif
   } else {
-    Ffy = chain_fast(sk.ch[0], den, vy, om, d, dm, K);
-    Fry = chain_fast(sk.ch[1], den, vy, om, 0.0, dm, K);
+    Ffy = chain_fast<ChainEst<1>::value>(sk.ch[0], den, vy, om, d, dm, K);
+    Fry = chain_fast<ChainEst<1>::value>(sk.ch[1], den, vy, om, 0.0, dm, K);
   }
   double sp, cp;
 #ifdef LLAMPC_ABL_NOPSI   // diagnostic ablation builds only

@@ -207,7 +207,7 @@ constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 4 
 // issue slots per use — 2.5x on a Horner chain in the one-wave-per-SIMD regime.
 struct FmK {
   double at[22], sw[11], sq[7], cq[7];
-  double pio2, pio2t, two_pi, cw0, cw1, cw2, sixth, six, rmagic;
+  double pio2, pio2t, two_pi, cw0, cw1, cw2, sixth, six, rmagic, rmagic2;
 
   __device__ __forceinline__ static void pin(double& x) { asm volatile("" : "+v"(x)); }
   __device__ __forceinline__ static FmK load() {
@@ -232,8 +232,9 @@ struct FmK {
     k.sixth = 1.0 / 6.0;
     k.six = 6.0;
     k.rmagic = 0x1.8p52;
+    k.rmagic2 = 0x1.8p53;
     pin(k.pio2); pin(k.pio2t); pin(k.two_pi); pin(k.cw0); pin(k.cw1); pin(k.cw2);
-    pin(k.sixth); pin(k.six); pin(k.rmagic);
+    pin(k.sixth); pin(k.six); pin(k.rmagic); pin(k.rmagic2);
     return k;
   }
 };
@@ -276,9 +277,33 @@ __device__ __forceinline__ double div6(double v, const FmK& K) {
   return fma(fma(-K.six, q, v), K.sixth, q);
 }
 
+// Estrin forms of the fast cores' polynomials: dependency depth 5 (22 terms) / 4 (11 terms)
+// instead of 21 / 10 for +4 / +3 instructions.  With one wave per SIMD a dependent fp64 FMA
+// costs ~6 cycles and an independent one ~4 (issue), so a chain that nothing else can fill
+// — the tire chain of a lane-split rollout (LPM >= 2) — is faster in Estrin form.
+__device__ __forceinline__ double estrin22(const double* c, double s) {
+  const double s2 = s * s, s4 = s2 * s2, s8 = s4 * s4, s16 = s8 * s8;
+  const double p0 = fma(c[1], s, c[0]), p1 = fma(c[3], s, c[2]), p2 = fma(c[5], s, c[4]),
+               p3 = fma(c[7], s, c[6]), p4 = fma(c[9], s, c[8]), p5 = fma(c[11], s, c[10]),
+               p6 = fma(c[13], s, c[12]), p7 = fma(c[15], s, c[14]), p8 = fma(c[17], s, c[16]),
+               p9 = fma(c[19], s, c[18]), p10 = fma(c[21], s, c[20]);
+  const double q0 = fma(p1, s2, p0), q1 = fma(p3, s2, p2), q2 = fma(p5, s2, p4),
+               q3 = fma(p7, s2, p6), q4 = fma(p9, s2, p8);
+  const double r0 = fma(q1, s4, q0), r1 = fma(q3, s4, q2), r2 = fma(p10, s4, q4);
+  return fma(r2, s16, fma(r1, s8, r0));
+}
+__device__ __forceinline__ double estrin11(const double* c, double s) {
+  const double s2 = s * s, s4 = s2 * s2, s8 = s4 * s4;
+  const double p0 = fma(c[1], s, c[0]), p1 = fma(c[3], s, c[2]), p2 = fma(c[5], s, c[4]),
+               p3 = fma(c[7], s, c[6]), p4 = fma(c[9], s, c[8]);
+  const double q0 = fma(p1, s2, p0), q1 = fma(p3, s2, p2), q2 = fma(c[10], s2, p4);
+  return fma(q2, s8, fma(q1, s4, q0));
+}
+
+template <bool EST = false>
 __device__ __forceinline__ double atan_core_k(double t, const FmK& K) {
   const double s = t * t;
-  return fma(t * s, horner<22>(K.at, s), t);
+  return fma(t * s, EST ? estrin22(K.at, s) : horner<22>(K.at, s), t);
 }
 
 // atan2(y, x) for x >= 0 on the domain atan2_fast_ok(y, x): the sum |y| + x in
@@ -289,10 +314,11 @@ __device__ __host__ __forceinline__ bool atan2_fast_ok(double y, double x) {
 }
 // hi = max(|y|, x), the divisor: hi in [2^-1000, 2^999] lies inside the domain (the
 // rollout checks its running extremes once, dyn.hpp Dom).
+template <bool EST = false>
 __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K, double& hi) {
   const double ay = fabs(y);
   hi = fmax(ay, x);
-  const double r = atan_core_k(div_fast(fmin(ay, x), hi), K);
+  const double r = atan_core_k<EST>(div_fast(fmin(ay, x), hi), K);
   const double o = (ay > x) ? (K.pio2 - r) + K.pio2t : r;
   return copysign(o, y);
 }
@@ -305,10 +331,11 @@ __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K) {
 // (exact when |z| <= 1).
 __device__ __host__ __forceinline__ bool atan_fast_ok(double z) { return fabs(z) <= 0x1p1000; }
 // hz = max(|z|, 1), the divisor: hz <= 2^1000 is the domain.
+template <bool EST = false>
 __device__ __forceinline__ double atan_fast(double z, const FmK& K, double& hz) {
   const double az = fabs(z);
   hz = fmax(az, 1.0);
-  const double r = atan_core_k(div_fast(fmin(az, 1.0), hz), K);
+  const double r = atan_core_k<EST>(div_fast(fmin(az, 1.0), hz), K);
   const double o = (az > 1.0) ? (K.pio2 - r) + K.pio2t : r;
   return copysign(o, z);
 }
@@ -319,9 +346,10 @@ __device__ __forceinline__ double atan_fast(double z, const FmK& K) {
 
 // sin(a) for |a| <= kSinWideMax, one polynomial (the Pacejka argument C*atan(.) is
 // bounded by |C| pi/2, so |C| <= 1.9 keeps every call in range).
+template <bool EST = false>
 __device__ __forceinline__ double sin_wide(double a, const FmK& K) {
   const double s = a * a;
-  return fma(a * s, horner<11>(K.sw, s), a);
+  return fma(a * s, EST ? estrin11(K.sw, s) : horner<11>(K.sw, s), a);
 }
 
 // sincos(a) for |a| <= kSinCosMax (NaN/inf -> not ok): Cody-Waite reduction, quadrant

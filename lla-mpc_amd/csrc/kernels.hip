@@ -40,11 +40,20 @@ __device__ unsigned long long g_lb_stamps[8][8][2];   // first 8 look-back block
       g_lb_stamps[blk][slot][1] = __builtin_amdgcn_s_memrealtime();                      \
     }                                                                                    \
   } while (0)
+__device__ unsigned long long g_la_all[1024][4][2];    // every look-ahead block, last launch
 #define LA_STAMP(blk, slot)                                                              \
   do {                                                                                   \
-    if (threadIdx.x == 0 && (blk) < 8) {                                                 \
-      g_la_stamps[blk][slot][0] = __builtin_amdgcn_s_memtime();                          \
-      g_la_stamps[blk][slot][1] = __builtin_amdgcn_s_memrealtime();                      \
+    if (threadIdx.x == 0) {                                                              \
+      const unsigned long long c_ = __builtin_amdgcn_s_memtime();                        \
+      const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                    \
+      if ((blk) < 8) {                                                                   \
+        g_la_stamps[blk][slot][0] = c_;                                                  \
+        g_la_stamps[blk][slot][1] = r_;                                                  \
+      }                                                                                  \
+      if ((blk) < 1024) {                                                                \
+        g_la_all[blk][slot][0] = c_;                                                     \
+        g_la_all[blk][slot][1] = r_;                                                     \
+      }                                                                                  \
     }                                                                                    \
   } while (0)
 #define STAMP(slot)                                                                      \
@@ -609,6 +618,11 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
         const int bi = bad;
         bad = __builtin_amdgcn_mov_dpp(bi, kPair0, 0xF, 0xF, false) |
               __builtin_amdgcn_mov_dpp(bi, kPair1, 0xF, 0xF, false);
+      } else if (LPM == 4) {            // the quad shares one rollout
+        int bi = bad;
+        bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX1, 0xF, 0xF, false);
+        bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX2, 0xF, 0xF, false);
+        bad = bi;
       }
       if (__builtin_expect(__any(bad), 0)) {
         bool unused = false;
@@ -1155,17 +1169,20 @@ int lookahead_group(int32_t C) {
   return G;
 }
 
-// Lanes per rollout: split the two tire chains over a lane pair while the launch has
-// fewer waves than the chip has SIMDs (latency-bound: a wave's time is its instruction
-// stream); one lane per rollout once the chip fills (fewest instructions per rollout).
+// Lanes per rollout while the launch has fewer waves than the chip has SIMDs (latency-
+// bound: a wave's time is its instruction stream): a quad (LPM = 4: front chain, rear
+// chain, sin psi, cos psi in one stream) up to 16k rollouts, a lane pair (front / rear
+// chain) up to 32k; one lane per rollout once the chip fills (fewest instructions per
+// rollout).
 int lookahead_lpm(int64_t n, int32_t C, int32_t integrator) {
   if (integrator == LLAMPC_RK6) return 1;
   const int G = lookahead_group(C);
   if (const char* e = getenv("LLAMPC_LPM")) {     // benchmarking override
     const int v = atoi(e);
-    if (v == 1 || (v == 2 && 2 * G <= kBlock)) return v;
+    if (v == 1 || ((v == 2 || v == 4) && v * G <= kBlock)) return v;
   }
   const int64_t lanes = n * G;
+  if (lanes <= 16384 && 4 * G <= kBlock) return 4;
   return (lanes <= 32768 && 2 * G <= kBlock) ? 2 : 1;
 }
 
@@ -1231,7 +1248,8 @@ static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, c
 template <int INTEG, bool STAGE>
 static void launch_plan_l(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
                           int G, int cpl, int lpm, size_t lds, hipStream_t s) {
-  if (lpm == 2) launch_plan_t<INTEG, STAGE, 2>(lb, la, f, G, cpl, lds, s);
+  if (lpm == 4) launch_plan_t<INTEG, STAGE, 4>(lb, la, f, G, cpl, lds, s);
+  else if (lpm == 2) launch_plan_t<INTEG, STAGE, 2>(lb, la, f, G, cpl, lds, s);
   else launch_plan_t<INTEG, STAGE, 1>(lb, la, f, G, cpl, lds, s);
 }
 
@@ -1288,6 +1306,9 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
 #ifdef LLAMPC_STAMPS
 extern "C" int llampc_debug_lb_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lb_stamps), sizeof(g_lb_stamps)) == hipSuccess ? 0 : -2;
+}
+extern "C" int llampc_debug_la_all(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_all), sizeof(g_la_all)) == hipSuccess ? 0 : -2;
 }
 extern "C" int llampc_debug_la_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_stamps), sizeof(g_la_stamps)) == hipSuccess ? 0 : -2;

@@ -59,8 +59,12 @@ class ShardedBank:
         self._torch = torch
         self.d_local = torch.empty(B, dtype=torch.uint8, device=dev)
         self.d_all = torch.empty(B * world, dtype=torch.uint8, device=dev)
-        # one shard: its record IS the result (no gather, no merge launch)
-        self.d_merged = torch.empty(B, dtype=torch.uint8, device=dev) if world > 1 else self.d_local
+        # one shard: its record IS the result (no gather, no merge launch).
+        # LLAMPC_FORCE_EXCHANGE=1 runs the exchange anyway (a 1-rank group): measures the
+        # collective + merge cost per tick on one GPU (diagnostic)
+        import os
+        self.exchange = world > 1 or (self.backend is not None and bool(os.environ.get("LLAMPC_FORCE_EXCHANGE")))
+        self.d_merged = torch.empty(B, dtype=torch.uint8, device=dev) if self.exchange else self.d_local
         self.h_merged = torch.empty(B, dtype=torch.uint8).pin_memory()
         self._inputs = None
 
@@ -108,7 +112,7 @@ class ShardedBank:
         lib = nat.load()
         nat.check(lib.llampc_plan_device(self.bank.handle, C.byref(pin), self.d_local.data_ptr(),
                                          None, None, None, s.cuda_stream))
-        if self.world > 1:
+        if self.exchange:
             import torch.distributed as dist
             if self.backend == "nccl":
                 with torch.cuda.stream(s):

@@ -502,7 +502,7 @@ def test_lookahead_out_of_domain_fallback(nat):
     """Rollouts whose operands leave the fast cores' domains take the general evaluation
     (dyn.hpp rhs_fast): models with |C| > 1.9, a yaw beyond 2^20 pi/2, a standing start
     (|y| + |vx| = 0), and a linear-tire bank — all against the oracle, in waves that mix
-    fast and fallback lanes (both LPM = 1 and the lane-pair split)."""
+    fast and fallback lanes (LPM = 1, the lane-pair split and the quad with folded sincos)."""
     from llampc.mpc import ModelBank, generate_bank
     N, C, H = 640, 3, 12
     p = generate_bank(N, seed=11)
@@ -520,7 +520,7 @@ def test_lookahead_out_of_domain_fallback(nat):
         with np.errstate(all="ignore"):
             traj = O.rollout_rk4(shared(), tuple(p), x0, U, TS)
             cref = O.mpc_cost(traj, U, xref, np.zeros(2), Q, R, P)
-        for lpm in ("1", "2"):
+        for lpm in ("1", "2", "4"):
             os.environ["LLAMPC_LPM"] = lpm
             try:
                 with ModelBank(p, device=0) as b:

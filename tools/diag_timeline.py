@@ -4,7 +4,7 @@
 import ctypes, os, sys
 import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["LLAMPC_HIP_LIB"] = os.path.join(REPO, "lla-mpc_amd/llampc/_lib/libllampc_hip_stamps.so")
+os.environ.setdefault("LLAMPC_HIP_LIB", os.path.join(REPO, "lla-mpc_amd/llampc/_lib/libllampc_hip_stamps.so"))
 sys.path[:0] = [REPO, os.path.join(REPO, "lla-mpc_amd")]
 from llampc import _native as nat
 from llampc.mpc import ModelBank, generate_bank
@@ -43,5 +43,17 @@ for k in range(8):
     print(f"look-back block {k}: start {us(B[k,0,1]):.2f}, step+ring+mean end {us(B[k,1,1]):.2f}, "
           f"argmin end {us(B[k,2,1]):.2f}, top-K end {us(B[k,3,1]):.2f}  "
           f"(cycles {B[k,1,0]-B[k,0,0]}, {B[k,2,0]-B[k,1,0]}, {B[k,3,0]-B[k,2,0]})")
+ALL = (ctypes.c_ulonglong * (1024 * 4 * 2))()
+lib.llampc_debug_la_all.argtypes = [ctypes.c_void_p]
+lib.llampc_debug_la_all(ALL)
+Z = np.frombuffer(ALL, dtype=np.uint64).reshape(1024, 4, 2).astype(np.int64)
+nla = int((Z[:, 3, 1] >= A[:, 0].min()).sum())
+Z = Z[:nla]
+q = lambda v: f"{np.min(v):.2f}/{np.median(v):.2f}/{np.max(v):.2f}"
+print(f"all {nla} look-ahead blocks (min/median/max): start {q(us(Z[:,0,1]))}, staged {q(us(Z[:,1,1]))}, "
+      f"rolled out {q(us(Z[:,2,1]))}, reduced {q(us(Z[:,3,1]))}")
+cyc = Z[:, 2, 0] - Z[:, 1, 0]
+rt = (Z[:, 2, 1] - Z[:, 1, 1]) / 100.0
+print(f"rollout per block: {q(rt)} us, {q(cyc)} shader cycles, clock {np.median(cyc / rt) / 1e3:.2f} GHz")
 print(f"lb_final: {us(R[0]):.2f} -> {us(R[1]):.2f} -> {us(R[2]):.2f}")
 print(f"final_select: {us(R[3]):.2f} -> {us(R[4]):.2f} -> {us(R[5]):.2f}")
