@@ -306,8 +306,8 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
   const double a2 = fm::atan2_fast<EST>(yy, den, K, h2);
   const double z = c.B * fma(-c.sg, a2, dsel);
   const double at = fm::atan_fast<EST>(z, K, hz);
-  dm.lo = fmin(dm.lo, h2);
-  dm.hi = fmax(dm.hi, fmax(h2, hz));
+  dm.lo = fm::vmin(dm.lo, h2);
+  dm.hi = fm::vmax(dm.hi, fm::vmax(h2, hz));
   return c.D * fm::sin_wide<EST>(c.C * at, K);
 }
 
@@ -344,8 +344,8 @@ __device__ __forceinline__ double chain_fold(const Chain& c, double den, double 
     const double a2 = fm::atan2_fast<EST>(yy, den, K, h2);
     const double z = c.B * fma(-c.sg, a2, dsel);
     at = fm::atan_fast<EST>(z, K, hz);
-    dm.lo = fmin(dm.lo, h2);
-    dm.hi = fmax(dm.hi, fmax(h2, hz));
+    dm.lo = fm::vmin(dm.lo, h2);
+    dm.hi = fm::vmax(dm.hi, fm::vmax(h2, hz));
   }
   return c.D * fm::sin_wide<EST>(fma(c.C, at, arg_psi), K);
 }
@@ -362,8 +362,11 @@ struct StageK {
   bool sok;
 };
 
+// psi_scale: LPM = 4 lanes 2/3 return psi_scale sin(psi), psi_scale cos(psi) (the fused RK4
+// passes h, so the stage increments need no h vx, h vy products).
 template <int LPM>
-__device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int sub) {
+__device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int sub,
+                                             double psi_scale = 1.0) {
   const bool front = (LPM == 1) || (sub & 1) == 0;
   StageK s;
   s.ch[0] = make_chain(v, t, front);
@@ -381,9 +384,38 @@ __device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int s
   s.sok = chain_static_ok(s.ch[0]) && ((LPM >= 2) || chain_static_ok(s.ch[1])) && !v.approx;
   if (LPM == 4 && sub >= 2) {   // lanes 2/3: the chain's sine takes the psi argument alone
     s.ch[0].C = 0.0;
-    s.ch[0].D = 1.0;
+    s.ch[0].D = psi_scale;
   }
   return s;
+}
+
+// Tire forces and sin/cos(psi) of one fast stage, in every lane of the rollout.
+struct StageF {
+  double Ffy, Fry, sp, cp;
+};
+template <int LPM>
+__device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, double vy, double om,
+                                              double d, double psi, const fm::FmK& K, Dom& dm) {
+  StageF f;
+  dm.ps = fm::vmax_abs(psi, dm.ps);
+  if (LPM == 4) {
+    const double r = chain_fold(sk.ch[0], den, vy, om, d * sk.fw, psi, sk.ra, sk.pm, sk.po, dm, K);
+    f.Ffy = dpp_bcast<kQuad0>(r);
+    f.Fry = dpp_bcast<kQuad1>(r);
+    f.sp = dpp_bcast<kQuad2>(r);
+    f.cp = dpp_bcast<kQuad3>(r);
+    return f;
+  }
+  if (LPM == 2) {
+    const double r = chain_fast<ChainEst<2>::value>(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
+    f.Ffy = dpp_bcast<kPair0>(r);
+    f.Fry = dpp_bcast<kPair1>(r);
+  } else {
+    f.Ffy = chain_fast<ChainEst<1>::value>(sk.ch[0], den, vy, om, d, dm, K);
+    f.Fry = chain_fast<ChainEst<1>::value>(sk.ch[1], den, vy, om, 0.0, dm, K);
+  }
+  fm::sincos_fast(psi, &f.sp, &f.cp, K);
+  return f;
 }
 
 // dx/dt on the fast path.  No fallback and no domain test here: the operands go to `dm`;
@@ -403,50 +435,15 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const 
     cd = 1.0;
     vx = 0.05;
   }
-  const double den = (F == Form::Ref) ? fabs(vx) : vx;
-  dm.ps = fmax(dm.ps, fabs(x[2]));
-  double Ffy, Fry;
-  if (LPM == 4) {
-    const double r = chain_fold(sk.ch[0], den, vy, om, d * sk.fw, x[2], sk.ra, sk.pm, sk.po, dm, K);
-    Ffy = dpp_bcast<kQuad0>(r);
-    Fry = dpp_bcast<kQuad1>(r);
-    const double sp = dpp_bcast<kQuad2>(r), cp = dpp_bcast<kQuad3>(r);
-    const double Frx = (sk.k1 - sk.k2 * vx) * u.a - sk.k0 - sk.k3 * (vx * vx);
-    dx[0] = vx * cp - vy * sp;
-    dx[1] = vx * sp + vy * cp;
-    dx[2] = om;
-    dx[3] = v.inv_mass * (Frx - Ffy * sd) + vy * om;
-    dx[4] = v.inv_mass * (Fry + Ffy * cd) - vx * om;
-    dx[5] = v.inv_Iz * (Ffy * v.lf * cd - Fry * v.lr);
-    return;
-  }
-  if (LPM == 2) {
-    const double r = chain_fast<ChainEst<2>::value>(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
-#ifdef LLAMPC_ABL_NODPP   // diagnostic ablation builds only
-    Ffy = r;
-    Fry = r * 0.5;
-#else
-    Ffy = dpp_bcast<kPair0>(r);
-    Fry = dpp_bcast<kPair1>(r);
-#endif
-  } else {
-    Ffy = chain_fast<ChainEst<1>::value>(sk.ch[0], den, vy, om, d, dm, K);
-    Fry = chain_fast<ChainEst<1>::value>(sk.ch[1], den, vy, om, 0.0, dm, K);
-  }
-  double sp, cp;
-#ifdef LLAMPC_ABL_NOPSI   // diagnostic ablation builds only
-  sp = x[2] * 0.5;
-  cp = x[2] * 0.25;
-#else
-  fm::sincos_fast(x[2], &sp, &cp, K);
-#endif
+  // den = vx: the fast atan2 takes |den| (Ref: atan2(., |vx|); Nlp: vx >= vmin after the clamp)
+  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, x[2], K, dm);
   const double Frx = (sk.k1 - sk.k2 * vx) * u.a - sk.k0 - sk.k3 * (vx * vx);
-  dx[0] = vx * cp - vy * sp;
-  dx[1] = vx * sp + vy * cp;
+  dx[0] = vx * f.cp - vy * f.sp;
+  dx[1] = vx * f.sp + vy * f.cp;
   dx[2] = om;
-  dx[3] = v.inv_mass * (Frx - Ffy * sd) + vy * om;
-  dx[4] = v.inv_mass * (Fry + Ffy * cd) - vx * om;
-  dx[5] = v.inv_Iz * (Ffy * v.lf * cd - Fry * v.lr);
+  dx[3] = v.inv_mass * (Frx - f.Ffy * sd) + vy * om;
+  dx[4] = v.inv_mass * (f.Fry + f.Ffy * cd) - vx * om;
+  dx[5] = v.inv_Iz * (f.Ffy * v.lf * cd - f.Fry * v.lr);
 }
 
 __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::FmK& K,
@@ -457,6 +454,75 @@ __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::F
   fm::sincos_fast(d, &u.sd, &u.cd, K);
   bad = (int)bad | (int)!fm::sincos_fast_ok(d);
   return u;
+}
+
+// Fused RK4 of the look-ahead rollouts: the stage increments k = h f(y) are formed directly
+// (h folded into the force and geometry constants, Frx as a polynomial in vx with per-step
+// coefficients) and the update is x + (k1 + 2k2 + 2k3 + k4) * (1/6) as one FMA — the
+// arithmetic of rk4_step / dynamic.py:98-115 with other roundings of its products and sums
+// (~1 ulp per step, the transcendental cores' class; tests/test_gpu_parity.py bounds the
+// rollouts at 1e-7 relative).  42 fewer instructions per step than step_fast's reference
+// roundings, which the look-back keeps (its errors are ranked against the oracle's).
+struct FusedK {
+  double h, hm, hIlf, hIlr, m1, m0, m2, m3;   // hm = h/m; m1 = hm k1, m0 = hm k0,
+};                                            // m2 = hm k2, m3 = -hm k3 (StageK)
+__device__ __forceinline__ FusedK make_fused(const VehK& v, const StageK& sk, double h) {
+  FusedK q;
+  q.h = h;
+  q.hm = h * v.inv_mass;
+  q.hIlf = h * v.inv_Iz * v.lf;
+  q.hIlr = h * v.inv_Iz * v.lr;
+  q.m1 = q.hm * sk.k1;
+  q.m0 = q.hm * sk.k0;
+  q.m2 = q.hm * sk.k2;
+  q.m3 = -(q.hm * sk.k3);
+  return q;
+}
+
+template <int LPM>
+__device__ __forceinline__ void k_fused(const StageK& sk, const FusedK& q, double F0, double F1,
+                                        double hmsd, double hmcd, double c5a, double d,
+                                        const double* y, double* k, const fm::FmK& K, Dom& dm) {
+  const double vx = y[3], vy = y[4], om = y[5];
+  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, y[2], K, dm);
+  // h sin(psi), h cos(psi): LPM = 4 lanes 2/3 scale their sine by h already (make_stage)
+  const double hsp = (LPM == 4) ? f.sp : q.h * f.sp, hcp = (LPM == 4) ? f.cp : q.h * f.cp;
+  const double hmFrx = fma(vx, fma(q.m3, vx, F1), F0);                     // hm Frx
+  k[2] = q.h * om;
+  k[0] = fma(vx, hcp, -(vy * hsp));                                       // h (vx cos - vy sin)
+  k[1] = fma(vx, hsp, vy * hcp);
+  k[3] = fma(-f.Ffy, hmsd, fma(vy, k[2], hmFrx));                         // h/m (Frx - Ffy sd) + h vy om
+  k[4] = fma(f.Ffy, hmcd, fma(-vx, k[2], q.hm * f.Fry));                  // h/m (Fry + Ffy cd) - h vx om
+  k[5] = fma(f.Ffy, c5a, -(f.Fry * q.hIlr));                              // h/Iz (Ffy lf cd - Fry lr)
+}
+
+template <int LPM>
+__device__ __forceinline__ void step_fused(const StageK& sk, const FusedK& q, double* x,
+                                           const Input& u, const fm::FmK& K, Dom& dm) {
+  const double F0 = fma(q.m1, u.a, -q.m0), F1 = -(q.m2 * u.a);
+  const double hmsd = q.hm * u.sd, hmcd = q.hm * u.cd, c5a = q.hIlf * u.cd;
+  double y[6], k[6], acc[6];
+  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, x, k, K, dm);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    acc[i] = k[i];
+    y[i] = fma(0.5, k[i], x[i]);
+  }
+  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, y, k, K, dm);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    acc[i] = fma(2.0, k[i], acc[i]);
+    y[i] = fma(0.5, k[i], x[i]);
+  }
+  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, y, k, K, dm);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    acc[i] = fma(2.0, k[i], acc[i]);
+    y[i] = x[i] + k[i];
+  }
+  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, y, k, K, dm);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = fma(acc[i] + k[i], K.sixth, x[i]);
 }
 
 // One look-ahead step on the fast path.

@@ -207,7 +207,7 @@ constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 4 
 // issue slots per use — 2.5x on a Horner chain in the one-wave-per-SIMD regime.
 struct FmK {
   double at[22], sw[11], sq[7], cq[7];
-  double pio2, pio2t, two_pi, cw0, cw1, cw2, sixth, six, rmagic, rmagic2;
+  double pio2, two_pi, cw0, cw1, cw2, sixth, six, rmagic, rmagic2, one;
 
   __device__ __forceinline__ static void pin(double& x) { asm volatile("" : "+v"(x)); }
   __device__ __forceinline__ static FmK load() {
@@ -224,7 +224,6 @@ struct FmK {
       pin(k.cq[i]);
     }
     k.pio2 = kPio2;
-    k.pio2t = kPio2Tail;
     k.two_pi = kTwoOverPi;
     k.cw0 = kPio2Hi;
     k.cw1 = kPio2Mid;
@@ -233,8 +232,9 @@ struct FmK {
     k.six = 6.0;
     k.rmagic = 0x1.8p52;
     k.rmagic2 = 0x1.8p53;
-    pin(k.pio2); pin(k.pio2t); pin(k.two_pi); pin(k.cw0); pin(k.cw1); pin(k.cw2);
-    pin(k.sixth); pin(k.six); pin(k.rmagic); pin(k.rmagic2);
+    k.one = 1.0;
+    pin(k.pio2); pin(k.two_pi); pin(k.cw0); pin(k.cw1); pin(k.cw2);
+    pin(k.sixth); pin(k.six); pin(k.rmagic); pin(k.rmagic2); pin(k.one);
     return k;
   }
 };
@@ -261,6 +261,8 @@ __device__ __forceinline__ double div_fast(double num, double den) {
   double r = __builtin_amdgcn_rcp(den);
   const double e = fma(-den, r, 1.0);
   r = fma(r, e, r);
+  // the residual correction is needed: without it atan2 reaches 18 ulp for divisors just
+  // below powers of two (v_rcp_f64 is least accurate there; tools/diag/ulp_probe.py)
   const double q = num * r;
   return fma(r, fma(-den, q, num), q);
 }
@@ -300,6 +302,42 @@ __device__ __forceinline__ double estrin11(const double* c, double s) {
   return fma(q2, s8, fma(q1, s4, q0));
 }
 
+// IEEE maxNum / minNum as ONE instruction.  fmax/fmin compile to v_max_f64/v_min_f64 plus a
+// canonicalising v_max_f64 x, x of every operand the compiler cannot prove canonical (loop-
+// carried values, fabs results): 5 extra instructions per rollout stage.  The operands here
+// are arithmetic results, never signalling NaNs, so the raw instruction has fmax's meaning
+// (a NaN operand yields the other one).  |a| by the source modifier.
+__device__ __forceinline__ double vmax(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmin(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmax_abs(double a, double b) {   // max(|a|, b)
+  double r;
+  asm("v_max_f64 %0, |%1|, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmin_abs(double a, double b) {   // min(|a|, b)
+  double r;
+  asm("v_min_f64 %0, |%1|, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmax_abs2(double a, double b) {  // max(|a|, |b|)
+  double r;
+  asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmin_abs2(double a, double b) {  // min(|a|, |b|)
+  double r;
+  asm("v_min_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 template <bool EST = false>
 __device__ __forceinline__ double atan_core_k(double t, const FmK& K) {
   const double s = t * t;
@@ -312,14 +350,15 @@ __device__ __host__ __forceinline__ bool atan2_fast_ok(double y, double x) {
   const double s = fabs(y) + x;
   return s >= 0x1p-1000 && s <= 0x1p1000;
 }
-// hi = max(|y|, x), the divisor: hi in [2^-1000, 2^999] lies inside the domain (the
-// rollout checks its running extremes once, dyn.hpp Dom).
+// hi = max(|y|, |x|), the divisor: hi in [2^-1000, 2^999] lies inside the domain (the
+// rollout checks its running extremes once, dyn.hpp Dom).  x enters as |x| (the callers'
+// x is |vx| or the clamped vx >= vmin, so passing vx itself saves materialising |vx|).
 template <bool EST = false>
 __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K, double& hi) {
   const double ay = fabs(y);
-  hi = fmax(ay, x);
-  const double r = atan_core_k<EST>(div_fast(fmin(ay, x), hi), K);
-  const double o = (ay > x) ? (K.pio2 - r) + K.pio2t : r;
+  hi = vmax_abs2(y, x);
+  const double r = atan_core_k<EST>(div_fast(vmin_abs2(y, x), hi), K);
+  const double o = (ay > fabs(x)) ? K.pio2 - r : r;   // no pi/2 tail: <= 2 ulp (measured)
   return copysign(o, y);
 }
 __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K) {
@@ -334,9 +373,9 @@ __device__ __host__ __forceinline__ bool atan_fast_ok(double z) { return fabs(z)
 template <bool EST = false>
 __device__ __forceinline__ double atan_fast(double z, const FmK& K, double& hz) {
   const double az = fabs(z);
-  hz = fmax(az, 1.0);
-  const double r = atan_core_k<EST>(div_fast(fmin(az, 1.0), hz), K);
-  const double o = (az > 1.0) ? (K.pio2 - r) + K.pio2t : r;
+  hz = vmax_abs(z, K.one);
+  const double r = atan_core_k<EST>(div_fast(vmin_abs(z, K.one), hz), K);
+  const double o = (az > 1.0) ? K.pio2 - r : r;   // no pi/2 tail: <= 2 ulp (measured)
   return copysign(o, z);
 }
 __device__ __forceinline__ double atan_fast(double z, const FmK& K) {

@@ -275,6 +275,7 @@ __device__ __forceinline__ double window_mean(const double* ring, int64_t ld, in
 // G17): [0,64) sv[2][4] double | [64,128) si[2][4] int64 | [128,144) sn[4] int32 |
 // pad to 160 | role-specific region from 160.
 constexpr int kScratchBytes = 160;
+constexpr int kStageW = 6;              // doubles per staged (step, candidate) input
 constexpr int kWaves = kBlock / 64;     // look-back lists per block (one per wave)
 constexpr int kListsPerLane = 8;        // lb_final: lists per lane of the merging wave
 
@@ -438,6 +439,19 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
   LB_STAMP(blk, 3);
 }
 
+// Input-rate term du' R du of one step (nmpc.py:65-68, 111) and the bounds / rate
+// feasibility of one input (nmpc.py:102-105; branch-free: |d| <= dmax is false for NaN like
+// the two one-sided tests; dmax < 0 disables).
+__device__ __forceinline__ double act_term(const CostK& q, double d0, double d1) {
+  return d0 * (q.R[0] * d0 + q.R[1] * d1) + d1 * (q.R[2] * d0 + q.R[3] * d1);
+}
+__device__ __forceinline__ bool input_feasible(const CostK& q, double ua, double ud, double d0,
+                                               double d1) {
+  return (int)(ua <= q.umax[0]) & (int)(ua >= q.umin[0]) & (int)(ud <= q.umax[1]) &
+         (int)(ud >= q.umin[1]) & ((int)(q.dmax[0] < 0) | (int)(fabs(d0) <= q.dmax[0])) &
+         ((int)(q.dmax[1] < 0) | (int)(fabs(d1) <= q.dmax[1]));
+}
+
 // One (model, candidate) rollout over H steps and its NLP objective (nmpc.py:44-111).
 // FAST: the branch-free stage (dyn.hpp step_fast); `bad` |= any operand of this lane outside
 // the fast cores' domains.  !FAST: the general evaluation (rk4_step / euler / rk6 with the
@@ -448,7 +462,7 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
                                           const double* sx, const double* su, const VehK& veh,
                                           const Tire& t, const StageK& sk, const CostK& q,
                                           double Ts, double up0, double up1, const fm::FmK& K,
-                                          bool& bad) {
+                                          const FusedK& fq, bool& bad) {
   const int H = a.H, C = a.C;
   double x[6];
 #pragma unroll
@@ -456,6 +470,7 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   double track = 0.0, act = 0.0;
   double p0 = up0, p1 = up1;
   bool feas = true;
+  double feas_s = 1.0;
   double xr0 = 0.0, xr1 = 0.0;
   const double* xpm = XM ? a.xref_pm + n * 2 * H : nullptr;   // this model's reference
   Dom dm;                               // FAST: the operands' running extremes
@@ -464,13 +479,15 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     double ua, ud;
     Input u;
     if (STAGE) {                        // sincos(delta) staged with the fast/general rule
-      const double* o = su + 4 * (k * C + c);
+      const double* o = su + kStageW * (k * C + c);
       ua = o[0];
       ud = o[1];
       u.a = ua;
       u.d = ud;
       u.sd = o[2];
       u.cd = o[3];
+      act = act + o[4];                 // the candidate's input-rate term and feasibility,
+      feas_s = feas_s * o[5];           // formed once per block (lookahead_block)
     } else {
       ua = a.U[2 * ((int64_t)c * H + k)];
       ud = a.U[2 * ((int64_t)c * H + k) + 1];
@@ -478,14 +495,9 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
       else u = make_input(ua, ud);
     }
     const double d0 = ua - p0, d1 = ud - p1;          // nmpc.py:65-68
-    if (q.enforce) {                                  // nmpc.py:102-105 (branch-free:
-      // |d| <= dmax is false for NaN like the two one-sided tests; dmax < 0 disables)
-      feas = (int)feas & (int)(ua <= q.umax[0]) & (int)(ua >= q.umin[0]) &
-             (int)(ud <= q.umax[1]) & (int)(ud >= q.umin[1]) &
-             ((int)(q.dmax[0] < 0) | (int)(fabs(d0) <= q.dmax[0])) &
-             ((int)(q.dmax[1] < 0) | (int)(fabs(d1) <= q.dmax[1]));
-    }
-    if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, dm);
+    if (!STAGE && q.enforce) feas = (int)feas & (int)input_feasible(q, ua, ud, d0, d1);
+    if (FAST && INTEG == 0) step_fused<LPM>(sk, fq, x, u, K, dm);
+    else if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, dm);
     else step<INTEG>(veh, t, x, u, Ts);
     if (XM) {
       xr0 = xpm[2 * k];
@@ -496,7 +508,7 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     }
     const double e0 = x[0] - xr0, e1 = x[1] - xr1;
     track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
-    act = act + (d0 * (q.R[0] * d0 + q.R[1] * d1) + d1 * (q.R[2] * d0 + q.R[3] * d1));
+    if (!STAGE) act = act + act_term(q, d0, d1);
     p0 = ua;
     p1 = ud;
   }
@@ -507,6 +519,7 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   // the later stages' positions, the last stage's feeds vx, vy, omega only through a NaN
   // state that the position update already carries), so a non-finite J is re-run too
   if (FAST) bad = (int)bad | (int)!sk.sok | (int)!dm.ok() | (int)!(fabs(J) <= __DBL_MAX__);
+  if (STAGE) feas = feas_s != 0.0;
   if (!feas) J = __builtin_inf();
   return J;
 }
@@ -515,7 +528,8 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
 // Look-ahead body.  Lane layout inside a block: sub = lane % LPM (LPM = 2: the lane pair
 // of one rollout, front/rear chain), cl = lane / LPM; G candidate-lanes per model (power of two); a model's
 // candidates c = g + j*G, j < cpl, run sequentially in its G*LPM lanes.
-//   LDS from kScratchBytes: xref as [k][2]; U as [k][c][4] (pwm, delta, sin, cos) when staged.
+//   LDS from kScratchBytes: xref as [k][2]; U as [k][c][kStageW] (pwm, delta, sin, cos,
+//   input-rate cost term, feasibility) when staged.
 // ------------------------------------------------------------------------------------
 template <int INTEG, bool STAGE, int LPM, int XM>
 __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int blk, int G, int cpl,
@@ -526,7 +540,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   const int H = a.H, C = a.C;
   // XM = 1 (per-model raceline reference): knots [n] and the x/y spline rows [2][4][n-1]
   // after the (optional) U staging; a.xref holds the shared start {s0, v0, scale}
-  double* rl_knots = su + (STAGE ? 4 * C * H : 0);
+  double* rl_knots = su + (STAGE ? kStageW * C * H : 0);
   double* rl_xy = rl_knots + a.rl.n;
   if (XM) {
     const int nk = a.rl.n, nxy = 8 * (a.rl.n - 1);
@@ -561,11 +575,16 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       double sd, cd;
       if (fm::sincos_fast_ok(dl)) fm::sincos_fast(dl, &sd, &cd, K);
       else LL_SINCOS(dl, &sd, &cd);
-      double* o = su + 4 * (k * C + c);
-      o[0] = a.U[2 * e];
+      double* o = su + kStageW * (k * C + c);
+      const double ua = a.U[2 * e];
+      const double p0 = k ? a.U[2 * e - 2] : a.uprev[0], p1 = k ? a.U[2 * e - 1] : a.uprev[1];
+      const double d0 = ua - p0, d1 = dl - p1;
+      o[0] = ua;
       o[1] = dl;
       o[2] = sd;
       o[3] = cd;
+      o[4] = act_term(a.cost, d0, d1);
+      o[5] = (!a.cost.enforce || input_feasible(a.cost, ua, dl, d0, d1)) ? 1.0 : 0.0;
     }
   }
   __syncthreads();
@@ -607,13 +626,14 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   if (live) {
     const Tire t = load_tire(a.params, a.n, n);
     // LPM = 2: lane 0 of the pair evaluates the front chain, lane 1 the rear (dyn.hpp)
-    const StageK sk = make_stage<LPM>(veh, t, sub);
+    const StageK sk = make_stage<LPM>(veh, t, sub, INTEG == 0 ? Ts : 1.0);
+    const FusedK fq = make_fused(veh, sk, Ts);
     const fm::FmK K = fm::FmK::load();
     for (int j = 0; j < cpl; ++j) {
       const int c = g + j * G;
       if (c >= C) break;
       bool bad = false;
-      double J = rollout<INTEG, STAGE, LPM, XM, true>(a, c, n, sx, su, veh, t, sk, q, Ts, up0, up1, K, bad);
+      double J = rollout<INTEG, STAGE, LPM, XM, true>(a, c, n, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, bad);
       if (LPM == 2) {                   // the pair shares one rollout: re-run both or neither
         const int bi = bad;
         bad = __builtin_amdgcn_mov_dpp(bi, kPair0, 0xF, 0xF, false) |
@@ -626,7 +646,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       }
       if (__builtin_expect(__any(bad), 0)) {
         bool unused = false;
-        if (bad) J = rollout<INTEG, STAGE, LPM, XM, false>(a, c, n, sx, su, veh, t, sk, q, Ts, up0, up1, K, unused);
+        if (bad) J = rollout<INTEG, STAGE, LPM, XM, false>(a, c, n, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, unused);
       }
       if (sub == 0) {
         if (a.cost_out) a.cost_out[n * C + c] = J;
@@ -1191,13 +1211,16 @@ int lookahead_blocks(int64_t n, int32_t C, int lpm) {
   return (int)((n + mpb - 1) / mpb);
 }
 
-constexpr size_t kStageLimit = 48 * 1024;
+// Staged inputs per (step, candidate): pwm, delta, sin delta, cos delta, the input-rate
+// cost term and the feasibility (1/0) — kStageW doubles.  One block per CU (the launch's LDS
+// request), so the staging may use most of the CU's 160 KiB.
+constexpr size_t kStageLimit = 128 * 1024;
 
 size_t raceline_lds_bytes(int32_t n) { return 8 * (size_t)n + 64 * (size_t)(n - 1); }
 
 size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u) {
   const size_t base = kScratchBytes + 16 * (size_t)(H + 1);
-  const size_t ub = 32 * (size_t)C * H;           // (pwm, delta, sin delta, cos delta)
+  const size_t ub = 8 * kStageW * (size_t)C * H;
   *stage_u = base + ub <= kStageLimit;
   return *stage_u ? base + ub : base;
 }
