@@ -33,7 +33,7 @@ for _p in (REPO, os.path.join(REPO, "lla-mpc_amd")):
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector spec
-TIMING_STRIDE = 8               # HIP-event sampling of the plan kernel inside the timed loop
+TIMING_STRIDE = 8               # HIP-event pairs bracket groups of 8 consecutive plan launches
 FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation (excl. transcendentals)
 
 
@@ -198,8 +198,8 @@ def main():
     for i in range(args.warmup):
         step(i)
     if not args.no_timing:
-        # events bracket every TIMING_STRIDE-th launch of the timed loop: the kernel's
-        # duration measured live without the events' own ~5 us/launch in the wall clock
+        # event pairs bracket groups of TIMING_STRIDE consecutive launches of the timed loop:
+        # the kernel's mean duration measured live, the events' own cost spread over a group
         nat.check(lib.llampc_bank_timing(sb.bank.handle, TIMING_STRIDE, args.steps // TIMING_STRIDE + 8))
     torch.cuda.synchronize()
     if world > 1:

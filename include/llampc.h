@@ -159,10 +159,10 @@ int llampc_bank_window(llampc_bank* bank, double* ring, int32_t* window_count);
 int llampc_bank_set_stream(llampc_bank* bank, void* stream);
 
 /* Per-kernel HIP-event timing of the bank's launches, on the stream they run on (for the
- * benchmark's roofline).  enable=k >= 1 arms `max_launches` event pairs and brackets
- * every k-th launch of the plan kernel (the whole tick: look-back + look-ahead +
- * selection) with hipEventRecord (k > 1 keeps the events' own cost out of a timed loop);
- * enable=0 disarms. */
+ * benchmark's roofline).  enable=k >= 1 arms `max_launches` event pairs; each pair brackets
+ * a group of k consecutive launches of the plan kernel (the whole tick: look-back +
+ * look-ahead + selection), so the mean launch duration is elapsed / k (k > 1 spreads the
+ * events' own cost over the group); enable=0 disarms.  count = launches timed. */
 int llampc_bank_timing(llampc_bank* bank, int32_t enable, int32_t max_launches);
 /* Synchronises, returns avg_ms[3] and count[3] for {plan kernel, reserved, reserved}
  * since the last read, and re-arms the counters. */

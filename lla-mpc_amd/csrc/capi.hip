@@ -209,7 +209,10 @@ int check_plan_in(const llampc_bank* b, const llampc_plan_in* in) {
   return LLAMPC_OK;
 }
 
-// Event bracket around one launch of kernel `k` (0 the plan kernel; 1, 2 reserved).
+// Event pair around a GROUP of timing_stride consecutive launches of kernel `k` (0 the plan
+// kernel; 1, 2 reserved): start before the group's first launch, stop after its last, so a
+// launch's mean duration is elapsed / group — the events' own cost (~2 us per record on
+// this stack) is spread over the group instead of inflating every bracketed launch.
 struct TimedLaunch {
   llampc_bank* b;
   int k;
@@ -217,13 +220,16 @@ struct TimedLaunch {
   hipEvent_t stop = nullptr;
   TimedLaunch(llampc_bank* b_, int k_, hipStream_t s_) : b(b_), k(k_), s(s_) {
     if (!b->timing || 2 * (b->ev_used[k] + 1) > b->ev[k].size()) return;
-    if (b->timing_seen[k]++ % b->timing_stride) return;
-    const size_t i = b->ev_used[k]++;
-    (void)hipEventRecord(b->ev[k][2 * i], s);
-    stop = b->ev[k][2 * i + 1];
+    const int64_t pos = b->timing_seen[k]++ % b->timing_stride;
+    const size_t i = b->ev_used[k];
+    if (pos == 0) (void)hipEventRecord(b->ev[k][2 * i], s);
+    if (pos == b->timing_stride - 1) stop = b->ev[k][2 * i + 1];
   }
   ~TimedLaunch() {
-    if (stop) (void)hipEventRecord(stop, s);
+    if (stop) {
+      (void)hipEventRecord(stop, s);
+      b->ev_used[k]++;
+    }
   }
 };
 
@@ -560,9 +566,10 @@ int llampc_bank_timing_read(llampc_bank* b, double* avg_ms, int64_t* count) {
       HIP_TRY(hipEventElapsedTime(&ms, b->ev[k][2 * i], b->ev[k][2 * i + 1]));
       tot += ms;
     }
-    count[k] = (int64_t)b->ev_used[k];
-    avg_ms[k] = b->ev_used[k] ? tot / b->ev_used[k] : 0.0;
+    count[k] = (int64_t)b->ev_used[k] * b->timing_stride;
+    avg_ms[k] = b->ev_used[k] ? tot / ((double)b->ev_used[k] * b->timing_stride) : 0.0;
     b->ev_used[k] = 0;
+    b->timing_seen[k] = 0;
   }
   return LLAMPC_OK;
 }

@@ -260,10 +260,11 @@ struct ChainEst {
 // One tire's constants in this lane: front (lw = lf, sg = +1) or rear (lw = lr, sg = -1).
 struct Chain {
   double lw, sg, B, C, D;
+  double nsB;   // -sg B (chain_fold: z = fma(nsB, atan2, B dsel))
 };
 
 __device__ __host__ __forceinline__ Chain make_chain(const VehK& v, const Tire& t, bool front) {
-  return front ? Chain{v.lf, 1.0, t.Bf, t.Cf, t.Df} : Chain{v.lr, -1.0, t.Br, t.Cr, t.Dr};
+  return front ? Chain{v.lf, 1.0, t.Bf, t.Cf, t.Df, -t.Bf} : Chain{v.lr, -1.0, t.Br, t.Cr, t.Dr, t.Br};
 }
 
 // Static part of the fast chain's domain: |C atan(.)| <= |C| pi/2 must stay inside
@@ -320,7 +321,7 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
 // clears the sign), pm = 0 / 1 / -1 and po = 0 / 0 / pi/2 place the angle argument
 // po + pm r' (exactly 0 in lanes 0/1, so their argument is C atan(.) as at LPM 1/2).
 __device__ __forceinline__ double chain_fold(const Chain& c, double den, double vy, double om,
-                                             double dsel, double psi, int ra, double pm,
+                                             double Bd, double psi, int ra, double pm,
                                              double po, Dom& dm, const fm::FmK& K) {
   constexpr bool EST = ChainEst<4>::value;
   const double t2 = fma(psi, K.two_pi, K.rmagic2);       // 2^53 (1.5 + 2k 2^-53): ulp 2
@@ -342,7 +343,7 @@ __device__ __forceinline__ double chain_fold(const Chain& c, double den, double 
     const double yy = fma(c.lw, om, c.sg * vy);
     double h2, hz;
     const double a2 = fm::atan2_fast<EST>(yy, den, K, h2);
-    const double z = c.B * fma(-c.sg, a2, dsel);
+    const double z = fma(c.nsB, a2, Bd);                  // B (dsel - sg a2)
     at = fm::atan_fast<EST>(z, K, hz);
     dm.lo = fm::vmin(dm.lo, h2);
     dm.hi = fm::vmax(dm.hi, fm::vmax(h2, hz));
@@ -385,6 +386,8 @@ __device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int s
   if (LPM == 4 && sub >= 2) {   // lanes 2/3: the chain's sine takes the psi argument alone
     s.ch[0].C = 0.0;
     s.ch[0].D = psi_scale;
+    // (their atan2 / atan duplicate lanes 0/1's chains; constant operands there instead
+    // — yy = z = 0 — clocked 1.5 % higher but took 4.5 % more cycles)
   }
   return s;
 }
@@ -393,13 +396,15 @@ __device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int s
 struct StageF {
   double Ffy, Fry, sp, cp;
 };
+// Bd = B d fw, the chain's steering term (LPM = 4 only; formed once per step).
 template <int LPM>
 __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, double vy, double om,
-                                              double d, double psi, const fm::FmK& K, Dom& dm) {
+                                              double d, double psi, const fm::FmK& K, Dom& dm,
+                                              double Bd = 0.0) {
   StageF f;
   dm.ps = fm::vmax_abs(psi, dm.ps);
   if (LPM == 4) {
-    const double r = chain_fold(sk.ch[0], den, vy, om, d * sk.fw, psi, sk.ra, sk.pm, sk.po, dm, K);
+    const double r = chain_fold(sk.ch[0], den, vy, om, Bd, psi, sk.ra, sk.pm, sk.po, dm, K);
     f.Ffy = dpp_bcast<kQuad0>(r);
     f.Fry = dpp_bcast<kQuad1>(r);
     f.sp = dpp_bcast<kQuad2>(r);
@@ -436,7 +441,7 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const 
     vx = 0.05;
   }
   // den = vx: the fast atan2 takes |den| (Ref: atan2(., |vx|); Nlp: vx >= vmin after the clamp)
-  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, x[2], K, dm);
+  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, x[2], K, dm, sk.ch[0].B * (d * sk.fw));
   const double Frx = (sk.k1 - sk.k2 * vx) * u.a - sk.k0 - sk.k3 * (vx * vx);
   dx[0] = vx * f.cp - vy * f.sp;
   dx[1] = vx * f.sp + vy * f.cp;
@@ -481,10 +486,10 @@ __device__ __forceinline__ FusedK make_fused(const VehK& v, const StageK& sk, do
 
 template <int LPM>
 __device__ __forceinline__ void k_fused(const StageK& sk, const FusedK& q, double F0, double F1,
-                                        double hmsd, double hmcd, double c5a, double d,
+                                        double hmsd, double hmcd, double c5a, double d, double Bd,
                                         const double* y, double* k, const fm::FmK& K, Dom& dm) {
   const double vx = y[3], vy = y[4], om = y[5];
-  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, y[2], K, dm);
+  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, y[2], K, dm, Bd);
   // h sin(psi), h cos(psi): LPM = 4 lanes 2/3 scale their sine by h already (make_stage)
   const double hsp = (LPM == 4) ? f.sp : q.h * f.sp, hcp = (LPM == 4) ? f.cp : q.h * f.cp;
   const double hmFrx = fma(vx, fma(q.m3, vx, F1), F0);                     // hm Frx
@@ -501,26 +506,27 @@ __device__ __forceinline__ void step_fused(const StageK& sk, const FusedK& q, do
                                            const Input& u, const fm::FmK& K, Dom& dm) {
   const double F0 = fma(q.m1, u.a, -q.m0), F1 = -(q.m2 * u.a);
   const double hmsd = q.hm * u.sd, hmcd = q.hm * u.cd, c5a = q.hIlf * u.cd;
+  const double Bd = (LPM == 4) ? sk.ch[0].B * (u.d * sk.fw) : 0.0;
   double y[6], k[6], acc[6];
-  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, x, k, K, dm);
+  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, x, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     acc[i] = k[i];
     y[i] = fma(0.5, k[i], x[i]);
   }
-  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, y, k, K, dm);
+  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     acc[i] = fma(2.0, k[i], acc[i]);
     y[i] = fma(0.5, k[i], x[i]);
   }
-  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, y, k, K, dm);
+  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     acc[i] = fma(2.0, k[i], acc[i]);
     y[i] = x[i] + k[i];
   }
-  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, y, k, K, dm);
+  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) x[i] = fma(acc[i] + k[i], K.sixth, x[i]);
 }

@@ -341,6 +341,37 @@ __device__ __forceinline__ double sq_err4(const double* x, const double* xn) {
   return s;
 }
 
+// The sorted top-K of one wave's 64 window means (R == 1) by rank: every lane counts the
+// lanes whose (value, index) key precedes its own — NaN last, ties to the lower index
+// (rt.py:360 argsort order) — and the lanes ranked below K store their entry at that rank.
+// Keys as order-preserving u64 (+0 for -0, one canonical NaN above +inf); lanes without a
+// model take a key above every model's (kNoIndex entries at the end of a short list).
+__device__ __forceinline__ void wave_topk_rank(const LookbackLaunch& a, int64_t list, double w,
+                                               int64_t n, unsigned char* lds) {
+  const int lane = threadIdx.x & 63;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(lds + (threadIdx.x >> 6) * 768);
+  uint32_t* ids = reinterpret_cast<uint32_t*>(keys + 64);
+  const bool valid = n < a.n;
+  const double wc = (w != w) ? __builtin_nan("") : w + 0.0;
+  const uint64_t b = (uint64_t)__double_as_longlong(wc);
+  const uint64_t key = !valid ? ~0ull : ((b >> 63) ? ~b : (b | 0x8000000000000000ull));
+  const uint32_t id = valid ? (uint32_t)n : 0xFFFFFF00u + (uint32_t)lane;
+  keys[lane] = key;
+  ids[lane] = id;
+  __syncthreads();
+  int rank = 0;
+#pragma unroll 16
+  for (int j = 0; j < 64; ++j) {
+    const uint64_t kj = keys[j];
+    const uint32_t ij = ids[j];
+    rank += (int)(kj < key) | ((int)(kj == key) & (int)(ij < id));
+  }
+  if (rank < a.K) {
+    st_wt(&a.tk_val[list * a.K + rank], valid ? w : __builtin_nan(""));
+    st_wt(&a.tk_idx[list * a.K + rank], valid ? a.goff + n : kNoIndex);
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Look-back body: one block = 256*R models (R models per lane, coalesced in r).
 // RK4 step from (x_{t-1}, u_{t-1}), 4-state MSE against x_t, in-place ring write, window
@@ -413,7 +444,12 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     st_wt(&a.am_idx[list], li == kNoLocal ? kNoIndex : a.goff + li);
   }
   LB_STAMP(blk, 2);
-  // K rounds of "next key after the previous pick" (NaN last, ties -> lower index)
+  if (a.R == 1) {                       // launch-uniform
+    wave_topk_rank(a, list, wm0, base + threadIdx.x, reinterpret_cast<unsigned char*>(sc.sv) + kScratchBytes);
+    LB_STAMP(blk, 3);
+    return;
+  }
+  // R > 1: K rounds of "next key after the previous pick" (NaN last, ties -> lower index)
   double lv = 0.0;
   uint32_t ll = kNoLocal;
   for (int k = 0; k < a.K; ++k) {
@@ -459,14 +495,14 @@ __device__ __forceinline__ bool input_feasible(const CostK& q, double ua, double
 // own operands only.  Returns J (+inf when infeasible).
 template <int INTEG, bool STAGE, int LPM, int XM, bool FAST>
 __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64_t n,
-                                          const double* sx, const double* su, const VehK& veh,
+                                          const double* x0, const double* sx, const double* su, const VehK& veh,
                                           const Tire& t, const StageK& sk, const CostK& q,
                                           double Ts, double up0, double up1, const fm::FmK& K,
                                           const FusedK& fq, bool& bad) {
   const int H = a.H, C = a.C;
   double x[6];
 #pragma unroll
-  for (int m = 0; m < 6; ++m) x[m] = a.x0[m];
+  for (int m = 0; m < 6; ++m) x[m] = x0[m];
   double track = 0.0, act = 0.0;
   double p0 = up0, p1 = up1;
   bool feas = true;
@@ -538,6 +574,18 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);
   double* su = sx + 2 * (a.H + 1);
   const int H = a.H, C = a.C;
+  // this lane's model: its Pacejka row and the start state are loaded first, so they are in
+  // flight while the block stages the shared inputs (one HBM round trip, not two)
+  const int sub = threadIdx.x % LPM;
+  const int cl = threadIdx.x / LPM;
+  const int g = cl & (G - 1);
+  const int64_t n = (int64_t)blk * (kBlock / (G * LPM)) + cl / G;
+  const bool live = n < a.n;
+  Tire t{};
+  if (live) t = load_tire(a.params, a.n, n);
+  double x0[6];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) x0[m] = a.x0[m];
   // XM = 1 (per-model raceline reference): knots [n] and the x/y spline rows [2][4][n-1]
   // after the (optional) U staging; a.xref holds the shared start {s0, v0, scale}
   double* rl_knots = su + (STAGE ? kStageW * C * H : 0);
@@ -589,11 +637,6 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   }
   __syncthreads();
 
-  const int sub = threadIdx.x % LPM;
-  const int cl = threadIdx.x / LPM;
-  const int g = cl & (G - 1);
-  const int64_t n = (int64_t)blk * (kBlock / (G * LPM)) + cl / G;
-  const bool live = n < a.n;
   CostK q = a.cost;
   VehK veh = a.veh;
   double Ts = a.Ts;
@@ -624,7 +667,6 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   int nf = 0;
   LA_STAMP(blk, 1);
   if (live) {
-    const Tire t = load_tire(a.params, a.n, n);
     // LPM = 2: lane 0 of the pair evaluates the front chain, lane 1 the rear (dyn.hpp)
     const StageK sk = make_stage<LPM>(veh, t, sub, INTEG == 0 ? Ts : 1.0);
     const FusedK fq = make_fused(veh, sk, Ts);
@@ -633,7 +675,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       const int c = g + j * G;
       if (c >= C) break;
       bool bad = false;
-      double J = rollout<INTEG, STAGE, LPM, XM, true>(a, c, n, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, bad);
+      double J = rollout<INTEG, STAGE, LPM, XM, true>(a, c, n, x0, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, bad);
       if (LPM == 2) {                   // the pair shares one rollout: re-run both or neither
         const int bi = bad;
         bad = __builtin_amdgcn_mov_dpp(bi, kPair0, 0xF, 0xF, false) |
@@ -646,7 +688,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       }
       if (__builtin_expect(__any(bad), 0)) {
         bool unused = false;
-        if (bad) J = rollout<INTEG, STAGE, LPM, XM, false>(a, c, n, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, unused);
+        if (bad) J = rollout<INTEG, STAGE, LPM, XM, false>(a, c, n, x0, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, unused);
       }
       if (sub == 0) {
         if (a.cost_out) a.cost_out[n * C + c] = J;
@@ -782,7 +824,9 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
   const int L = f.nb_lb * kWaves;          // one sorted K-list + argmin per look-back wave
   const int K = f.K;
   Ent* buf = reinterpret_cast<Ent*>(smem + kScratchBytes);
+  Ent* am = buf + L * K;                   // the lists' argmins, loaded in the same round trip
   for (int e = tid; e < L * K; e += kBlock) buf[e] = Ent{ld_wt(&f.tk_val[e]), ld_wt(&f.tk_idx[e])};
+  for (int b = tid; b < L; b += kBlock) am[b] = Ent{ld_wt(&f.am_val[b]), ld_wt(&f.am_idx[b])};
   __syncthreads();
   STAMP(1);
   if (tid >= 64) return;                   // one wave merges; the caller re-converges
@@ -792,8 +836,8 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
   double v = f.nan_first ? __builtin_inf() : __builtin_nan("");
   uint32_t li = kNoLocal;
   for (int b = lane; b < L; b += 64) {
-    const double bv = ld_wt(&f.am_val[b]);
-    const uint32_t bl = local(ld_wt(&f.am_idx[b]));
+    const double bv = am[b].v;
+    const uint32_t bl = local(am[b].i);
     const bool t = (int)(bl != kNoLocal) &
                    (int)(f.nan_first ? less_bf<1>(bv, bl, v, li) : less_bf<0>(bv, bl, v, li));
     v = t ? bv : v;
@@ -1289,7 +1333,7 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
     lbv = *lb;
     lbv.R = lookback_r(lb->n, std::max(1, lb->K));
     f.nb_lb = lookback_blocks_r(lb->n, lbv.R);
-    if (lb->full) lds = std::max(lds, kScratchBytes + (size_t)f.nb_lb * kWaves * lb->K * sizeof(Ent));
+    if (lb->full) lds = std::max(lds, kScratchBytes + (size_t)f.nb_lb * kWaves * (lb->K + 1) * sizeof(Ent));
   }
   if (la) {
     lav = *la;
