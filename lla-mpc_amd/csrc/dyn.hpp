@@ -467,7 +467,7 @@ __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::F
 // arithmetic of rk4_step / dynamic.py:98-115 with other roundings of its products and sums
 // (~1 ulp per step, the transcendental cores' class; tests/test_gpu_parity.py bounds the
 // rollouts at 1e-7 relative).  42 fewer instructions per step than step_fast's reference
-// roundings, which the look-back keeps (its errors are ranked against the oracle's).
+// roundings, which the look-back keeps (its errors are ranked, rt.py:359-360).
 struct FusedK {
   double h, hm, hIlf, hIlr, m1, m0, m2, m3;   // hm = h/m; m1 = hm k1, m0 = hm k0,
 };                                            // m2 = hm k2, m3 = -hm k3 (StageK)
