@@ -46,7 +46,8 @@ enum llampc_status {
   LLAMPC_E_HIP = -2,        /* HIP runtime error                          */
   LLAMPC_E_NODEV = -3,      /* no HIP device                              */
   LLAMPC_E_STATE = -4,      /* call not valid in the handle's state       */
-  LLAMPC_E_OOM = -5         /* device allocation failed                   */
+  LLAMPC_E_OOM = -5,        /* device allocation failed                   */
+  LLAMPC_E_DEVICE = -6      /* the tick's record reports a device-side status != 0 */
 };
 
 /* Integrators.  RK4 = odeintRK4_batch (rk6.py:50-68) on the |vx| dynamics
@@ -113,6 +114,7 @@ typedef struct llampc_plan_in {
 } llampc_plan_in;
 
 /* One tick's result (fixed size: also the cross-GPU payload, see llampc_merge). */
+#define LLAMPC_STATUS_POLL_TIMEOUT 1
 typedef struct llampc_plan_out {
   int32_t window_count;   /* transitions in the window, <= W (rt.py:354)           */
   int32_t window_full;    /* window_count >= W: selection valid (rt.py:357)        */
@@ -126,7 +128,8 @@ typedef struct llampc_plan_out {
   double  sel_cost;
   int64_t la_best_model;  /* argmin over all (model, candidate) costs              */
   int32_t la_best_cand;
-  int32_t reserved;
+  int32_t status;         /* 0 ok; LLAMPC_STATUS_POLL_TIMEOUT (1): the in-launch
+                             completion gave up waiting (a device fault, never expected) */
   double  la_best_cost;
   int64_t topk[LLAMPC_KMAX];      /* argsort(window mean)[:K] (rt.py:360), -1 pad  */
   double  topk_val[LLAMPC_KMAX];

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -141,6 +142,9 @@ struct llampc_bank {
   double* d_xref_pm = nullptr;     // per-model references [n][H][2] (RACELINE ticks)
   size_t xref_pm_cap = 0;
   int64_t timing_seen[3] = {0, 0, 0};
+  uint64_t* d_la_tag = nullptr;    // polled completion: [n][3] tagged per-model results
+  uint64_t* d_blk_tag = nullptr;   // [blocks][5] tagged look-ahead block partials
+  uint32_t seq = 0;                // launch tag (1, 2, ...; never 0 = the zeroed buffers)
 };
 
 namespace {
@@ -333,6 +337,21 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   f.pv = b->d_pv;
   f.pidx = b->d_pidx;
   f.pnf = b->d_pnf;
+  // polled completion whenever look-back blocks exist to host the poller (LLAMPC_NO_POLL=1:
+  // the ticket + last-block path, for A/B runs)
+  const bool no_poll = getenv("LLAMPC_NO_POLL") != nullptr;
+  const int32_t poll = (lb && la && !no_poll) ? 1 : 0;
+  if (poll && ++b->seq == 0) b->seq = 1;
+  f.la_tag = b->d_la_tag;
+  f.blk_tag = b->d_blk_tag;
+  f.seq = b->seq;
+  f.poll = poll;
+  if (la) {
+    lal.la_tag = b->d_la_tag;
+    lal.blk_tag = b->d_blk_tag;
+    lal.seq = b->seq;
+    lal.poll = poll;
+  }
   {
     TimedLaunch tl(b, 0, s);
     HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s));
@@ -440,13 +459,16 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
       (rc = dev_alloc(&b->d_pidx, lab)) || (rc = dev_alloc(&b->d_pnf, lab)) ||
       (rc = dev_alloc(&b->d_best_cand, n)) || (rc = dev_alloc(&b->d_best_cost, n)) ||
       (rc = dev_alloc(&b->d_err, n)) || (rc = dev_alloc(&b->d_wmean, n)) ||
-      (rc = dev_alloc(&b->d_out, 1)) || (rc = dev_alloc(&b->d_tickets, 2)))
+      (rc = dev_alloc(&b->d_out, 1)) || (rc = dev_alloc(&b->d_tickets, 2)) ||
+      (rc = dev_alloc(&b->d_la_tag, 3 * (size_t)n)) || (rc = dev_alloc(&b->d_blk_tag, 5 * (size_t)lab)))
     return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&b->h_out), sizeof(llampc_plan_out), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(out) failed"));
   if (hipMemcpy(b->d_params, params, 6 * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(b->d_ring, 0, (size_t)W * n * sizeof(double)) != hipSuccess ||
       hipMemset(b->d_tickets, 0, 2 * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(b->d_la_tag, 0, 3 * (size_t)n * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(b->d_blk_tag, 0, 5 * (size_t)lab * sizeof(uint64_t)) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "bank upload failed"));
   *out = b;
@@ -461,7 +483,7 @@ int llampc_bank_destroy(llampc_bank* b) {
     void* dptrs[] = {b->d_params, b->d_ring, b->d_am_val, b->d_am_idx, b->d_tk_val, b->d_tk_idx,
                      b->d_pv, b->d_pidx, b->d_pnf, b->d_best_cand, b->d_best_cost, b->d_in,
                      b->d_out, b->d_err, b->d_wmean, b->d_cost, b->d_tickets, b->d_rl,
-                     b->d_xref_pm};
+                     b->d_xref_pm, b->d_la_tag, b->d_blk_tag};
     for (void* p : dptrs)
       if (p) (void)hipFree(p);
     if (b->h_in) (void)hipHostFree(b->h_in);
@@ -599,6 +621,7 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
     HIP_TRY(hipMemcpyAsync(cost_out, d_cost, (size_t)b->n * in->C * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   *out = *b->h_out;
+  if (out->status) return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", out->status);
   return LLAMPC_OK;
 }
 
@@ -656,6 +679,7 @@ int llampc_plan_wait(llampc_bank* b, llampc_plan_out* out) {
   b->async_pending = false;
   HIP_TRY(hipStreamSynchronize(b->stream));
   *out = *b->h_out;
+  if (out->status) return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", out->status);
   return LLAMPC_OK;
 }
 

@@ -212,6 +212,15 @@ __device__ __forceinline__ T ld_wt(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Tagged 64-bit words of the polled completion: launch tag in the high half, payload low.
+__device__ __forceinline__ uint64_t tag_word(uint32_t seq, uint32_t payload) {
+  return ((uint64_t)seq << 32) | payload;
+}
+__device__ __forceinline__ bool tag_ok(uint64_t w, uint32_t seq) { return (uint32_t)(w >> 32) == seq; }
+__device__ __forceinline__ uint64_t join_words(uint64_t hi, uint64_t lo) {
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
 __device__ __forceinline__ int wave_sum(int x) {
   x += dpp_i<kDppXor1>(x);
   x += dpp_i<kDppXor2>(x);
@@ -733,8 +742,16 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     }
   }
   if (live && g == 0 && sub == 0) {
-    st_wt(&a.best_cand[n], (int32_t)bc);
-    st_wt(&a.best_cost[n], bv);
+    if (a.poll) {                       // plain stores (read after the launch) + tagged words
+      a.best_cand[n] = (int32_t)bc;
+      a.best_cost[n] = bv;
+      st_wt(&a.la_tag[3 * n], tag_word(a.seq, (uint32_t)(__double_as_longlong(bv) >> 32)));
+      st_wt(&a.la_tag[3 * n + 1], tag_word(a.seq, (uint32_t)__double_as_longlong(bv)));
+      st_wt(&a.la_tag[3 * n + 2], tag_word(a.seq, (uint32_t)(int32_t)bc));
+    } else {
+      st_wt(&a.best_cand[n], (int32_t)bc);
+      st_wt(&a.best_cost[n], bv);
+    }
   }
   // per-block argmin over (model, candidate) in flattened order (goff+n)*C + c: branch-free
   // wave picks, one LDS exchange of the waves' picks and non-finite counts
@@ -759,9 +776,19 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       key = t ? si[w] : key;
       nfs += sc.sn[w];
     }
-    st_wt(&a.pv[blk], v);
-    st_wt(&a.pidx[blk], key);
-    st_wt(&a.pnf[blk], nfs);
+    if (a.poll) {
+      uint64_t* r = a.blk_tag + 5 * (int64_t)blk;
+      const uint64_t vb = (uint64_t)__double_as_longlong(v), kb = (uint64_t)key;
+      st_wt(&r[0], tag_word(a.seq, (uint32_t)(vb >> 32)));
+      st_wt(&r[1], tag_word(a.seq, (uint32_t)vb));
+      st_wt(&r[2], tag_word(a.seq, (uint32_t)(kb >> 32)));
+      st_wt(&r[3], tag_word(a.seq, (uint32_t)kb));
+      st_wt(&r[4], tag_word(a.seq, (uint32_t)nfs));
+    } else {
+      st_wt(&a.pv[blk], v);
+      st_wt(&a.pidx[blk], key);
+      st_wt(&a.pnf[blk], nfs);
+    }
   }
   LA_STAMP(blk, 3);
 }
@@ -906,6 +933,54 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
   }
 }
 
+// Completes the record from the gathered look-ahead results (final_select / final_poll).
+__device__ __forceinline__ void final_write(const FinalLaunch& f, bool lb, int64_t sel, bool owned,
+                                            int32_t kcand, double kcost, int32_t scand,
+                                            double scost, double lav, int64_t lai, int nf,
+                                            int status = 0) {
+  const int tid = threadIdx.x;
+  llampc_plan_out* o = f.out;
+  if (tid < LLAMPC_KMAX) {
+    const int k = tid;
+    if (!lb) {
+      o->topk[k] = -1;
+      o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = __builtin_nan("");
+    }
+    o->topk_cand[k] = kcand;
+    o->topk_cost[k] = kcost;
+  }
+  if (tid == 0) {
+    if (!lb) {
+      o->lb_best = -1;
+      o->lb_best_val = __builtin_nan("");
+    }
+    o->window_count = f.window_count;
+    o->window_full = f.full;
+    o->K = f.K;
+    o->n_nonfinite = nf;
+    o->status = status;
+    o->sel_model = sel;
+    o->sel_owned = owned;
+    o->sel_cand = scand;
+    o->sel_cost = scost;
+    if (f.do_la && lai != kNoIndex) {
+      o->la_best_model = lai / f.C;
+      o->la_best_cand = (int32_t)(lai % f.C);
+      o->la_best_cost = lav;
+    } else {
+      o->la_best_model = -1;
+      o->la_best_cand = -1;
+      o->la_best_cost = __builtin_nan("");
+    }
+    __hip_atomic_store(&f.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&f.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  STAMP(5);
+#ifdef LLAMPC_STAMPS
+  if (tid == 0) g_stamp_launch++;
+#endif
+}
+
 __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch& sc) {
   STAMP(3);
   const int tid = threadIdx.x;
@@ -961,45 +1036,112 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
     }
   }
   STAMP(4);
-  if (tid < LLAMPC_KMAX) {
-    const int k = tid;
-    if (!lb) {
-      o->topk[k] = -1;
-      o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = __builtin_nan("");
+  final_write(f, lb, sel, owned, kcand, kcost, scand, scost, lav, lai, nf);
+}
+
+// Polled completion (f.poll): run by the look-back ticket winner after lb_final.  Every
+// poll round loads, in ONE round trip, each look-ahead block's tagged partial (5 words) and
+// the tagged per-model result of each top-K model and of the selected model (3 words), and
+// repeats until every word carries this launch's tag.  The blocks it waits for never wait,
+// so it cannot deadlock; a bound of ~0.2 s (s_memrealtime) ends a poll that would never
+// finish (a bug) with status LLAMPC_STATUS_POLL_TIMEOUT in the record instead of a hang.
+constexpr int kPollTimeoutStatus = LLAMPC_STATUS_POLL_TIMEOUT;
+__device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& sc) {
+  STAMP(3);
+  const int tid = threadIdx.x;
+  llampc_plan_out* o = f.out;
+  const bool lb = f.do_lb && f.full;
+  const int64_t idk = (lb && tid < LLAMPC_KMAX) ? ld_wt(&o->topk[tid]) : -1;
+  const int64_t lbi = (tid == 0 && lb) ? ld_wt(&o->lb_best) : -1;
+  const int64_t sel = lbi >= 0 ? lbi : f.current_model;
+  const bool owned = sel >= f.goff && sel < f.goff + f.n;
+  // this thread's model record: top-K entry tid, or (thread 0's second slot) the selection
+  const int64_t mk = (lb && tid < LLAMPC_KMAX && idk >= 0) ? idk - f.goff : -1;
+  const int64_t ms = (tid == 0 && owned) ? sel - f.goff : -1;
+  const int nbt = (f.nb_la + kBlock - 1) / kBlock;        // block records per thread
+  uint64_t kw[3] = {0, 0, 0}, sw[3] = {0, 0, 0};
+  double lav = __builtin_nan("");
+  int64_t lai = kNoIndex;
+  int nf = 0;
+  int status = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  int* done = reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(sc.sv) + 152);  // scratch pad
+  for (;;) {
+    bool ok = true;
+    if (mk >= 0) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) kw[w] = ld_wt(&f.la_tag[3 * mk + w]);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) ok = (int)ok & (int)tag_ok(kw[w], f.seq);
     }
-    o->topk_cand[k] = kcand;
-    o->topk_cost[k] = kcost;
+    if (ms >= 0) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) sw[w] = ld_wt(&f.la_tag[3 * ms + w]);
+#pragma unroll
+      for (int w = 0; w < 3; ++w) ok = (int)ok & (int)tag_ok(sw[w], f.seq);
+    }
+    lav = __builtin_nan("");
+    lai = kNoIndex;
+    nf = 0;
+    for (int j = 0; j < nbt; ++j) {
+      const int b = tid + j * kBlock;
+      if (b < f.nb_la) {
+        uint64_t r[5];
+#pragma unroll
+        for (int w = 0; w < 5; ++w) r[w] = ld_wt(&f.blk_tag[5 * (int64_t)b + w]);
+#pragma unroll
+        for (int w = 0; w < 5; ++w) ok = (int)ok & (int)tag_ok(r[w], f.seq);
+        const double pv = __longlong_as_double((long long)join_words(r[0], r[1]));
+        const int64_t pi = (int64_t)join_words(r[2], r[3]);
+        nf += (int)(uint32_t)r[4];
+        const bool t = (int)(pi != kNoIndex) & (int)less_bf<0>(pv, pi, lav, lai);
+        lav = t ? pv : lav;
+        lai = t ? pi : lai;
+      }
+    }
+    if (tid == 0) *done = 0;
+    __syncthreads();
+    if (!ok) *done = 1;                 // any thread not ready -> another round
+    if (tid == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) *done = 2;
+    __syncthreads();
+    const int d = *done;
+    __syncthreads();
+    if (d == 0) break;
+    if (d == 2) {
+      status = kPollTimeoutStatus;
+      break;
+    }
   }
-  if (tid == 0) {
-    if (!lb) {
-      o->lb_best = -1;
-      o->lb_best_val = __builtin_nan("");
-    }
-    o->window_count = f.window_count;
-    o->window_full = f.full;
-    o->K = f.K;
-    o->n_nonfinite = nf;
-    o->reserved = 0;
-    o->sel_model = sel;
-    o->sel_owned = owned;
-    o->sel_cand = scand;
-    o->sel_cost = scost;
-    if (f.do_la && lai != kNoIndex) {
-      o->la_best_model = lai / f.C;
-      o->la_best_cand = (int32_t)(lai % f.C);
-      o->la_best_cost = lav;
-    } else {
-      o->la_best_model = -1;
-      o->la_best_cand = -1;
-      o->la_best_cost = __builtin_nan("");
-    }
-    __hip_atomic_store(&f.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&f.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int32_t kcand = -1, scand = -1;
+  double kcost = __builtin_nan(""), scost = __builtin_nan("");
+  if (mk >= 0 && f.do_la) {
+    kcost = __longlong_as_double((long long)join_words(kw[0], kw[1]));
+    kcand = (int32_t)(uint32_t)kw[2];
   }
-  STAMP(5);
-#ifdef LLAMPC_STAMPS
-  if (tid == 0) g_stamp_launch++;
-#endif
+  if (ms >= 0 && f.do_la) {
+    scost = __longlong_as_double((long long)join_words(sw[0], sw[1]));
+    scand = (int32_t)(uint32_t)sw[2];
+  }
+  wave_pick_nl64(lav, lai);
+  nf = wave_sum(nf);
+  if ((tid & 63) == 0) {
+    sc.sv[4 + (tid >> 6)] = lav;
+    sc.si[4 + (tid >> 6)] = lai;
+    sc.sn[tid >> 6] = nf;
+  }
+  __syncthreads();
+  lav = sc.sv[4];
+  lai = sc.si[4];
+  nf = sc.sn[0];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) {
+    const bool t = (int)(sc.si[4 + w] != kNoIndex) & (int)less_bf<0>(sc.sv[4 + w], sc.si[4 + w], lav, lai);
+    lav = t ? sc.sv[4 + w] : lav;
+    lai = t ? sc.si[4 + w] : lai;
+    nf += sc.sn[w];
+  }
+  STAMP(4);
+  final_write(f, lb, sel, owned, kcand, kcost, scand, scost, lav, lai, nf, status);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1019,8 +1161,14 @@ __global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, Lookahe
     lookback_block(lb, blockIdx.x, sc);
     if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
     if (fin.full) lb_final(fin, smem);
+    if (fin.poll) {                      // the look-back winner completes the tick
+      __syncthreads();
+      final_poll(fin, sc);
+      return;
+    }
   } else {
     lookahead_block<INTEG, STAGE, LPM, XM>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
+    if (fin.poll) return;                // published tagged records; no ticket
   }
   const unsigned expected = (unsigned)fin.nb_la + (fin.nb_lb > 0 ? 1u : 0u);
   if (!ticket_last(&fin.tickets[1], expected, flag)) return;
@@ -1118,7 +1266,9 @@ __global__ __launch_bounds__(64) void merge_kernel(const llampc_plan_out* parts,
   m->window_count = p0.window_count;
   m->window_full = p0.window_full;
   m->K = K;
-  m->reserved = 0;
+  int32_t st = 0;
+  for (int g = 0; g < G; ++g) st |= parts[g].status;
+  m->status = st;
   m->lb_best = bi == kNoIndex ? -1 : bi;
   m->lb_best_val = bi == kNoIndex ? __builtin_nan("") : bv;
   if (m->window_full && owner_lb >= 0) {

@@ -48,6 +48,12 @@ struct LookaheadLaunch {
   int32_t xref_mode;                     // LLAMPC_XREF_*; RACELINE: xref = {s0, v0, scale}
   RacelineK rl;
   double* xref_pm;                       // RACELINE: per-model reference [n][H][2]
+  // polled completion (FinalLaunch::poll): tagged records, each 64-bit word = seq << 32 |
+  // 32 payload bits, so a reader validates every word it loads on its own
+  uint64_t* la_tag;                      // [n][3]: best cost hi, lo, best candidate
+  uint64_t* blk_tag;                     // [blocks][5]: partial value hi, lo, key hi, lo, nf
+  uint32_t seq;                          // this launch's tag (never 0)
+  int32_t poll;
 };
 
 // What the ticket winners of the plan launch need (see plan_kernel).
@@ -60,6 +66,13 @@ struct FinalLaunch {
   const int32_t* best_cand; const double* best_cost;
   const double* am_val; const int64_t* am_idx; const double* tk_val; const int64_t* tk_idx;
   const double* pv; const int64_t* pidx; const int32_t* pnf;
+  // poll = 1: look-ahead blocks publish tagged records and exit; the look-back ticket winner
+  // (after lb_final) polls them and completes the record — no look-ahead ticket, no
+  // last-block scan.  Deadlock-free: only that one block per launch waits, and only for
+  // blocks that never wait.  Needs look-back blocks (do_lb) to host the poller.
+  const uint64_t* la_tag; const uint64_t* blk_tag;
+  uint32_t seq;
+  int32_t poll;
 };
 
 int lookback_blocks(int64_t n);

@@ -29,7 +29,8 @@ __device__ __host__ inline void merge_plan_parts(const llampc_plan_out* parts, i
   m->window_count = p0.window_count;
   m->window_full = p0.window_full;
   m->K = p0.K;
-  m->reserved = 0;
+  m->status = 0;
+  for (int g = 0; g < G; ++g) m->status |= parts[g].status;
 
   // look-back argmin
   double bv = nan_first ? __builtin_inf() : __builtin_nan("");

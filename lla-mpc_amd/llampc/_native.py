@@ -20,7 +20,7 @@ INTEGRATORS = {"rk4": RK4, "euler_nlp": EULER_NLP, "rk6": RK6}
 NAN_FIRST, NAN_IGNORE = 0, 1
 XREF_GIVEN, XREF_RACELINE = 0, 1
 OP_FORCES, OP_DERIV = 0, 1
-E_ARG, E_HIP, E_NODEV, E_STATE, E_OOM = -1, -2, -3, -4, -5
+E_ARG, E_HIP, E_NODEV, E_STATE, E_OOM, E_DEVICE = -1, -2, -3, -4, -5, -6
 
 
 class NativeError(RuntimeError):
@@ -62,7 +62,7 @@ class PlanOut(C.Structure):
                 ("sel_owned", C.c_int32), ("lb_best", C.c_int64), ("lb_best_val", C.c_double),
                 ("sel_model", C.c_int64), ("sel_cand", C.c_int32), ("n_nonfinite", C.c_int32),
                 ("sel_cost", C.c_double), ("la_best_model", C.c_int64), ("la_best_cand", C.c_int32),
-                ("reserved", C.c_int32), ("la_best_cost", C.c_double),
+                ("status", C.c_int32), ("la_best_cost", C.c_double),
                 ("topk", C.c_int64 * KMAX), ("topk_val", C.c_double * KMAX),
                 ("topk_Df", C.c_double * KMAX), ("topk_Dr", C.c_double * KMAX),
                 ("topk_cand", C.c_int32 * KMAX), ("topk_cost", C.c_double * KMAX)]
@@ -214,7 +214,7 @@ def plan_out_to_dict(o: PlanOut) -> dict:
         lb_best=o.lb_best, lb_best_val=o.lb_best_val,
         sel_model=o.sel_model, sel_owned=bool(o.sel_owned), sel_cand=o.sel_cand, sel_cost=o.sel_cost,
         la_best_model=o.la_best_model, la_best_cand=o.la_best_cand, la_best_cost=o.la_best_cost,
-        n_nonfinite=o.n_nonfinite,
+        n_nonfinite=o.n_nonfinite, status=o.status,
         topk=np.array(o.topk[:K], dtype=np.int64), topk_val=np.array(o.topk_val[:K]),
         topk_Df=np.array(o.topk_Df[:K]), topk_Dr=np.array(o.topk_Dr[:K]),
         topk_cand=np.array(o.topk_cand[:K], dtype=np.int32), topk_cost=np.array(o.topk_cost[:K]),

@@ -45,6 +45,8 @@ class PlanResult:
 
 def result_from_out(o: nat.PlanOut, U=None, **extra) -> PlanResult:
     d = nat.plan_out_to_dict(o)
+    if d.get("status", 0):
+        raise nat.NativeError(f"tick record status {d['status']}: the in-launch completion timed out")
     full = d["window_full"] and d["lb_best"] >= 0
     u_seq = None
     if U is not None and d["sel_cand"] >= 0:

@@ -572,6 +572,44 @@ def test_plan_async_two_banks(nat):
             b.close()
 
 
+def test_polled_completion_equals_ticket_completion(nat):
+    """The polled in-launch completion (look-ahead blocks publish tagged records, the
+    look-back winner polls them) gives records identical to the ticket + last-block path
+    (LLAMPC_NO_POLL=1), tick after tick (tags advance per launch; stale words never pass),
+    at C = 1 (LPM 4), C = 3 and C = 64, with the window filling and full; status stays 0."""
+    from llampc import _native
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    H, W = 20, 3
+    rng = np.random.RandomState(9)
+    for N, C in ((5000, 1), (1200, 3), (300, 64)):
+        a_bank = ModelBank(generate_bank(N, seed=3), W=W, device=0)
+        b_bank = ModelBank(generate_bank(N, seed=3), W=W, device=0)
+        try:
+            for t in range(1, W + 4):
+                U = np.repeat(u[:, t:t + H].T[None], C, axis=0)
+                U[1:] += rng.uniform(-0.02, 0.02, U[1:].shape)
+                xref = s[:2, t:t + H + 1] + 0.01 * np.arange(2)[:, None]
+                args = (s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1])
+                o = a_bank.plan_raw(*args, K=5, current_model=1)[0]
+                os.environ["LLAMPC_NO_POLL"] = "1"
+                try:
+                    w = b_bank.plan_raw(*args, K=5, current_model=1)[0]
+                finally:
+                    del os.environ["LLAMPC_NO_POLL"]
+                A, B = _native.plan_out_to_dict(o), _native.plan_out_to_dict(w)
+                assert A["status"] == 0 and B["status"] == 0
+                for k in A:
+                    if isinstance(A[k], np.ndarray):
+                        np.testing.assert_array_equal(A[k], B[k], err_msg=k)
+                    else:
+                        assert A[k] == B[k] or (A[k] != A[k] and B[k] != B[k]), (k, A[k], B[k])
+        finally:
+            a_bank.close()
+            b_bank.close()
+
+
 def test_setupnlp_solve_sampling(nat):
     """setupNLP.solve drop-in (sampling over the NLP transcription on the GPU): the returned
     (umpc, fval, xmpc) are consistent with the oracle's NLP restatement — xmpc is the Euler
