@@ -366,8 +366,10 @@ def lpm_of(n, C):
     while G < C and G < 256:
         G <<= 1
     env = os.environ.get("LLAMPC_LPM")
-    if env == "1" or (env == "2" and G <= 128):
+    if env == "1" or (env == "2" and G <= 128) or (env == "4" and G <= 64):
         return int(env)
+    if n * G <= 16384 and G <= 64:
+        return 4
     return 2 if (n * G <= 32768 and G <= 128) else 1
 
 

@@ -1043,7 +1043,7 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
 // poll round loads, in ONE round trip, each look-ahead block's tagged partial (5 words) and
 // the tagged per-model result of each top-K model and of the selected model (3 words), and
 // repeats until every word carries this launch's tag.  The blocks it waits for never wait,
-// so it cannot deadlock; a bound of ~0.2 s (s_memrealtime) ends a poll that would never
+// so it cannot deadlock; a bound of 2 s (s_memrealtime, 100 MHz) ends a poll that would never
 // finish (a bug) with status LLAMPC_STATUS_POLL_TIMEOUT in the record instead of a hang.
 constexpr int kPollTimeoutStatus = LLAMPC_STATUS_POLL_TIMEOUT;
 __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& sc) {
@@ -1102,7 +1102,7 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
     if (tid == 0) *done = 0;
     __syncthreads();
     if (!ok) *done = 1;                 // any thread not ready -> another round
-    if (tid == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) *done = 2;
+    if (tid == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) *done = 2;   // 2 s
     __syncthreads();
     const int d = *done;
     __syncthreads();
