@@ -803,33 +803,35 @@ __device__ __forceinline__ bool ent_less(const Ent& x, const Ent& y) {
 }
 
 // Element k (0-based) of merge(A, B), |A| = |B| = K, both sorted with sentinel padding:
-// co-rank binary search (merge path), ~log2(K) dependent LDS reads.
-__device__ __forceinline__ Ent merge_path_at(const Ent* A, const Ent* B, int K, int k) {
+// co-rank binary search (merge path), ~log2(K) dependent LDS reads.  E has fields v, i.
+template <typename E>
+__device__ __forceinline__ E merge_path_at(const E* A, const E* B, int K, int k) {
   int lo = 0, hi = k;                       // i = elements taken from A before output k
   while (lo < hi) {
     const int i = (lo + hi) >> 1;
-    if (ent_less(A[i], B[k - i - 1])) lo = i + 1;   // A[i] precedes B[k-i-1]: take more A
+    if (less_nan_last(A[i].v, A[i].i, B[k - i - 1].v, B[k - i - 1].i)) lo = i + 1;
     else hi = i;
   }
   const int i = lo, j = k - lo;
-  return ent_less(A[i], B[j]) ? A[i] : B[j];
+  return (less_nan_last(A[i].v, A[i].i, B[j].v, B[j].i)) ? A[i] : B[j];
 }
 
-// Tree-merge L sorted K-lists in LDS (the cross-shard merge_kernel) (buf0 holds them; buf1 same size); every output
-// element of a level is computed by its own thread.  Returns the buffer holding the merged
-// list (first K entries).
-__device__ __forceinline__ Ent* tree_merge(Ent* buf0, Ent* buf1, int L, int K) {
-  Ent* src = buf0;
-  Ent* dst = buf1;
+// Tree-merge L sorted K-lists in LDS (the cross-shard merge_kernel) (buf0 holds them; buf1
+// same size); every output element of a level is computed by its own thread.  Returns the
+// buffer holding the merged list (first K entries).
+template <typename E>
+__device__ __forceinline__ E* tree_merge(E* buf0, E* buf1, int L, int K) {
+  E* src = buf0;
+  E* dst = buf1;
   while (L > 1) {
     const int P = (L + 1) >> 1;
     for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
       const int p = t / K, k = t - p * K;
-      const Ent* A = src + (size_t)(2 * p) * K;
+      const E* A = src + (size_t)(2 * p) * K;
       dst[t] = (2 * p + 1 < L) ? merge_path_at(A, A + K, K, k) : A[k];
     }
     __syncthreads();
-    Ent* tmp = src;
+    E* tmp = src;
     src = dst;
     dst = tmp;
     L = P;
@@ -1178,82 +1180,85 @@ __global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, Lookahe
 // Cross-shard merge after the all-gather: one wave.  Scalars by lane-parallel reads and
 // shuffles; the shards' sorted top-K lists by the LDS tree merge.  merge.hpp holds the
 // same semantics as straight-line host code (llampc_merge); the tests check both agree.
-__global__ __launch_bounds__(64) void merge_kernel(const llampc_plan_out* parts, int32_t G,
-                                                   int32_t nan_first, llampc_plan_out* m) {
+// A top-K entry of the cross-shard merge with its position in the gathered lists.
+struct EntS {
+  double v;
+  int64_t i;
+  int32_t src;
+  int32_t pad;
+};
+
+__global__ __launch_bounds__(kBlock) void merge_kernel(const llampc_plan_out* parts, int32_t G,
+                                                       int32_t nan_first, llampc_plan_out* m) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = threadIdx.x;
-  const int K = parts[0].K;
+  const int tid = threadIdx.x;
+  // the G gathered records -> LDS in ONE round trip of 16-B loads (every later read is LDS)
+  llampc_plan_out* rec = reinterpret_cast<llampc_plan_out*>(smem);
+  constexpr int kWords = sizeof(llampc_plan_out) / 16;
+  static_assert(sizeof(llampc_plan_out) % 16 == 0, "records staged as 16-B words");
+  const uint4* srcw = reinterpret_cast<const uint4*>(parts);
+  uint4* dstw = reinterpret_cast<uint4*>(rec);
+  for (int e = tid; e < G * kWords; e += kBlock) dstw[e] = srcw[e];
+  __syncthreads();
+  const int K = rec[0].K;
   const int M = G * K;
-  Ent* buf0 = reinterpret_cast<Ent*>(smem);
-  Ent* buf1 = buf0 + M;
-  int64_t* sidx = reinterpret_cast<int64_t*>(buf1 + M);
-  for (int e = lane; e < M; e += 64) {
+  EntS* buf0 = reinterpret_cast<EntS*>(smem + (size_t)G * sizeof(llampc_plan_out));
+  EntS* buf1 = buf0 + M;
+  for (int e = tid; e < M; e += kBlock) {
     const int g = e / K, j = e - g * K;
-    const int64_t id = parts[g].topk[j] < 0 ? kNoIndex : parts[g].topk[j];
-    buf0[e] = Ent{id == kNoIndex ? __builtin_nan("") : parts[g].topk_val[j], id};
-    sidx[e] = id;
+    const int64_t id = rec[g].topk[j] < 0 ? kNoIndex : rec[g].topk[j];
+    buf0[e] = EntS{id == kNoIndex ? __builtin_nan("") : rec[g].topk_val[j], id, e, 0};
   }
-  // look-back argmin over the shards' local argmins; look-ahead best; counts; owners
+  // wave 0: look-back argmin over the shards' local argmins; look-ahead best; counts; owners
+  // — DPP wave reductions over lanes g < G (no LDS shuffles)
   double bv = nan_first ? __builtin_inf() : __builtin_nan("");
   int64_t bi = kNoIndex;
   double av = __builtin_nan("");
-  int64_t am = kNoIndex;
-  int32_t ac = INT32_MAX;
+  int64_t akey = kNoIndex;              // (model << 24 | candidate): la_less's order
   int nf = 0;
-  for (int g = lane; g < G; g += 64) {
-    const llampc_plan_out& p = parts[g];
-    if (p.lb_best >= 0 && key_less(nan_first, p.lb_best_val, p.lb_best, bv, bi)) {
-      bv = p.lb_best_val;
-      bi = p.lb_best;
+  uint32_t owner_lb = kNoLocal, owner_sel = kNoLocal;
+  if (tid < 64) {
+    const int lane = tid;
+    for (int g = lane; g < G; g += 64) {
+      const llampc_plan_out& p = rec[g];
+      if (p.lb_best >= 0 && key_less(nan_first, p.lb_best_val, p.lb_best, bv, bi)) {
+        bv = p.lb_best_val;
+        bi = p.lb_best;
+      }
+      nf += p.n_nonfinite;
+      const int64_t k2 = p.la_best_model >= 0 ? ((int64_t)p.la_best_model << 24) | (uint32_t)p.la_best_cand : kNoIndex;
+      if (k2 != kNoIndex && less_nan_last(p.la_best_cost, k2, av, akey)) {
+        av = p.la_best_cost;
+        akey = k2;
+      }
     }
-    nf += p.n_nonfinite;
-    if (p.la_best_model >= 0 && la_less(p.la_best_cost, p.la_best_model, p.la_best_cand, av, am, ac)) {
-      av = p.la_best_cost;
-      am = p.la_best_model;
-      ac = p.la_best_cand;
+    if (nan_first) wave_min<1>(bv, bi);
+    else wave_min<0>(bv, bi);
+    wave_min<0>(av, akey);
+    nf = wave_sum(nf);
+    uint32_t ol = kNoLocal, os = kNoLocal;
+    for (int g = lane; g < G; g += 64) {
+      if (bi != kNoIndex && rec[g].lb_best == bi) ol = min(ol, (uint32_t)g);
+      if (rec[g].sel_owned) os = min(os, (uint32_t)g);
     }
+    owner_lb = wave_min_u32(ol);
+    owner_sel = wave_min_u32(os);
   }
-  if (nan_first) wave_min<1>(bv, bi);
-  else wave_min<0>(bv, bi);
-  int owner_lb = -1, owner_sel = -1;
-  for (int g = lane; g < G; g += 64) {
-    if (bi != kNoIndex && parts[g].lb_best == bi) owner_lb = g;
-    if (parts[g].sel_owned) owner_sel = g;
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double ov = __shfl_xor(av, off, 64);
-    const int64_t om = __shfl_xor(am, off, 64);
-    const int32_t oc = __shfl_xor(ac, off, 64);
-    if (la_less(ov, om, oc, av, am, ac)) {
-      av = ov;
-      am = om;
-      ac = oc;
-    }
-    nf += __shfl_xor(nf, off, 64);
-    owner_lb = max(owner_lb, __shfl_xor(owner_lb, off, 64));
-    owner_sel = max(owner_sel, __shfl_xor(owner_sel, off, 64));
-  }
+  const int64_t am = akey == kNoIndex ? kNoIndex : (akey >> 24);
+  const int32_t ac = akey == kNoIndex ? INT32_MAX : (int32_t)(akey & 0xFFFFFF);
   __syncthreads();
-  const Ent* r = tree_merge(buf0, buf1, G, K);
-  if (lane < LLAMPC_KMAX) {
-    const int k = lane;
-    const int64_t id = k < K ? r[k].i : kNoIndex;
-    int src = -1;
-    if (id != kNoIndex)
-      for (int e = 0; e < M; ++e)
-        if (sidx[e] == id) {
-          src = e;
-          break;
-        }
-    if (src >= 0) {
-      const int g = src / K, j = src - g * K;
-      m->topk[k] = id;
+  const EntS* r = tree_merge(buf0, buf1, G, K);
+  if (tid < LLAMPC_KMAX) {
+    const int k = tid;
+    const bool have = k < K && r[k].i != kNoIndex;
+    if (have) {                          // the merged entry carries its gathered position
+      const int src = r[k].src, g = src / K, j = src - g * K;
+      m->topk[k] = r[k].i;
       m->topk_val[k] = r[k].v;
-      m->topk_Df[k] = parts[g].topk_Df[j];
-      m->topk_Dr[k] = parts[g].topk_Dr[j];
-      m->topk_cand[k] = parts[g].topk_cand[j];
-      m->topk_cost[k] = parts[g].topk_cost[j];
+      m->topk_Df[k] = rec[g].topk_Df[j];
+      m->topk_Dr[k] = rec[g].topk_Dr[j];
+      m->topk_cand[k] = rec[g].topk_cand[j];
+      m->topk_cost[k] = rec[g].topk_cost[j];
     } else {
       m->topk[k] = -1;
       m->topk_val[k] = m->topk_Df[k] = m->topk_Dr[k] = m->topk_cost[k] =
@@ -1261,26 +1266,26 @@ __global__ __launch_bounds__(64) void merge_kernel(const llampc_plan_out* parts,
       m->topk_cand[k] = -1;
     }
   }
-  if (lane != 0) return;
-  const llampc_plan_out& p0 = parts[0];
+  if (tid != 0) return;
+  const llampc_plan_out& p0 = rec[0];
   m->window_count = p0.window_count;
   m->window_full = p0.window_full;
   m->K = K;
   int32_t st = 0;
-  for (int g = 0; g < G; ++g) st |= parts[g].status;
+  for (int g = 0; g < G; ++g) st |= rec[g].status;
   m->status = st;
   m->lb_best = bi == kNoIndex ? -1 : bi;
   m->lb_best_val = bi == kNoIndex ? __builtin_nan("") : bv;
-  if (m->window_full && owner_lb >= 0) {
+  if (m->window_full && owner_lb != kNoLocal) {
     m->sel_model = bi;
-    m->sel_owned = parts[owner_lb].sel_owned;
-    m->sel_cand = parts[owner_lb].sel_cand;
-    m->sel_cost = parts[owner_lb].sel_cost;
-  } else {
+    m->sel_owned = rec[owner_lb].sel_owned;
+    m->sel_cand = rec[owner_lb].sel_cand;
+    m->sel_cost = rec[owner_lb].sel_cost;
+  } else {                               // the first shard owning sel (merge.hpp)
     m->sel_model = p0.sel_model;
-    m->sel_owned = owner_sel >= 0;
-    m->sel_cand = owner_sel >= 0 ? parts[owner_sel].sel_cand : -1;
-    m->sel_cost = owner_sel >= 0 ? parts[owner_sel].sel_cost : __builtin_nan("");
+    m->sel_owned = owner_sel != kNoLocal;
+    m->sel_cand = owner_sel != kNoLocal ? rec[owner_sel].sel_cand : -1;
+    m->sel_cost = owner_sel != kNoLocal ? rec[owner_sel].sel_cost : __builtin_nan("");
   }
   m->la_best_model = am == kNoIndex ? -1 : am;
   m->la_best_cand = am == kNoIndex ? -1 : ac;
@@ -1538,10 +1543,11 @@ extern "C" int llampc_debug_stamps(unsigned long long* out, unsigned* launches) 
 
 hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
                         llampc_plan_out* merged, hipStream_t s) {
-  if (G < 1 || G > 32) return hipErrorInvalidValue;   // LDS: 40 KB at G = 32
+  if (G < 1 || G > 32) return hipErrorInvalidValue;   // LDS: 95 KB at G = 32
   const size_t M = (size_t)G * LLAMPC_KMAX;      // K <= KMAX (read on device)
-  const size_t lds = 2 * M * sizeof(Ent) + M * sizeof(int64_t);
-  hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(64), lds, s, parts, G, nan_first, merged);
+  const size_t lds = (size_t)G * sizeof(llampc_plan_out) + 2 * M * sizeof(EntS);
+  allow_lds(merge_kernel);
+  hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(kBlock), lds, s, parts, G, nan_first, merged);
   return hipGetLastError();
 }
 

@@ -336,14 +336,16 @@ def test_plan_fused_tick_vs_oracle(nat):
             assert res.global_best[0] * C + res.global_best[1] == int(np.argmin(cref.ravel()))
 
 
-def test_merge_device_equals_host_and_unsharded(nat):
-    """Shard a bank 4 ways on one GPU: device merge == host merge == unsharded tick."""
+@pytest.mark.parametrize("G", [1, 4, 8, 32])
+def test_merge_device_equals_host_and_unsharded(nat, G):
+    """Shard a bank G ways on one GPU (G up to the merge's 32): device merge == host merge
+    == unsharded tick."""
     import ctypes
     import torch
     from llampc.mpc import ModelBank, generate_bank, shard_range
     d = golden("dyn_slice.npz")
     s, u = d["states"], d["inputs"]
-    N, W, G, H, C = 3000, 3, 4, 20, 4
+    N, W, H, C = 3000, 3, 20, 4
     p = generate_bank(N, seed=9)
     U = np.repeat(u[:, 5:5 + H].T[None], C, axis=0)
     U[:, :, 1] += np.linspace(-0.02, 0.02, C)[:, None]
