@@ -35,6 +35,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector spec
 TIMING_STRIDE = 8               # HIP-event pairs bracket groups of 8 consecutive plan launches
 FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation (excl. transcendentals)
+# Issue roofline: instructions per rollout step of the fast look-ahead loop, per lane, by lane
+# split (tools/diag/isa_counts.py on the current sources), and the chip's fp64 VALU issue
+# capacity: 1,024 SIMDs x 16 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md max clock).
+ISSUE_INSTR_PER_STEP = {4: 575, 2: 664, 1: 1033}
+ISSUE_PEAK_LANE_INSTR = 1024 * 16 * 2.4e9
 
 
 def parse():
@@ -264,6 +269,7 @@ def main():
                      "frac": valu_gf / (FP64_VALU_PEAK_TFLOPS * 1e3) if valu_gf else None,
                      "flops_per_model_step": FLOPS_PER_MODEL_STEP,
                      "note": "plain flops only; the 29 fp64 transcendentals per RK4 step are excluded"},
+            "issue": issue_roofline(N_local, C, H, lpm_of(N_local, C), plan_ms),
             "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0])},
             "host_issue_us_per_step": t_issue / args.steps * 1e6,
             "lpm": lpm_of(N_local, C),
@@ -305,7 +311,8 @@ def extras(args, sb, stream, world, rank=0):
     Nt = args.n_per_gpu * world
     if world > 1:
         ms = max_over_ranks(ms)
-    out["C64"] = {"ms_per_step": ms, "value": (Nt * 64 * H + Nt) / (ms / 1e3)}
+    out["C64"] = {"ms_per_step": ms, "value": (Nt * 64 * H + Nt) / (ms / 1e3),
+                  "issue": issue_roofline(args.n_per_gpu, 64, H, lpm_of(args.n_per_gpu, 64), ms)}
     if world == 1:
         pk = make_ticks(args, 1)[0]
         C = args.C
@@ -358,6 +365,21 @@ def concurrent_tracks(args, ticks=1000, warm=50):
             "sel_models": [int(o.sel_model) for o in outs],
             "note": "two independent plan() instances per control step (ETHZ + ETHZMobil), "
                     "async on two streams, host pointers incl. H2D/D2H"}
+
+
+def issue_roofline(n, C, H, lpm, ms):
+    """fp64 VALU issue roofline of the plan kernel: lane-instructions of the look-ahead
+    rollouts (+ the look-back's one LPM-1 step per model) per launch / the launch's mean
+    duration, against the chip's issue capacity.  The binding resource of this kernel."""
+    if not ms or ms <= 0:
+        return None
+    lane_instr = n * C * H * lpm * ISSUE_INSTR_PER_STEP[lpm] + n * ISSUE_INSTR_PER_STEP[1]
+    achieved = lane_instr / (ms * 1e-3)
+    return {"bound": "fp64-valu-issue", "achieved": achieved, "peak": ISSUE_PEAK_LANE_INSTR,
+            "unit": "lane-instructions/s", "frac": achieved / ISSUE_PEAK_LANE_INSTR,
+            "instr_per_step_per_lane": ISSUE_INSTR_PER_STEP[lpm], "lanes_per_rollout": lpm,
+            "note": "a tick at C=1 is one rollout's instruction stream long (628 of 1,024 SIMDs "
+                    "busy at LPM 4, ~4.75 cycles per instruction); C=64 fills the chip"}
 
 
 def lpm_of(n, C):

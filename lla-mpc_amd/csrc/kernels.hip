@@ -285,6 +285,7 @@ __device__ __forceinline__ double window_mean(const double* ring, int64_t ld, in
 // pad to 160 | role-specific region from 160.
 constexpr int kScratchBytes = 160;
 constexpr int kStageW = 6;              // doubles per staged (step, candidate) input
+constexpr int kRankBytes = 64 * 8 + 64 * 4 + 256;   // wave_topk_rank: keys + ids per wave (+pad)
 constexpr int kWaves = kBlock / 64;     // look-back lists per block (one per wave)
 constexpr int kListsPerLane = 8;        // lb_final: lists per lane of the merging wave
 
@@ -358,7 +359,7 @@ __device__ __forceinline__ double sq_err4(const double* x, const double* xn) {
 __device__ __forceinline__ void wave_topk_rank(const LookbackLaunch& a, int64_t list, double w,
                                                int64_t n, unsigned char* lds) {
   const int lane = threadIdx.x & 63;
-  uint64_t* keys = reinterpret_cast<uint64_t*>(lds + (threadIdx.x >> 6) * 768);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(lds + (threadIdx.x >> 6) * kRankBytes);
   uint32_t* ids = reinterpret_cast<uint32_t*>(keys + 64);
   const bool valid = n < a.n;
   const double wc = (w != w) ? __builtin_nan("") : w + 0.0;
@@ -1437,9 +1438,10 @@ int lookback_r(int64_t n, int32_t K) {
 
 int lookback_blocks_r(int64_t n, int R) { return (int)((n + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R)); }
 
-// The in-launch hand-offs (st_wt / ld_wt) are valid for one workgroup per CU: every plan
-// launch requests more than half of the CU's 160 KiB of LDS, so no second block can share a
-// CU whatever the register allocation (the kernel runs one wave per SIMD anyway).
+// Every plan launch requests more than half of the CU's 160 KiB of LDS, so each block has
+// its CU — and each wave its SIMD — to itself.  (Letting LPM-1 launches pack two blocks per
+// CU measured no gain at C = 64: 567-574 vs 568-569 us.)  Every cross-block hand-off is an
+// agent-scope atomic (sc1: L1-bypassing, st_wt / ld_wt).
 constexpr size_t kOneBlockPerCuLds = 82 * 1024;
 
 template <typename KERN>
@@ -1488,7 +1490,10 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
     lbv = *lb;
     lbv.R = lookback_r(lb->n, std::max(1, lb->K));
     f.nb_lb = lookback_blocks_r(lb->n, lbv.R);
-    if (lb->full) lds = std::max(lds, kScratchBytes + (size_t)f.nb_lb * kWaves * (lb->K + 1) * sizeof(Ent));
+    if (lb->full) {
+      lds = std::max(lds, kScratchBytes + (size_t)f.nb_lb * kWaves * (lb->K + 1) * sizeof(Ent));  // lb_final
+      lds = std::max(lds, kScratchBytes + (size_t)kWaves * kRankBytes);                         // wave_topk_rank
+    }
   }
   if (la) {
     lav = *la;
