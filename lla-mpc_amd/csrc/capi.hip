@@ -142,7 +142,7 @@ struct llampc_bank {
   double* d_xref_pm = nullptr;     // per-model references [n][H][2] (RACELINE ticks)
   size_t xref_pm_cap = 0;
   int64_t timing_seen[3] = {0, 0, 0};
-  uint64_t* d_la_tag = nullptr;    // polled completion: [n][3] tagged per-model results
+  uint64_t* d_la_tag = nullptr;    // polled completion: [3][n] tagged per-model results
   uint64_t* d_blk_tag = nullptr;   // [blocks][5] tagged look-ahead block partials
   uint32_t seq = 0;                // launch tag (1, 2, ...; never 0 = the zeroed buffers)
 };

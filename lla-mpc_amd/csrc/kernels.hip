@@ -743,12 +743,10 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     }
   }
   if (live && g == 0 && sub == 0) {
-    if (a.poll) {                       // plain stores (read after the launch) + tagged words
-      a.best_cand[n] = (int32_t)bc;
-      a.best_cost[n] = bv;
-      st_wt(&a.la_tag[3 * n], tag_word(a.seq, (uint32_t)(__double_as_longlong(bv) >> 32)));
-      st_wt(&a.la_tag[3 * n + 1], tag_word(a.seq, (uint32_t)__double_as_longlong(bv)));
-      st_wt(&a.la_tag[3 * n + 2], tag_word(a.seq, (uint32_t)(int32_t)bc));
+    if (a.poll) {                       // tagged words only (SoA: coalesced rows)
+      st_wt(&a.la_tag[n], tag_word(a.seq, (uint32_t)(__double_as_longlong(bv) >> 32)));
+      st_wt(&a.la_tag[a.n + n], tag_word(a.seq, (uint32_t)__double_as_longlong(bv)));
+      st_wt(&a.la_tag[2 * a.n + n], tag_word(a.seq, (uint32_t)(int32_t)bc));
     } else {
       st_wt(&a.best_cand[n], (int32_t)bc);
       st_wt(&a.best_cost[n], bv);
@@ -1073,13 +1071,13 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
     bool ok = true;
     if (mk >= 0) {
 #pragma unroll
-      for (int w = 0; w < 3; ++w) kw[w] = ld_wt(&f.la_tag[3 * mk + w]);
+      for (int w = 0; w < 3; ++w) kw[w] = ld_wt(&f.la_tag[w * f.n + mk]);
 #pragma unroll
       for (int w = 0; w < 3; ++w) ok = (int)ok & (int)tag_ok(kw[w], f.seq);
     }
     if (ms >= 0) {
 #pragma unroll
-      for (int w = 0; w < 3; ++w) sw[w] = ld_wt(&f.la_tag[3 * ms + w]);
+      for (int w = 0; w < 3; ++w) sw[w] = ld_wt(&f.la_tag[w * f.n + ms]);
 #pragma unroll
       for (int w = 0; w < 3; ++w) ok = (int)ok & (int)tag_ok(sw[w], f.seq);
     }

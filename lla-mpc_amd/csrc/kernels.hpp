@@ -50,7 +50,7 @@ struct LookaheadLaunch {
   double* xref_pm;                       // RACELINE: per-model reference [n][H][2]
   // polled completion (FinalLaunch::poll): tagged records, each 64-bit word = seq << 32 |
   // 32 payload bits, so a reader validates every word it loads on its own
-  uint64_t* la_tag;                      // [n][3]: best cost hi, lo, best candidate
+  uint64_t* la_tag;                      // [3][n]: best cost hi, lo, best candidate (SoA)
   uint64_t* blk_tag;                     // [blocks][5]: partial value hi, lo, key hi, lo, nf
   uint32_t seq;                          // this launch's tag (never 0)
   int32_t poll;
