@@ -28,19 +28,6 @@
 #define LL_SIN(a) ::llampc::fm::sin_(a)
 #define LL_SINCOS(a, s, c) ::llampc::fm::sincos_((a), (s), (c))
 #endif
-// Estrin (short-chain) variants for the latency-bound split kernels.
-#ifdef LLAMPC_OCML_MATH
-#define LL_ATAN2P_E(y, x) atan2((y), (x))
-#define LL_ATAN_E(z) atan(z)
-#define LL_SIN_E(a) sin(a)
-#define LL_SINCOS_E(a, s, c) sincos((a), (s), (c))
-#else
-#define LL_ATAN2P_E(y, x) ::llampc::fm::atan2_xpos<true>((y), (x))
-#define LL_ATAN_E(z) ::llampc::fm::atan_<true>(z)
-#define LL_SIN_E(a) ::llampc::fm::sin_<true>(a)
-#define LL_SINCOS_E(a, s, c) ::llampc::fm::sincos_<true>((a), (s), (c))
-#endif
-
 namespace llampc {
 
 // Per-bank constants in kernel-argument space (wave-uniform → SGPRs).
@@ -244,19 +231,6 @@ constexpr int kPair0 = 0xA0, kPair1 = 0xF5;
 constexpr int kQuad0 = 0x00, kQuad1 = 0x55, kQuad2 = 0xAA, kQuad3 = 0xFF;
 constexpr int kQuadX1 = 0xB1, kQuadX2 = 0x4E;
 
-// Polynomial scheme of the fast chain: Horner.  Estrin (-DLLAMPC_CHAIN_EST=1, A/B builds)
-// shortens the chain's dependency depth but adds instructions, and the stage is issue-
-// bound even at LPM 4 (measured: 4.7 shader cycles per instruction at one wave per SIMD;
-// Estrin +1 us per tick at LPM 2 and 4).
-template <int LPM>
-struct ChainEst {
-#ifdef LLAMPC_CHAIN_EST
-  static constexpr bool value = LLAMPC_CHAIN_EST != 0;
-#else
-  static constexpr bool value = false;
-#endif
-};
-
 // One tire's constants in this lane: front (lw = lf, sg = +1) or rear (lw = lr, sg = -1).
 struct Chain {
   double lw, sg, B, C, D;
@@ -299,17 +273,16 @@ struct Dom {
 // F = D sin(C atan(B slip)) with slip = dsel - atan2(yy, den) for the front tire
 // (dsel = delta) and atan2(yy, den) for the rear (dsel = 0); yy = lf om + vy | lr om - vy
 // (dynamic.py:149-152 / :215-220).  The divisors go to the lane's Dom.
-template <bool EST>
 __device__ __forceinline__ double chain_fast(const Chain& c, double den, double vy, double om,
                                              double dsel, Dom& dm, const fm::FmK& K) {
   const double yy = fma(c.lw, om, c.sg * vy);
   double h2, hz;
-  const double a2 = fm::atan2_fast<EST>(yy, den, K, h2);
+  const double a2 = fm::atan2_fast(yy, den, K, h2);
   const double z = c.B * fma(-c.sg, a2, dsel);
-  const double at = fm::atan_fast<EST>(z, K, hz);
+  const double at = fm::atan_fast(z, K, hz);
   dm.lo = fm::vmin(dm.lo, h2);
   dm.hi = fm::vmax(dm.hi, fm::vmax(h2, hz));
-  return c.D * fm::sin_wide<EST>(c.C * at, K);
+  return c.D * fm::sin_wide(c.C * at, K);
 }
 
 // LPM = 4: the quad's lanes run ONE instruction stream — lanes 0/1 the front/rear chain,
@@ -323,7 +296,6 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
 __device__ __forceinline__ double chain_fold(const Chain& c, double den, double vy, double om,
                                              double Bd, double psi, int ra, double pm,
                                              double po, Dom& dm, const fm::FmK& K) {
-  constexpr bool EST = ChainEst<4>::value;
   const double t2 = fma(psi, K.two_pi, K.rmagic2);       // 2^53 (1.5 + 2k 2^-53): ulp 2
   const double k2 = t2 - K.rmagic2;
   double r = fma(-k2, K.cw0, psi);
@@ -342,13 +314,13 @@ __device__ __forceinline__ double chain_fold(const Chain& c, double den, double 
 #endif
     const double yy = fma(c.lw, om, c.sg * vy);
     double h2, hz;
-    const double a2 = fm::atan2_fast<EST>(yy, den, K, h2);
+    const double a2 = fm::atan2_fast(yy, den, K, h2);
     const double z = fma(c.nsB, a2, Bd);                  // B (dsel - sg a2)
-    at = fm::atan_fast<EST>(z, K, hz);
+    at = fm::atan_fast(z, K, hz);
     dm.lo = fm::vmin(dm.lo, h2);
     dm.hi = fm::vmax(dm.hi, fm::vmax(h2, hz));
   }
-  return c.D * fm::sin_wide<EST>(fma(c.C, at, arg_psi), K);
+  return c.D * fm::sin_wide(fma(c.C, at, arg_psi), K);
 }
 
 // Per-rollout constants of the fast stage.  ch[0] is this lane's chain (LPM = 2) or the
@@ -412,12 +384,12 @@ __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, doub
     return f;
   }
   if (LPM == 2) {
-    const double r = chain_fast<ChainEst<2>::value>(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
+    const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
     f.Ffy = dpp_bcast<kPair0>(r);
     f.Fry = dpp_bcast<kPair1>(r);
   } else {
-    f.Ffy = chain_fast<ChainEst<1>::value>(sk.ch[0], den, vy, om, d, dm, K);
-    f.Fry = chain_fast<ChainEst<1>::value>(sk.ch[1], den, vy, om, 0.0, dm, K);
+    f.Ffy = chain_fast(sk.ch[0], den, vy, om, d, dm, K);
+    f.Fry = chain_fast(sk.ch[1], den, vy, om, 0.0, dm, K);
   }
   fm::sincos_fast(psi, &f.sp, &f.cp, K);
   return f;

@@ -47,36 +47,20 @@ constexpr double kTwoOverPi = 0.6366197723675814, kPio2 = 1.5707963267948966,
 constexpr double kPio2Tail = 6.123233995736766e-17;   // pi/2 - (double)(pi/2)
 constexpr double kSinCosMax = 1647099.3291652855;      // 2^20 * pi/2
 
-// Two evaluation schemes for every polynomial core:
-//   EST = false  Horner: one SGPR constant per v_fmac, fewest instructions — for the
-//                issue-bound one-lane-per-rollout kernels (many waves per SIMD);
-//   EST = true   Estrin: dependency depth ~log2(terms) — for the lane/wave-split kernels
-//                where ONE dependent chain per wave bounds the stage (latency-bound).
-template <bool EST>
+// Horner evaluation throughout: the kernels are issue-bound (Estrin's
+// shorter dependency chains cost more instructions and measured slower).
 __device__ __host__ __forceinline__ double atan_q(double s) {
   const double* c = kAtanQ;
-  if (!EST) {
-    double p = c[21];
+  double p = c[21];
 #pragma unroll
-    for (int i = 20; i >= 0; --i) p = fma(p, s, c[i]);
-    return p;
-  }
-  const double s2 = s * s, s4 = s2 * s2, s8 = s4 * s4, s16 = s8 * s8;
-  const double p0 = fma(c[1], s, c[0]), p1 = fma(c[3], s, c[2]), p2 = fma(c[5], s, c[4]),
-               p3 = fma(c[7], s, c[6]), p4 = fma(c[9], s, c[8]), p5 = fma(c[11], s, c[10]),
-               p6 = fma(c[13], s, c[12]), p7 = fma(c[15], s, c[14]), p8 = fma(c[17], s, c[16]),
-               p9 = fma(c[19], s, c[18]), p10 = fma(c[21], s, c[20]);
-  const double q0 = fma(p1, s2, p0), q1 = fma(p3, s2, p2), q2 = fma(p5, s2, p4),
-               q3 = fma(p7, s2, p6), q4 = fma(p9, s2, p8);
-  const double r0 = fma(q1, s4, q0), r1 = fma(q3, s4, q2), r2 = fma(p10, s4, q4);
-  return fma(r2, s16, fma(r1, s8, r0));
+  for (int i = 20; i >= 0; --i) p = fma(p, s, c[i]);
+  return p;
 }
 
 // atan(t) for |t| <= 1.
-template <bool EST>
 __device__ __host__ __forceinline__ double atan_core(double t) {
   const double s = t * t;
-  return fma(t * s, atan_q<EST>(s), t);
+  return fma(t * s, atan_q(s), t);
 }
 
 // num / den by reciprocal + two Newton steps + one residual correction (8 VALU instead of
@@ -100,11 +84,10 @@ __device__ __host__ __forceinline__ double div_(double num, double den) {
 
 // atan2(y, x) for x >= +0 (or NaN): one division, no quadrant branches.  Special cases
 // follow C99 atan2 for x >= 0: (+-0, +0) -> +-0, (+-inf, +inf) -> +-pi/4.
-template <bool EST = false>
 __device__ __host__ __forceinline__ double atan2_xpos(double y, double x) {
   const bool swap = fabs(y) > x;
   const double num = swap ? x : y, den = swap ? y : x;
-  const double r = atan_core<EST>(div_(num, den));
+  const double r = atan_core(div_(num, den));
   double out = swap ? (copysign(kPio2, y) - r) + copysign(kPio2Tail, y) : r;
   if (x == 0.0 && y == 0.0) out = y;
   if (isinf(x) && isinf(y)) out = copysign(kPio4, y);
@@ -112,45 +95,35 @@ __device__ __host__ __forceinline__ double atan2_xpos(double y, double x) {
 }
 
 // atan(z): the division only when some |z| > 1.
-template <bool EST = false>
 __device__ __host__ __forceinline__ double atan_(double z) {
   const bool swap = fabs(z) > 1.0;
   double t = z;
   if (swap) t = 1.0 / z;
-  const double r = atan_core<EST>(t);
+  const double r = atan_core(t);
   return swap ? (copysign(kPio2, z) - r) + copysign(kPio2Tail, z) : r;
 }
 
-template <bool EST>
 __device__ __host__ __forceinline__ double poly7(const double* a, double s1) {
-  if (!EST) {
-    double p = a[6];
+  double p = a[6];
 #pragma unroll
-    for (int i = 5; i >= 0; --i) p = fma(p, s1, a[i]);
-    return p;
-  }
-  const double s2 = s1 * s1, s4 = s2 * s2;
-  return fma(fma(a[6], s2, fma(a[5], s1, a[4])), s4, fma(fma(a[3], s1, a[2]), s2, fma(a[1], s1, a[0])));
+  for (int i = 5; i >= 0; --i) p = fma(p, s1, a[i]);
+  return p;
 }
 
-template <bool EST>
 __device__ __host__ __forceinline__ double sin_poly(double r, double s1) {
-  return fma(r * s1, poly7<EST>(kSinQ, s1), r);
+  return fma(r * s1, poly7(kSinQ, s1), r);
 }
 
-template <bool EST>
 __device__ __host__ __forceinline__ double cos_poly(double s1) {
-  return fma(s1 * s1, poly7<EST>(kCosQ, s1), fma(-0.5, s1, 1.0));
+  return fma(s1 * s1, poly7(kCosQ, s1), fma(-0.5, s1, 1.0));
 }
 
-template <bool EST>
 __device__ __host__ __forceinline__ void sincos_core(double r, double* s, double* c) {
   const double s1 = r * r;
-  *s = sin_poly<EST>(r, s1);
-  *c = cos_poly<EST>(s1);
+  *s = sin_poly(r, s1);
+  *c = cos_poly(s1);
 }
 
-template <bool EST = false>
 __device__ __host__ __forceinline__ void sincos_(double a, double* s, double* c) {
   if (!(fabs(a) <= kSinCosMax)) {       // huge or non-finite: ocml (Payne-Hanek)
     sincos(a, s, c);
@@ -162,7 +135,7 @@ __device__ __host__ __forceinline__ void sincos_(double a, double* s, double* c)
   r = fma(-k, kPio2Lo, r);
   const int q = (int)k & 3;
   double sr, cr;
-  sincos_core<EST>(r, &sr, &cr);
+  sincos_core(r, &sr, &cr);
   double so = (q & 1) ? cr : sr, co = (q & 1) ? sr : cr;
   so = (q & 2) ? -so : so;
   co = ((q + 1) & 2) ? -co : co;
@@ -172,13 +145,12 @@ __device__ __host__ __forceinline__ void sincos_(double a, double* s, double* c)
 
 // sin(a): wave-uniform fast path when every |a| <= pi/4 (no reduction, one polynomial) —
 // the common case for the tire argument C*atan(B*alpha) at moderate slip.
-template <bool EST = false>
 __device__ __host__ __forceinline__ double sin_(double a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (__all(fabs(a) <= kPio4)) return sin_poly<EST>(a, a * a);
+  if (__all(fabs(a) <= kPio4)) return sin_poly(a, a * a);
 #endif
   double s, c;
-  sincos_<EST>(a, &s, &c);
+  sincos_(a, &s, &c);
   return s;
 }
 
@@ -279,29 +251,6 @@ __device__ __forceinline__ double div6(double v, const FmK& K) {
   return fma(fma(-K.six, q, v), K.sixth, q);
 }
 
-// Estrin forms of the fast cores' polynomials: dependency depth 5 (22 terms) / 4 (11 terms)
-// instead of 21 / 10 for +4 / +3 instructions.  With one wave per SIMD a dependent fp64 FMA
-// costs ~6 cycles and an independent one ~4 (issue), so a chain that nothing else can fill
-// — the tire chain of a lane-split rollout (LPM >= 2) — is faster in Estrin form.
-__device__ __forceinline__ double estrin22(const double* c, double s) {
-  const double s2 = s * s, s4 = s2 * s2, s8 = s4 * s4, s16 = s8 * s8;
-  const double p0 = fma(c[1], s, c[0]), p1 = fma(c[3], s, c[2]), p2 = fma(c[5], s, c[4]),
-               p3 = fma(c[7], s, c[6]), p4 = fma(c[9], s, c[8]), p5 = fma(c[11], s, c[10]),
-               p6 = fma(c[13], s, c[12]), p7 = fma(c[15], s, c[14]), p8 = fma(c[17], s, c[16]),
-               p9 = fma(c[19], s, c[18]), p10 = fma(c[21], s, c[20]);
-  const double q0 = fma(p1, s2, p0), q1 = fma(p3, s2, p2), q2 = fma(p5, s2, p4),
-               q3 = fma(p7, s2, p6), q4 = fma(p9, s2, p8);
-  const double r0 = fma(q1, s4, q0), r1 = fma(q3, s4, q2), r2 = fma(p10, s4, q4);
-  return fma(r2, s16, fma(r1, s8, r0));
-}
-__device__ __forceinline__ double estrin11(const double* c, double s) {
-  const double s2 = s * s, s4 = s2 * s2, s8 = s4 * s4;
-  const double p0 = fma(c[1], s, c[0]), p1 = fma(c[3], s, c[2]), p2 = fma(c[5], s, c[4]),
-               p3 = fma(c[7], s, c[6]), p4 = fma(c[9], s, c[8]);
-  const double q0 = fma(p1, s2, p0), q1 = fma(p3, s2, p2), q2 = fma(c[10], s2, p4);
-  return fma(q2, s8, fma(q1, s4, q0));
-}
-
 // IEEE maxNum / minNum as ONE instruction.  fmax/fmin compile to v_max_f64/v_min_f64 plus a
 // canonicalising v_max_f64 x, x of every operand the compiler cannot prove canonical (loop-
 // carried values, fabs results): 5 extra instructions per rollout stage.  The operands here
@@ -338,10 +287,9 @@ __device__ __forceinline__ double vmin_abs2(double a, double b) {  // min(|a|, |
   return r;
 }
 
-template <bool EST = false>
 __device__ __forceinline__ double atan_core_k(double t, const FmK& K) {
   const double s = t * t;
-  return fma(t * s, EST ? estrin22(K.at, s) : horner<22>(K.at, s), t);
+  return fma(t * s, horner<22>(K.at, s), t);
 }
 
 // atan2(y, x) for x >= 0 on the domain atan2_fast_ok(y, x): the sum |y| + x in
@@ -353,11 +301,10 @@ __device__ __host__ __forceinline__ bool atan2_fast_ok(double y, double x) {
 // hi = max(|y|, |x|), the divisor: hi in [2^-1000, 2^999] lies inside the domain (the
 // rollout checks its running extremes once, dyn.hpp Dom).  x enters as |x| (the callers'
 // x is |vx| or the clamped vx >= vmin, so passing vx itself saves materialising |vx|).
-template <bool EST = false>
 __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K, double& hi) {
   const double ay = fabs(y);
   hi = vmax_abs2(y, x);
-  const double r = atan_core_k<EST>(div_fast(vmin_abs2(y, x), hi), K);
+  const double r = atan_core_k(div_fast(vmin_abs2(y, x), hi), K);
   const double o = (ay > fabs(x)) ? K.pio2 - r : r;   // no pi/2 tail: <= 2 ulp (measured)
   return copysign(o, y);
 }
@@ -370,11 +317,10 @@ __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K) {
 // (exact when |z| <= 1).
 __device__ __host__ __forceinline__ bool atan_fast_ok(double z) { return fabs(z) <= 0x1p1000; }
 // hz = max(|z|, 1), the divisor: hz <= 2^1000 is the domain.
-template <bool EST = false>
 __device__ __forceinline__ double atan_fast(double z, const FmK& K, double& hz) {
   const double az = fabs(z);
   hz = vmax_abs(z, K.one);
-  const double r = atan_core_k<EST>(div_fast(vmin_abs(z, K.one), hz), K);
+  const double r = atan_core_k(div_fast(vmin_abs(z, K.one), hz), K);
   const double o = (az > 1.0) ? K.pio2 - r : r;   // no pi/2 tail: <= 2 ulp (measured)
   return copysign(o, z);
 }
@@ -385,10 +331,9 @@ __device__ __forceinline__ double atan_fast(double z, const FmK& K) {
 
 // sin(a) for |a| <= kSinWideMax, one polynomial (the Pacejka argument C*atan(.) is
 // bounded by |C| pi/2, so |C| <= 1.9 keeps every call in range).
-template <bool EST = false>
 __device__ __forceinline__ double sin_wide(double a, const FmK& K) {
   const double s = a * a;
-  return fma(a * s, EST ? estrin11(K.sw, s) : horner<11>(K.sw, s), a);
+  return fma(a * s, horner<11>(K.sw, s), a);
 }
 
 // sincos(a) for |a| <= kSinCosMax (NaN/inf -> not ok): Cody-Waite reduction, quadrant
