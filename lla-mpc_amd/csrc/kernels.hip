@@ -1040,13 +1040,15 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
   final_write(f, lb, sel, owned, kcand, kcost, scand, scost, lav, lai, nf);
 }
 
-// Polled completion (f.poll): run by the look-back ticket winner after lb_final.  Every
-// poll round loads, in ONE round trip, each look-ahead block's tagged partial (5 words) and
-// the tagged per-model result of each top-K model and of the selected model (3 words), and
-// repeats until every word carries this launch's tag.  The blocks it waits for never wait,
-// so it cannot deadlock; a bound of 2 s (s_memrealtime, 100 MHz) ends a poll that would never
-// finish (a bug) with status LLAMPC_STATUS_POLL_TIMEOUT in the record instead of a hang.
+// Polled completion (f.poll): run by the look-back ticket winner after lb_final.  Each thread
+// spins on its share of the tagged words — the look-ahead blocks' partials (5 words each),
+// the top-K models' and the selected model's results (3 words each) — until every word it
+// loads carries this launch's tag; one block barrier then joins them.  The blocks it waits
+// for never wait, so it cannot deadlock; a 2 s bound (s_memrealtime, 100 MHz) ends a poll
+// that could never finish (a bug) with status LLAMPC_STATUS_POLL_TIMEOUT in the record
+// instead of a hang.
 constexpr int kPollTimeoutStatus = LLAMPC_STATUS_POLL_TIMEOUT;
+constexpr uint64_t kPollBound = 200000000ull;   // 2 s of s_memrealtime (100 MHz)
 __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& sc) {
   STAMP(3);
   const int tid = threadIdx.x;
@@ -1065,54 +1067,53 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
   int64_t lai = kNoIndex;
   int nf = 0;
   int status = 0;
+  // every thread spins on its own words (no block barrier per round: a thread's next loads
+  // issue as soon as its previous ones return); one barrier after all are current
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  int* done = reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(sc.sv) + 152);  // scratch pad
-  for (;;) {
-    bool ok = true;
-    if (mk >= 0) {
+  bool late = false;
+  if (mk >= 0) {
+    for (;;) {
 #pragma unroll
       for (int w = 0; w < 3; ++w) kw[w] = ld_wt(&f.la_tag[w * f.n + mk]);
-#pragma unroll
-      for (int w = 0; w < 3; ++w) ok = (int)ok & (int)tag_ok(kw[w], f.seq);
-    }
-    if (ms >= 0) {
-#pragma unroll
-      for (int w = 0; w < 3; ++w) sw[w] = ld_wt(&f.la_tag[w * f.n + ms]);
-#pragma unroll
-      for (int w = 0; w < 3; ++w) ok = (int)ok & (int)tag_ok(sw[w], f.seq);
-    }
-    lav = __builtin_nan("");
-    lai = kNoIndex;
-    nf = 0;
-    for (int j = 0; j < nbt; ++j) {
-      const int b = tid + j * kBlock;
-      if (b < f.nb_la) {
-        uint64_t r[5];
-#pragma unroll
-        for (int w = 0; w < 5; ++w) r[w] = ld_wt(&f.blk_tag[5 * (int64_t)b + w]);
-#pragma unroll
-        for (int w = 0; w < 5; ++w) ok = (int)ok & (int)tag_ok(r[w], f.seq);
-        const double pv = __longlong_as_double((long long)join_words(r[0], r[1]));
-        const int64_t pi = (int64_t)join_words(r[2], r[3]);
-        nf += (int)(uint32_t)r[4];
-        const bool t = (int)(pi != kNoIndex) & (int)less_bf<0>(pv, pi, lav, lai);
-        lav = t ? pv : lav;
-        lai = t ? pi : lai;
-      }
-    }
-    if (tid == 0) *done = 0;
-    __syncthreads();
-    if (!ok) *done = 1;                 // any thread not ready -> another round
-    if (tid == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) *done = 2;   // 2 s
-    __syncthreads();
-    const int d = *done;
-    __syncthreads();
-    if (d == 0) break;
-    if (d == 2) {
-      status = kPollTimeoutStatus;
-      break;
+      if ((int)tag_ok(kw[0], f.seq) & (int)tag_ok(kw[1], f.seq) & (int)tag_ok(kw[2], f.seq)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kPollBound) { late = true; break; }
     }
   }
+  if (ms >= 0) {
+    for (;;) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) sw[w] = ld_wt(&f.la_tag[w * f.n + ms]);
+      if ((int)tag_ok(sw[0], f.seq) & (int)tag_ok(sw[1], f.seq) & (int)tag_ok(sw[2], f.seq)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kPollBound) { late = true; break; }
+    }
+  }
+  for (int j = 0; j < nbt; ++j) {
+    const int b = tid + j * kBlock;
+    if (b < f.nb_la) {
+      uint64_t r[5];
+      for (;;) {
+#pragma unroll
+        for (int w = 0; w < 5; ++w) r[w] = ld_wt(&f.blk_tag[5 * (int64_t)b + w]);
+        if ((int)tag_ok(r[0], f.seq) & (int)tag_ok(r[1], f.seq) & (int)tag_ok(r[2], f.seq) &
+            (int)tag_ok(r[3], f.seq) & (int)tag_ok(r[4], f.seq))
+          break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kPollBound) { late = true; break; }
+      }
+      const double pv = __longlong_as_double((long long)join_words(r[0], r[1]));
+      const int64_t pi = (int64_t)join_words(r[2], r[3]);
+      nf += (int)(uint32_t)r[4];
+      const bool t = (int)(pi != kNoIndex) & (int)less_bf<0>(pv, pi, lav, lai);
+      lav = t ? pv : lav;
+      lai = t ? pi : lai;
+    }
+  }
+  // (no __syncthreads_or: its static LDS would break the launches' full-LDS requests)
+  int* any_late = reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(sc.sv) + 152);
+  if (tid == 0) *any_late = 0;
+  __syncthreads();
+  if (late) *any_late = 1;
+  __syncthreads();
+  if (*any_late) status = kPollTimeoutStatus;
   int32_t kcand = -1, scand = -1;
   double kcost = __builtin_nan(""), scost = __builtin_nan("");
   if (mk >= 0 && f.do_la) {
