@@ -197,13 +197,17 @@ int llampc_bank_set_raceline(llampc_bank* bank, const double* knots, int32_t n, 
                              const double* speed, const double* mus, int32_t M);
 
 /* ---- fused tick ------------------------------------------------------------------ */
-/* Host pointers; blocking.  err_out [n], wmean_out [n], cost_out [n][C] may be NULL. */
+/* Host pointers; blocking.  err_out [n], wmean_out [n], cost_out [n][C] may be NULL.
+ * With all three NULL the kernel writes the record into the bank's pinned host buffer and
+ * then a completion tag; the call spins on the tag (no D2H copy, no stream synchronise).
+ * LLAMPC_SYNC_COMPLETION=1 in the environment selects the copy + synchronise path. */
 int llampc_plan(llampc_bank* bank, const llampc_plan_in* in, llampc_plan_out* out,
                 double* err_out, double* wmean_out, double* cost_out);
 /* Host pointers; asynchronous (SURVEY.md §8b "_async" variant): the inputs are copied
  * into the bank's pinned staging buffer before the call returns (the caller may reuse
- * them), and the H2D copy, the plan kernel and the D2H copy of the result record are
- * enqueued on the bank's stream.  llampc_plan_wait synchronises and returns the record.
+ * them), and the H2D copy and the plan kernel are enqueued on the bank's stream; the
+ * kernel writes the record to pinned host memory + a completion tag, on which
+ * llampc_plan_wait spins before returning the record.
  * At most one outstanding async tick per bank (LLAMPC_E_STATE otherwise); independent
  * banks (e.g. two tracks) overlap on the device. */
 int llampc_plan_async(llampc_bank* bank, const llampc_plan_in* in);

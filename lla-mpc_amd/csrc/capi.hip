@@ -5,10 +5,12 @@
 // the look-back ring [W][n] (slot-major, so each tick writes one contiguous row — the
 // reference's np.roll copy of N*W doubles per tick, rt.py:352, is gone), per-block
 // reduction partials, the per-model look-ahead result, and pinned host staging so one
-// tick = 1 H2D copy + 3 kernels + 1 D2H copy on one stream.
+// host-pointer tick = 1 H2D copy + 1 kernel on one stream, the record coming back through
+// pinned host memory with a completion tag (llampc_plan / llampc_plan_wait).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -145,6 +147,15 @@ struct llampc_bank {
   uint64_t* d_la_tag = nullptr;    // polled completion: [3][n] tagged per-model results
   uint64_t* d_blk_tag = nullptr;   // [blocks][5] tagged look-ahead block partials
   uint32_t seq = 0;                // launch tag (1, 2, ...; never 0 = the zeroed buffers)
+  // host completion (llampc_plan, llampc_plan_async/wait): the plan kernel writes the record
+  // straight into pinned host memory and then stores the tick's number into h_tag; the host
+  // spins on h_tag (no D2H copy, no stream synchronisation on the path)
+  llampc_plan_out* h_rec = nullptr;  // pinned, coherent; d_rec is its device alias
+  llampc_plan_out* d_rec = nullptr;
+  uint64_t* h_tag = nullptr;
+  uint64_t* d_tag = nullptr;
+  uint64_t hseq = 0;
+  uint64_t async_seq = 0;          // the outstanding llampc_plan_async tick's tag (0: copy path)
 };
 
 namespace {
@@ -251,7 +262,8 @@ void timing_free(llampc_bank* b) {
 // The tick on device pointers: ONE launch (look-back + look-ahead + completion).
 // Advances the window bookkeeping when a look-back runs.
 int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out, double* d_err,
-                double* d_wmean, double* d_cost, hipStream_t s) {
+                double* d_wmean, double* d_cost, hipStream_t s, uint64_t* host_tag = nullptr,
+                uint64_t host_seq = 0) {
   if (int rc = ensure_xref_pm(b, &in)) return rc;
   const bool lb = in.do_lookback != 0;
   const bool la = in.do_lookahead != 0;
@@ -346,6 +358,8 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   f.blk_tag = b->d_blk_tag;
   f.seq = b->seq;
   f.poll = poll;
+  f.host_tag = host_tag;
+  f.host_seq = host_seq;
   if (la) {
     lal.la_tag = b->d_la_tag;
     lal.blk_tag = b->d_blk_tag;
@@ -397,6 +411,30 @@ int stage_inputs(llampc_bank* b, const llampc_plan_in* in, llampc_plan_in* dev_i
 }
 
 hipStream_t pick_stream(llampc_bank* b, void* s) { return s ? (hipStream_t)s : b->stream; }
+
+// Host completion is the default for host-pointer ticks that return only the record;
+// LLAMPC_SYNC_COMPLETION=1 selects the D2H copy + hipStreamSynchronize path (A/B runs).
+bool host_completion(const llampc_bank* b) {
+  return b->h_tag && b->h_rec && getenv("LLAMPC_SYNC_COMPLETION") == nullptr;
+}
+
+// Spin until the plan kernel has published tick `seq` in h_tag, then copy the record out.
+// A tag that never arrives (a device fault) ends the spin after 10 s: the stream is then
+// synchronised so the HIP error, if any, is the one reported.
+int wait_host_tag(llampc_bank* b, uint64_t seq, llampc_plan_out* out) {
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t spins = 0;
+  while (__atomic_load_n(b->h_tag, __ATOMIC_ACQUIRE) != seq) {
+    __builtin_ia32_pause();
+    if ((++spins & 0xFFF) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      HIP_TRY(hipStreamSynchronize(b->stream));
+      if (__atomic_load_n(b->h_tag, __ATOMIC_ACQUIRE) == seq) break;
+      return fail(LLAMPC_E_DEVICE, "tick %llu: completion tag never arrived", (unsigned long long)seq);
+    }
+  }
+  std::memcpy(out, const_cast<const llampc_plan_out*>(b->h_rec), sizeof(llampc_plan_out));
+  return LLAMPC_OK;
+}
 
 
 
@@ -464,6 +502,14 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
     return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&b->h_out), sizeof(llampc_plan_out), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(out) failed"));
+  if (hipHostMalloc(reinterpret_cast<void**>(&b->h_rec), sizeof(llampc_plan_out),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&b->h_tag), 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(host completion record) failed"));
+  *b->h_tag = 0;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&b->d_rec), b->h_rec, 0) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&b->d_tag), b->h_tag, 0) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_HIP, "hipHostGetDevicePointer(host completion record) failed"));
   if (hipMemcpy(b->d_params, params, 6 * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(b->d_ring, 0, (size_t)W * n * sizeof(double)) != hipSuccess ||
       hipMemset(b->d_tickets, 0, 2 * sizeof(unsigned)) != hipSuccess ||
@@ -488,6 +534,8 @@ int llampc_bank_destroy(llampc_bank* b) {
       if (p) (void)hipFree(p);
     if (b->h_in) (void)hipHostFree(b->h_in);
     if (b->h_out) (void)hipHostFree(b->h_out);
+    if (b->h_rec) (void)hipHostFree(b->h_rec);
+    if (b->h_tag) (void)hipHostFree(b->h_tag);
     timing_free(b);
     if (b->own_stream && b->stream) (void)hipStreamDestroy(b->stream);
   }
@@ -608,6 +656,14 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
   if (cost_out && in->do_lookahead && (rc = ensure_cost(b, (size_t)b->n * in->C))) return rc;
   llampc_plan_in din;
   if ((rc = stage_inputs(b, in, &din, s))) return rc;
+  if (!err_out && !wmean_out && !cost_out && host_completion(b)) {
+    // the record only: the kernel writes it to pinned host memory and publishes a tag
+    const uint64_t seq = ++b->hseq;
+    if ((rc = plan_launch(b, din, b->d_rec, nullptr, nullptr, nullptr, s, b->d_tag, seq))) return rc;
+    if ((rc = wait_host_tag(b, seq, out))) return rc;
+    if (out->status) return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", out->status);
+    return LLAMPC_OK;
+  }
   double* d_cost = (cost_out && in->do_lookahead) ? b->d_cost : nullptr;
   if ((rc = plan_launch(b, din, b->d_out, err_out ? b->d_err : nullptr,
                         wmean_out ? b->d_wmean : nullptr, d_cost, s)))
@@ -665,8 +721,14 @@ int llampc_plan_async(llampc_bank* b, const llampc_plan_in* in) {
   hipStream_t s = b->stream;
   llampc_plan_in din;
   if ((rc = stage_inputs(b, in, &din, s))) return rc;
-  if ((rc = plan_launch(b, din, b->d_out, nullptr, nullptr, nullptr, s))) return rc;
-  HIP_TRY(hipMemcpyAsync(b->h_out, b->d_out, sizeof(llampc_plan_out), hipMemcpyDeviceToHost, s));
+  if (host_completion(b)) {
+    b->async_seq = ++b->hseq;
+    if ((rc = plan_launch(b, din, b->d_rec, nullptr, nullptr, nullptr, s, b->d_tag, b->async_seq))) return rc;
+  } else {
+    b->async_seq = 0;
+    if ((rc = plan_launch(b, din, b->d_out, nullptr, nullptr, nullptr, s))) return rc;
+    HIP_TRY(hipMemcpyAsync(b->h_out, b->d_out, sizeof(llampc_plan_out), hipMemcpyDeviceToHost, s));
+  }
   b->async_pending = true;
   return LLAMPC_OK;
 }
@@ -677,8 +739,12 @@ int llampc_plan_wait(llampc_bank* b, llampc_plan_out* out) {
   if (!b->async_pending) return fail(LLAMPC_E_STATE, "no async tick outstanding");
   DeviceGuard g(b->device);
   b->async_pending = false;
-  HIP_TRY(hipStreamSynchronize(b->stream));
-  *out = *b->h_out;
+  if (b->async_seq) {
+    if (int rc = wait_host_tag(b, b->async_seq, out)) return rc;
+  } else {
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    *out = *b->h_out;
+  }
   if (out->status) return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", out->status);
   return LLAMPC_OK;
 }

@@ -976,6 +976,11 @@ __device__ __forceinline__ void final_write(const FinalLaunch& f, bool lb, int64
     __hip_atomic_store(&f.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&f.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (f.host_tag) {                     // host completion: every record store performed, then the tag
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(f.host_tag, f.host_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   STAMP(5);
 #ifdef LLAMPC_STAMPS
   if (tid == 0) g_stamp_launch++;
@@ -1162,8 +1167,13 @@ __global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, Lookahe
   if ((int)blockIdx.x < fin.nb_lb) {
     lookback_block(lb, blockIdx.x, sc);
     if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
-    if (fin.full) lb_final(fin, smem);
-    if (fin.poll) {                      // the look-back winner completes the tick
+    if (fin.full) {
+      lb_final(fin, smem);
+      // host completion: lb_final's record stores are performed before any later hand-off
+      // (the final block, possibly another one, publishes the host tag after them)
+      if (fin.host_tag) __threadfence_system();
+    }
+    if (fin.poll) {                   // the look-back winner completes the tick
       __syncthreads();
       final_poll(fin, sc);
       return;

@@ -73,6 +73,12 @@ struct FinalLaunch {
   const uint64_t* la_tag; const uint64_t* blk_tag;
   uint32_t seq;
   int32_t poll;
+  // host completion (llampc_plan / llampc_plan_wait): `out` is then the device alias of a
+  // pinned host record, and the block that completes it stores host_seq to host_tag (pinned,
+  // system scope) after a system-scope fence — the host spins on that word instead of a D2H
+  // copy + stream synchronisation.  Null for device-resident ticks.
+  uint64_t* host_tag;
+  uint64_t host_seq;
 };
 
 int lookback_blocks(int64_t n);

@@ -612,6 +612,58 @@ def test_polled_completion_equals_ticket_completion(nat):
             b_bank.close()
 
 
+def _same_records(o, w):
+    from llampc import _native
+    A, B = _native.plan_out_to_dict(o), _native.plan_out_to_dict(w)
+    assert A["status"] == 0 and B["status"] == 0
+    for k in A:
+        if isinstance(A[k], np.ndarray):
+            np.testing.assert_array_equal(A[k], B[k], err_msg=k)
+        else:
+            assert A[k] == B[k] or (A[k] != A[k] and B[k] != B[k]), (k, A[k], B[k])
+
+
+def test_host_completion_equals_copy_completion(nat):
+    """Host completion (the kernel writes the record into pinned host memory, then a tag the
+    host spins on) returns the same records as the D2H copy + stream-synchronise path
+    (LLAMPC_SYNC_COMPLETION=1): polled and ticket (LLAMPC_NO_POLL=1) completions, look-back-
+    only and look-ahead-only ticks, and llampc_plan_async / llampc_plan_wait."""
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    H, W, C, N = 20, 3, 3, 3000
+    rng = np.random.RandomState(11)
+    banks = [ModelBank(generate_bank(N, seed=4), W=W, device=0) for _ in range(4)]
+    # bank 0: host completion, polled; 1: copy path; 2: host completion, ticket path;
+    # 3: host completion through plan_async / plan_wait
+    modes = [{}, {"LLAMPC_SYNC_COMPLETION": "1"}, {"LLAMPC_NO_POLL": "1"}, {}]
+    try:
+        for t in range(1, W + 4):
+            U = np.repeat(u[:, t:t + H].T[None], C, axis=0)
+            U[1:] += rng.uniform(-0.02, 0.02, U[1:].shape)
+            xref = s[:2, t:t + H + 1]
+            args = (s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1])
+            kw = dict(K=4, current_model=2,
+                      do_lookahead=(t != 2), do_lookback=(t != 3))   # one lb-only, one la-only tick
+            outs = []
+            for i, (b, env) in enumerate(zip(banks, modes)):
+                os.environ.update(env)
+                try:
+                    if i == 3:
+                        b.plan_async(*args, **kw)
+                        outs.append(b.plan_wait())
+                    else:
+                        outs.append(b.plan_raw(*args, **kw)[0])
+                finally:
+                    for k in env:
+                        del os.environ[k]
+            for o in outs[:1] + outs[2:]:
+                _same_records(o, outs[1])
+    finally:
+        for b in banks:
+            b.close()
+
+
 def test_setupnlp_solve_sampling(nat):
     """setupNLP.solve drop-in (sampling over the NLP transcription on the GPU): the returned
     (umpc, fval, xmpc) are consistent with the oracle's NLP restatement — xmpc is the Euler
