@@ -326,7 +326,7 @@ def extras(args, sb, stream, world, rank=0):
         lat = np.array(lat[50:]) * 1e6
         out["sync_plan_latency_us"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                        "ticks": int(lat.size),
-                                       "note": "host-pointer llampc_plan from Python: H2D copy + kernel, record via pinned host memory + completion-tag spin"}
+                                       "note": "host-pointer llampc_plan from Python: inputs as kernel arguments, record via pinned host memory + completion-tag spin"}
         out["config5"] = concurrent_tracks(args)
     return out
 
@@ -334,7 +334,7 @@ def extras(args, sb, stream, world, rank=0):
 def concurrent_tracks(args, ticks=1000, warm=50):
     """BASELINE config 5 on one GPU: ETHZ and ETHZMobil banks (N_per_gpu each, H=40) ticked
     concurrently every control step — llampc_plan_async on both, then llampc_plan_wait on
-    both (host pointers: H2D copy + kernel + the record through pinned host memory) — p50/p99 of the per-step latency
+    both (host pointers: inputs as kernel arguments, the record through pinned host memory) — p50/p99 of the per-step latency
     against the 1 kHz budget (1 ms)."""
     from llampc.mpc import ModelBank, generate_bank
     H, W, K = 40, args.W, args.K
@@ -364,7 +364,7 @@ def concurrent_tracks(args, ticks=1000, warm=50):
             "budget_us": 1000.0, "met": p99 <= 1000.0, "N_per_track": args.n_per_gpu, "H": H,
             "sel_models": [int(o.sel_model) for o in outs],
             "note": "two independent plan() instances per control step (ETHZ + ETHZMobil), "
-                    "async on two streams, host pointers incl. H2D copy and the record read back"}
+                    "async on two streams, host pointers in and the record read back"}
 
 
 def issue_roofline(n, C, H, lpm, ms):

@@ -263,7 +263,7 @@ void timing_free(llampc_bank* b) {
 // Advances the window bookkeeping when a look-back runs.
 int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out, double* d_err,
                 double* d_wmean, double* d_cost, hipStream_t s, uint64_t* host_tag = nullptr,
-                uint64_t host_seq = 0) {
+                uint64_t host_seq = 0, const InlinePack* pk = nullptr) {
   if (int rc = ensure_xref_pm(b, &in)) return rc;
   const bool lb = in.do_lookback != 0;
   const bool la = in.do_lookahead != 0;
@@ -368,7 +368,7 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   }
   {
     TimedLaunch tl(b, 0, s);
-    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s));
+    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s, pk));
   }
   if (lb) {
     b->slot = (slot + 1) % b->W;
@@ -377,13 +377,14 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   return LLAMPC_OK;
 }
 
-// Pack a host plan input into the pinned buffer; return a device-pointer copy of `in`.
-int stage_inputs(llampc_bank* b, const llampc_plan_in* in, llampc_plan_in* dev_in, hipStream_t s) {
+// Doubles of the packed inputs: x_prev[6] u_prev[2] x_now[6] uprev[2] xref[2][H+1] U[C][H][2].
+size_t pack_len(const llampc_plan_in* in) {
   const int64_t H = in->do_lookahead ? in->H : 0, C = in->do_lookahead ? in->C : 0;
-  const size_t total = 16 + 2 * (H + 1) + 2 * C * H;
-  int rc = ensure_in(b, total);
-  if (rc) return rc;
-  double* h = b->h_in;
+  return 16 + 2 * (H + 1) + 2 * C * H;
+}
+
+void pack_into(const llampc_plan_in* in, double* h) {
+  const int64_t H = in->do_lookahead ? in->H : 0, C = in->do_lookahead ? in->C : 0;
   std::memset(h, 0, 16 * sizeof(double));
   if (in->x_prev) std::memcpy(h + 0, in->x_prev, 6 * sizeof(double));
   if (in->u_prev) std::memcpy(h + 6, in->u_prev, 2 * sizeof(double));
@@ -398,6 +399,23 @@ int stage_inputs(llampc_bank* b, const llampc_plan_in* in, llampc_plan_in* dev_i
     }
     std::memcpy(h + 16 + 2 * (H + 1), in->U, 2 * C * H * sizeof(double));
   }
+}
+
+// Host ticks whose inputs travel as kernel arguments (InlinePack): no H2D copy.
+// LLAMPC_NO_INLINE=1 keeps the copy (A/B runs).
+bool inline_inputs(const llampc_plan_in* in) {
+  return in->do_lookahead && plan_inline_ok(in->C, in->H, in->integrator, in->xref_mode) &&
+         getenv("LLAMPC_NO_INLINE") == nullptr;
+}
+
+// Pack a host plan input into the pinned buffer; return a device-pointer copy of `in`.
+int stage_inputs(llampc_bank* b, const llampc_plan_in* in, llampc_plan_in* dev_in, hipStream_t s) {
+  const size_t total = pack_len(in);
+  const int64_t H = in->do_lookahead ? in->H : 0;
+  int rc = ensure_in(b, total);
+  if (rc) return rc;
+  double* h = b->h_in;
+  pack_into(in, h);
   HIP_TRY(hipMemcpyAsync(b->d_in, h, total * sizeof(double), hipMemcpyHostToDevice, s));
   *dev_in = *in;
   double* d = b->d_in;
@@ -654,16 +672,22 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
   DeviceGuard g(b->device);
   hipStream_t s = b->stream;
   if (cost_out && in->do_lookahead && (rc = ensure_cost(b, (size_t)b->n * in->C))) return rc;
-  llampc_plan_in din;
-  if ((rc = stage_inputs(b, in, &din, s))) return rc;
   if (!err_out && !wmean_out && !cost_out && host_completion(b)) {
     // the record only: the kernel writes it to pinned host memory and publishes a tag
+    llampc_plan_in din = *in;
+    InlinePack pk;
+    const bool inl = inline_inputs(in);
+    if (inl) pack_into(in, pk.v);
+    else if ((rc = stage_inputs(b, in, &din, s))) return rc;
     const uint64_t seq = ++b->hseq;
-    if ((rc = plan_launch(b, din, b->d_rec, nullptr, nullptr, nullptr, s, b->d_tag, seq))) return rc;
+    if ((rc = plan_launch(b, din, b->d_rec, nullptr, nullptr, nullptr, s, b->d_tag, seq, inl ? &pk : nullptr)))
+      return rc;
     if ((rc = wait_host_tag(b, seq, out))) return rc;
     if (out->status) return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", out->status);
     return LLAMPC_OK;
   }
+  llampc_plan_in din;
+  if ((rc = stage_inputs(b, in, &din, s))) return rc;
   double* d_cost = (cost_out && in->do_lookahead) ? b->d_cost : nullptr;
   if ((rc = plan_launch(b, din, b->d_out, err_out ? b->d_err : nullptr,
                         wmean_out ? b->d_wmean : nullptr, d_cost, s)))
@@ -719,12 +743,18 @@ int llampc_plan_async(llampc_bank* b, const llampc_plan_in* in) {
   if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
   DeviceGuard g(b->device);
   hipStream_t s = b->stream;
-  llampc_plan_in din;
-  if ((rc = stage_inputs(b, in, &din, s))) return rc;
+  llampc_plan_in din = *in;
   if (host_completion(b)) {
+    InlinePack pk;
+    const bool inl = inline_inputs(in);
+    if (inl) pack_into(in, pk.v);
+    else if ((rc = stage_inputs(b, in, &din, s))) return rc;
     b->async_seq = ++b->hseq;
-    if ((rc = plan_launch(b, din, b->d_rec, nullptr, nullptr, nullptr, s, b->d_tag, b->async_seq))) return rc;
+    if ((rc = plan_launch(b, din, b->d_rec, nullptr, nullptr, nullptr, s, b->d_tag, b->async_seq,
+                          inl ? &pk : nullptr)))
+      return rc;
   } else {
+    if ((rc = stage_inputs(b, in, &din, s))) return rc;
     b->async_seq = 0;
     if ((rc = plan_launch(b, din, b->d_out, nullptr, nullptr, nullptr, s))) return rc;
     HIP_TRY(hipMemcpyAsync(b->h_out, b->d_out, sizeof(llampc_plan_out), hipMemcpyDeviceToHost, s));

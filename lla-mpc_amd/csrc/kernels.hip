@@ -1159,8 +1159,8 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
 // llampc_plan_out record (final_select).
 // ------------------------------------------------------------------------------------
 template <int INTEG, bool STAGE, int LPM, int XM>
-__global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
-                                                      FinalLaunch fin, int G, int cpl) {
+__device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const LookaheadLaunch& la,
+                                          const FinalLaunch& fin, int G, int cpl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Scratch sc(smem);
   int* flag = reinterpret_cast<int*>(smem + 144);
@@ -1185,6 +1185,29 @@ __global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, Lookahe
   const unsigned expected = (unsigned)fin.nb_la + (fin.nb_lb > 0 ? 1u : 0u);
   if (!ticket_last(&fin.tickets[1], expected, flag)) return;
   final_select(fin, sc);
+}
+
+template <int INTEG, bool STAGE, int LPM, int XM>
+__global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
+                                                      FinalLaunch fin, int G, int cpl) {
+  plan_body<INTEG, STAGE, LPM, XM>(lb, la, fin, G, cpl);
+}
+
+// The same tick with its inputs in the kernarg segment (InlinePack): the pointers are set to
+// the pack's fields, read by flat loads like any other input (no H2D copy on the host path).
+template <int LPM>
+__global__ __launch_bounds__(kBlock) void plan_kernel_inl(LookbackLaunch lb, LookaheadLaunch la,
+                                                          FinalLaunch fin, int G, int cpl,
+                                                          InlinePack pk) {
+  const double* v = pk.v;
+  lb.x_prev = v;
+  lb.u_prev = v + 6;
+  lb.x_now = v + 8;
+  la.x0 = v + 8;
+  la.uprev = v + 14;
+  la.xref = v + 16;
+  la.U = v + 16 + 2 * (la.H + 1);
+  plan_body<0, true, LPM, 0>(lb, la, fin, G, cpl);
 }
 
 // Cross-shard merge after the all-gather: one wave.  Scalars by lane-parallel reads and
@@ -1478,6 +1501,23 @@ static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, c
   }
 }
 
+template <int LPM>
+static void launch_plan_inl(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
+                            int G, int cpl, size_t lds, hipStream_t s, const InlinePack& pk) {
+  lds = std::max(lds, kOneBlockPerCuLds);
+  allow_lds(plan_kernel_inl<LPM>);
+  hipLaunchKernelGGL((plan_kernel_inl<LPM>), dim3(f.nb_lb + f.nb_la), dim3(kBlock), lds, s, lb, la, f,
+                     G, cpl, pk);
+}
+
+bool plan_inline_ok(int32_t C, int32_t H, int32_t integrator, int32_t xref_mode) {
+  if (integrator != LLAMPC_RK4 || xref_mode != LLAMPC_XREF_GIVEN || C < 1 || H < 1) return false;
+  if (16 + 2 * ((int64_t)H + 1) + 2 * (int64_t)C * H > kInlineDoubles) return false;
+  bool stage = false;
+  (void)lookahead_lds_bytes(C, H, &stage);
+  return stage;
+}
+
 template <int INTEG, bool STAGE>
 static void launch_plan_l(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
                           int G, int cpl, int lpm, size_t lds, hipStream_t s) {
@@ -1487,7 +1527,7 @@ static void launch_plan_l(const LookbackLaunch& lb, const LookaheadLaunch& la, c
 }
 
 hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
-                       hipStream_t s) {
+                       hipStream_t s, const InlinePack* pk) {
   LookbackLaunch lbv{};
   LookaheadLaunch lav{};
   int G = 1, cpl = 1, lpm = 1, integ = LLAMPC_RK4;
@@ -1521,6 +1561,13 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
   f.do_lb = lb != nullptr;
   f.do_la = la != nullptr;
   if (f.nb_lb + f.nb_la == 0) return hipErrorInvalidValue;
+  if (pk) {
+    if (!la || !plan_inline_ok(la->C, la->H, integ, la->xref_mode) || !stage) return hipErrorInvalidValue;
+    if (lpm == 4) launch_plan_inl<4>(lbv, lav, f, G, cpl, lds, s, *pk);
+    else if (lpm == 2) launch_plan_inl<2>(lbv, lav, f, G, cpl, lds, s, *pk);
+    else launch_plan_inl<1>(lbv, lav, f, G, cpl, lds, s, *pk);
+    return hipGetLastError();
+  }
   switch (integ) {
     case LLAMPC_RK4:
       if (stage) launch_plan_l<0, true>(lbv, lav, f, G, cpl, lpm, lds, s);

@@ -81,6 +81,14 @@ struct FinalLaunch {
   uint64_t host_seq;
 };
 
+// Tick inputs in the kernarg segment (host-pointer ticks whose pack fits): x_prev[6],
+// u_prev[2], x_now[6], uprev[2], xref[2][H+1], U[C][H][2] — the layout of the H2D pack.  The
+// runtime copies kernargs as part of the launch, so such a tick needs no H2D copy.
+constexpr int kInlineDoubles = 352;
+struct InlinePack {
+  double v[kInlineDoubles];
+};
+
 int lookback_blocks(int64_t n);
 int lookahead_group(int32_t C);
 int lookahead_lpm(int64_t n, int32_t C, int32_t integrator);
@@ -90,8 +98,11 @@ size_t raceline_lds_bytes(int32_t n);
 
 // The whole tick in ONE launch: look-back blocks (if lb), look-ahead blocks (if la), and
 // the completion stages run by ticket winners; writes f.out.  f.nb_* / f.do_* are set here.
+// pk != null: the inputs are in *pk (see InlinePack); needs a look-ahead with RK4, the
+// given xref and U staged in LDS (plan_inline_ok), else hipErrorInvalidValue.
 hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
-                       hipStream_t s);
+                       hipStream_t s, const InlinePack* pk = nullptr);
+bool plan_inline_ok(int32_t C, int32_t H, int32_t integrator, int32_t xref_mode);
 hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
                         llampc_plan_out* merged, hipStream_t s);
 hipError_t launch_dynamics(int32_t op, const double* x, const double* u, const double* params,

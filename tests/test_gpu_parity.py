@@ -625,18 +625,20 @@ def _same_records(o, w):
 
 def test_host_completion_equals_copy_completion(nat):
     """Host completion (the kernel writes the record into pinned host memory, then a tag the
-    host spins on) returns the same records as the D2H copy + stream-synchronise path
-    (LLAMPC_SYNC_COMPLETION=1): polled and ticket (LLAMPC_NO_POLL=1) completions, look-back-
-    only and look-ahead-only ticks, and llampc_plan_async / llampc_plan_wait."""
+    host spins on) and inputs passed as kernel arguments return the same records as the
+    H2D/D2H copy + stream-synchronise path (LLAMPC_SYNC_COMPLETION=1): polled and ticket
+    (LLAMPC_NO_POLL=1) completions, look-back-only and look-ahead-only ticks,
+    llampc_plan_async / llampc_plan_wait, and the H2D input copy (LLAMPC_NO_INLINE=1)."""
     from llampc.mpc import ModelBank, generate_bank
     d = golden("dyn_slice.npz")
     s, u = d["states"], d["inputs"]
     H, W, C, N = 20, 3, 3, 3000
     rng = np.random.RandomState(11)
-    banks = [ModelBank(generate_bank(N, seed=4), W=W, device=0) for _ in range(4)]
-    # bank 0: host completion, polled; 1: copy path; 2: host completion, ticket path;
-    # 3: host completion through plan_async / plan_wait
-    modes = [{}, {"LLAMPC_SYNC_COMPLETION": "1"}, {"LLAMPC_NO_POLL": "1"}, {}]
+    banks = [ModelBank(generate_bank(N, seed=4), W=W, device=0) for _ in range(5)]
+    # bank 0: host completion, polled, inputs as kernel arguments; 1: H2D + D2H copies and a
+    # stream synchronise; 2: host completion, ticket path; 3: host completion through
+    # plan_async / plan_wait; 4: host completion with the H2D input copy
+    modes = [{}, {"LLAMPC_SYNC_COMPLETION": "1"}, {"LLAMPC_NO_POLL": "1"}, {}, {"LLAMPC_NO_INLINE": "1"}]
     try:
         for t in range(1, W + 4):
             U = np.repeat(u[:, t:t + H].T[None], C, axis=0)
