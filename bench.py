@@ -191,9 +191,10 @@ def main():
     ticks = make_ticks(args, T)
     dev = torch.device("cuda", local)
     packs = torch.from_numpy(ticks).to(dev)                 # resident tick inputs [T, L]
+    torch.cuda.synchronize()
     bank_global = generate_bank(N_total, seed=0 if args.track == "ETHZ" else 1)
     sb = ShardedBank(bank_global, rank, world, local, W=W)
-    stream = torch.cuda.current_stream(dev)
+    stream = sb.stream                  # plan, all-gather and merge: one stream (the bank's)
     pins = [sb.make_plan_in(packs[i], C, H, K=K, current_model=0) for i in range(T)]
     lib = nat.load()
 
@@ -204,8 +205,11 @@ def main():
         step(i)
     if not args.no_timing:
         # event pairs bracket groups of TIMING_STRIDE consecutive launches of the timed loop:
-        # the kernel's mean duration measured live, the events' own cost spread over a group
-        nat.check(lib.llampc_bank_timing(sb.bank.handle, TIMING_STRIDE, args.steps // TIMING_STRIDE + 8))
+        # the kernel's mean duration measured live, the events' own cost spread over a group.
+        # With the exchange, a group would also hold the all-gathers and merges in between,
+        # so every plan launch gets its own pair (reads ~2 us high: the events' own cost)
+        stride = 1 if sb.exchange else TIMING_STRIDE
+        nat.check(lib.llampc_bank_timing(sb.bank.handle, stride, args.steps // stride + 8))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -270,7 +274,11 @@ def main():
                      "flops_per_model_step": FLOPS_PER_MODEL_STEP,
                      "note": "plain flops only; the 29 fp64 transcendentals per RK4 step are excluded"},
             "issue": issue_roofline(N_local, C, H, lpm_of(N_local, C), plan_ms),
-            "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0])},
+            "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0]),
+                          "bracket": "one plan launch per event pair" if sb.exchange else
+                                     f"groups of {TIMING_STRIDE} consecutive plan launches"},
+            "exchange": (("native RCCL all-gather on the tick stream (llampc_exchange_device)" if sb._comm is not None
+                          else f"c10d all_gather_into_tensor ({sb.backend})") + " + merge_kernel") if sb.exchange else None,
             "host_issue_us_per_step": t_issue / args.steps * 1e6,
             "lpm": lpm_of(N_local, C),
             "result_check": {"sel_model": merged.best_model, "window_full": merged.window_full,
@@ -298,6 +306,7 @@ def extras(args, sb, stream, world, rank=0):
     a2.C = 64
     t64 = make_ticks(a2, 8)
     p64 = torch.from_numpy(t64).to(torch.device("cuda", sb.device))
+    torch.cuda.synchronize()
     pins = [sb.make_plan_in(p64[i], 64, H, K=args.K) for i in range(8)]
     for i in range(5):
         sb.launch(pins[i % 8], stream)

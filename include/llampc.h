@@ -226,6 +226,16 @@ int llampc_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_policy,
                  llampc_plan_out* merged);
 int llampc_merge_device(const void* d_parts, int32_t G, int32_t nan_policy, void* d_merged,
                         int32_t device, void* stream);
+/* The per-tick exchange of the sharded bank, enqueued on `stream` (hipStream_t) with no
+ * host round trip: an RCCL all-gather of this rank's record d_local (one llampc_plan_out)
+ * into d_all [world] over `comm`, then merge_kernel into d_merged.  comm is an ncclComm_t
+ * (e.g. a torch ProcessGroupNCCL communicator: backend._comm_ptr()); allgather_fn is the
+ * address of ncclAllGather in the RCCL library the process already loaded, so this library
+ * neither links nor initialises a second RCCL.  Replaces the reference-side gather that
+ * SURVEY.md §8e specifies (the reference itself is single-process). */
+int llampc_exchange_device(const void* d_local, void* d_all, int32_t world, void* d_merged,
+                           int32_t nan_policy, void* comm, void* allgather_fn, int32_t device,
+                           void* stream);
 
 /* ---- raw batched dynamics (Dynamic API parity) ---------------------------------- */
 /* x [n][6], u [n][2]; params [6][P] with P == 1 (one model broadcast) or P == n.

@@ -866,6 +866,25 @@ int llampc_merge_device(const void* d_parts, int32_t G, int32_t nan_policy, void
   return LLAMPC_OK;
 }
 
+// ncclAllGather(sendbuff, recvbuff, sendcount, datatype, comm, stream) (rccl.h); datatype
+// ncclUint8 = 1, ncclSuccess = 0.  Called through the process's own RCCL (see llampc.h).
+typedef int (*AllGatherFn)(const void*, void*, size_t, int, void*, hipStream_t);
+
+int llampc_exchange_device(const void* d_local, void* d_all, int32_t world, void* d_merged,
+                           int32_t nan_policy, void* comm, void* allgather_fn, int32_t device,
+                           void* stream) {
+  if (!d_local || !d_all || !d_merged || !comm || !allgather_fn || world < 1 || world > 32)
+    return fail(LLAMPC_E_ARG, "bad exchange arguments (world=%d, 1..32)", world);
+  DeviceGuard g(device);
+  if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", device);
+  const int r = reinterpret_cast<AllGatherFn>(allgather_fn)(d_local, d_all, sizeof(llampc_plan_out), 1,
+                                                            comm, (hipStream_t)stream);
+  if (r != 0) return fail(LLAMPC_E_HIP, "ncclAllGather failed: ncclResult %d", r);
+  HIP_TRY(launch_merge((const llampc_plan_out*)d_all, world, nan_policy == LLAMPC_NAN_FIRST,
+                       (llampc_plan_out*)d_merged, (hipStream_t)stream));
+  return LLAMPC_OK;
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------------------------

@@ -101,6 +101,8 @@ _SIGNATURES = {
     "llampc_merge": (C.c_int, [C.POINTER(PlanOut), C.c_int32, C.c_int32, C.POINTER(PlanOut)]),
     "llampc_merge_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
                                       C.c_void_p]),
+    "llampc_exchange_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                                         C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "llampc_dynamics_batch": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                         C.POINTER(Vehicle), C.c_int64, C.c_void_p, C.c_int32,
                                         C.c_int32, C.c_void_p]),

@@ -13,6 +13,7 @@ same merge code runs on the host (llampc_merge).
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -27,6 +28,20 @@ def _bytes_of(o: nat.PlanOut) -> np.ndarray:
 
 def _out_of(b: np.ndarray) -> nat.PlanOut:
     return nat.PlanOut.from_buffer_copy(np.ascontiguousarray(b, dtype=np.uint8).tobytes())
+
+
+def _rccl_allgather_addr() -> int:
+    """Address of ncclAllGather in the RCCL this process already loaded (torch's), found in
+    /proc/self/maps: llampc_exchange_device calls it, so no second RCCL is loaded."""
+    path = None
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "librccl" in line:
+                path = line.split()[-1]
+                break
+    if path is None:
+        raise nat.NativeError("no RCCL library loaded in this process")
+    return C.cast(C.CDLL(path).ncclAllGather, C.c_void_p).value
 
 
 def gather_merge_host(local: nat.PlanOut, group=None, nan_policy=nat.NAN_FIRST) -> nat.PlanOut:
@@ -67,6 +82,35 @@ class ShardedBank:
         self.d_merged = torch.empty(B, dtype=torch.uint8, device=dev) if self.exchange else self.d_local
         self.h_merged = torch.empty(B, dtype=torch.uint8).pin_memory()
         self._inputs = None
+        # every stage of the tick (input upload, plan, all-gather, merge, read-back) runs on
+        # ONE stream, which is also the bank's: torch's default stream has handle 0, which the
+        # C ABI reads as "the bank's own stream", so it is never used to launch a tick
+        self.stream = torch.cuda.Stream(device=dev)
+        self.bank.set_stream(self.stream.cuda_stream)
+        # native exchange (nccl): the all-gather is issued by llampc_exchange_device straight
+        # on the tick's stream, over the communicator of a group of its own — no c10d stream
+        # hand-off, ~1 us of host time per tick.  LLAMPC_C10D_EXCHANGE=1 keeps the c10d call.
+        self._comm = None
+        if self.exchange and self.backend == "nccl" and not os.environ.get("LLAMPC_C10D_EXCHANGE"):
+            self._setup_native_exchange(dev)
+
+    def _setup_native_exchange(self, dev):
+        import sys
+        import torch
+        import torch.distributed as dist
+        xg = dist.new_group(backend="nccl")        # collective: every rank builds its shard
+        # one c10d collective creates the group's communicator before its raw use
+        dist.all_gather_into_tensor(self.d_all, self.d_local, group=xg)
+        torch.cuda.synchronize(dev)
+        try:
+            comm = xg._get_backend(dev)._comm_ptr()
+            fn = _rccl_allgather_addr()
+        except Exception as e:                     # transport only: results are the same
+            print(f"llampc: native exchange unavailable ({e}); using the c10d all-gather",
+                  file=sys.stderr)
+            return
+        if comm:
+            self._xgroup, self._comm, self._allgather = xg, comm, fn
 
     def stage(self, x_prev, u_prev, x_now, U, xref, uprev) -> dict:
         """Upload one tick's inputs into a device pack (kept resident by the caller)."""
@@ -80,8 +124,16 @@ class ShardedBank:
                                np.asarray(x_now, dtype=np.float64).ravel(),
                                np.asarray(uprev, dtype=np.float64).ravel(),
                                np.asarray(xref, dtype=np.float64).ravel(), U.ravel()])
-        d = torch.from_numpy(pack).to(torch.device("cuda", self.device))
+        with torch.cuda.stream(self.stream):
+            d = torch.from_numpy(pack).to(torch.device("cuda", self.device))
         return dict(pack=d, C=C_, H=H, U=U)
+
+    def tick_stream(self, stream=None):
+        """The stream a tick runs on: ``stream`` if it is a non-default torch stream, else
+        this shard's own stream (self.stream)."""
+        if stream is None or stream.cuda_stream == 0:
+            return self.stream
+        return stream
 
     def make_plan_in(self, pack, C_, H, Ts=0.02, K=10, integrator="rk4", current_model=0,
                      do_lookback=True, nan_policy=nat.NAN_FIRST, cost=None) -> nat.PlanIn:
@@ -104,15 +156,19 @@ class ShardedBank:
         return pin
 
     def launch(self, pin: nat.PlanIn, stream=None):
-        """Enqueue one tick on ``stream`` (torch current stream by default): fused plan on
-        this shard, then (world > 1) ONE all-gather of the shard records and the on-device
-        merge.  The merged record is left in ``self.d_merged``; nothing synchronises."""
+        """Enqueue one tick on ``tick_stream(stream)``: fused plan on this shard, then (world
+        > 1) ONE all-gather of the shard records and the on-device merge, all stream-ordered.
+        The merged record is left in ``self.d_merged``; nothing synchronises."""
         torch = self._torch
-        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        s = self.tick_stream(stream)
         lib = nat.load()
         nat.check(lib.llampc_plan_device(self.bank.handle, C.byref(pin), self.d_local.data_ptr(),
                                          None, None, None, s.cuda_stream))
-        if self.exchange:
+        if self._comm is not None:           # native: all-gather + merge on stream s
+            nat.check(lib.llampc_exchange_device(self.d_local.data_ptr(), self.d_all.data_ptr(), self.world,
+                                                 self.d_merged.data_ptr(), pin.nan_policy, self._comm,
+                                                 self._allgather, self.device, s.cuda_stream))
+        elif self.exchange:
             import torch.distributed as dist
             if self.backend == "nccl":
                 with torch.cuda.stream(s):
@@ -136,7 +192,7 @@ class ShardedBank:
 
     def fetch(self, stream=None, U=None) -> PlanResult:
         torch = self._torch
-        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        s = self.tick_stream(stream)
         with torch.cuda.stream(s):
             self.h_merged.copy_(self.d_merged, non_blocking=True)
         s.synchronize()

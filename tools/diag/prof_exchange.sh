@@ -13,8 +13,20 @@ python3 - "$tag" <<'PY'
 import csv, sys
 tag = sys.argv[1]
 rows = list(csv.DictReader(open(f"gpurun_out/profx_{tag}/run_kernel_trace.csv")))
-for name in ("plan_kernel", "merge_kernel"):
-    d = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000 for r in rows if name in r["Kernel_Name"])
-    if d:
-        print(f"{tag} {name}: n={len(d)} min {d[0]:.2f} median {d[len(d)//2]:.2f} p90 {d[int(len(d)*0.9)]:.2f} us")
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+def short(n):
+    return "plan" if "plan_kernel" in n else "merge" if "merge_kernel" in n else ("rccl" if "ncclDevKernel" in n or "nccl" in n.lower() else n[:40])
+seq = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
+dur, gap = {}, {}
+for i, (n, a, b) in enumerate(seq):
+    dur.setdefault(n, []).append((b - a) / 1000)
+    if i:
+        p = seq[i - 1]
+        gap.setdefault(f"{p[0]}->{n}", []).append((a - p[2]) / 1000)
+med = lambda v: sorted(v)[len(v) // 2]
+for n, v in dur.items():
+    print(f"{tag} {n}: n={len(v)} median {med(v):.2f} us")
+for n, v in gap.items():
+    if len(v) > 20:
+        print(f"{tag} gap {n}: n={len(v)} median {med(v):.2f} us")
 PY

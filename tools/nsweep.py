@@ -45,12 +45,13 @@ def main():
     ticks = bench.make_ticks(targs, 16)
     dev = torch.device("cuda", 0)
     packs = torch.from_numpy(ticks).to(dev)
+    torch.cuda.synchronize()
     H, C = args.H, args.C
     for N in args.n:
         bank = generate_bank(N, seed=0)
         sb = ShardedBank(bank, 0, 1, 0, W=args.W)
         pins = [sb.make_plan_in(packs[i], C, H, K=min(args.K, N)) for i in range(len(ticks))]
-        s = torch.cuda.current_stream(dev)
+        s = sb.stream
         for i in range(args.warmup):
             sb.launch(pins[i % len(pins)], s)
         torch.cuda.synchronize()
