@@ -38,7 +38,7 @@ FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation
 # Issue roofline: instructions per rollout step of the fast look-ahead loop, per lane, by lane
 # split (tools/diag/isa_counts.py on the current sources), and the chip's fp64 VALU issue
 # capacity: 1,024 SIMDs x 16 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md max clock).
-ISSUE_INSTR_PER_STEP = {4: 575, 2: 664, 1: 1033}
+ISSUE_INSTR_PER_STEP = {4: 559, 2: 664, 1: 1032}
 ISSUE_PEAK_LANE_INSTR = 1024 * 16 * 2.4e9
 
 
@@ -207,9 +207,11 @@ def main():
         # event pairs bracket groups of TIMING_STRIDE consecutive launches of the timed loop:
         # the kernel's mean duration measured live, the events' own cost spread over a group.
         # With the exchange, a group would also hold the all-gathers and merges in between,
-        # so every plan launch gets its own pair (reads ~2 us high: the events' own cost)
-        stride = 1 if sb.exchange else TIMING_STRIDE
-        nat.check(lib.llampc_bank_timing(sb.bank.handle, stride, args.steps // stride + 8))
+        # so ONE plan launch in every TIMING_STRIDE gets its own pair (negative stride =
+        # sampling; the bracketed launch reads ~2 us high, the events' own cost, and only
+        # 1/TIMING_STRIDE of the timed ticks carry events)
+        stride = -TIMING_STRIDE if sb.exchange else TIMING_STRIDE
+        nat.check(lib.llampc_bank_timing(sb.bank.handle, stride, args.steps // abs(stride) + 8))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -275,7 +277,7 @@ def main():
                      "note": "plain flops only; the 29 fp64 transcendentals per RK4 step are excluded"},
             "issue": issue_roofline(N_local, C, H, lpm_of(N_local, C), plan_ms),
             "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0]),
-                          "bracket": "one plan launch per event pair" if sb.exchange else
+                          "bracket": f"one plan launch in every {TIMING_STRIDE} per event pair" if sb.exchange else
                                      f"groups of {TIMING_STRIDE} consecutive plan launches"},
             "exchange": (("native RCCL all-gather on the tick stream (llampc_exchange_device)" if sb._comm is not None
                           else f"c10d all_gather_into_tensor ({sb.backend})") + " + merge_kernel") if sb.exchange else None,

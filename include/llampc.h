@@ -165,7 +165,10 @@ int llampc_bank_set_stream(llampc_bank* bank, void* stream);
  * benchmark's roofline).  enable=k >= 1 arms `max_launches` event pairs; each pair brackets
  * a group of k consecutive launches of the plan kernel (the whole tick: look-back +
  * look-ahead + selection), so the mean launch duration is elapsed / k (k > 1 spreads the
- * events' own cost over the group); enable=0 disarms.  count = launches timed. */
+ * events' own cost over the group); enable=-k (k >= 1) brackets ONE launch out of every k
+ * (sampling: for ticks whose launches are separated by other work on the stream, e.g. the
+ * multi-GPU exchange, with the events' cost on 1/k of the ticks); enable=0 disarms.
+ * count = launches timed. */
 int llampc_bank_timing(llampc_bank* bank, int32_t enable, int32_t max_launches);
 /* Synchronises, returns avg_ms[3] and count[3] for {plan kernel, reserved, reserved}
  * since the last read, and re-arms the counters. */

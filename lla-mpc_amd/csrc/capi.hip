@@ -137,7 +137,8 @@ struct llampc_bank {
   std::vector<hipEvent_t> ev[3];
   size_t ev_used[3] = {0, 0, 0};
   bool timing = false;
-  int64_t timing_stride = 1;       // bracket every stride-th launch
+  int64_t timing_stride = 1;       // group of stride launches per pair (or sampling period)
+  bool timing_sample = false;      // pair around one launch of every stride
   bool async_pending = false;      // llampc_plan_async issued, llampc_plan_wait not yet
   double* d_rl = nullptr;          // raceline table: knots | xy | speed | mus
   int32_t rl_n = 0, rl_M = 0;
@@ -238,7 +239,8 @@ struct TimedLaunch {
     const int64_t pos = b->timing_seen[k]++ % b->timing_stride;
     const size_t i = b->ev_used[k];
     if (pos == 0) (void)hipEventRecord(b->ev[k][2 * i], s);
-    if (pos == b->timing_stride - 1) stop = b->ev[k][2 * i + 1];
+    // sampling: the pair brackets the period's first launch alone
+    if (pos == (b->timing_sample ? 0 : b->timing_stride - 1)) stop = b->ev[k][2 * i + 1];
   }
   ~TimedLaunch() {
     if (stop) {
@@ -257,6 +259,7 @@ void timing_free(llampc_bank* b) {
   for (int64_t& u : b->timing_seen) u = 0;
   b->timing = false;
   b->timing_stride = 1;
+  b->timing_sample = false;
 }
 
 // The tick on device pointers: ONE launch (look-back + look-ahead + completion).
@@ -631,14 +634,15 @@ int llampc_bank_timing(llampc_bank* b, int32_t enable, int32_t max_launches) {
   HIP_TRY(hipStreamSynchronize(b->stream));
   timing_free(b);
   if (!enable) return LLAMPC_OK;
-  if (enable < 0) return fail(LLAMPC_E_ARG, "enable must be >= 0");
+  if (enable == INT32_MIN) return fail(LLAMPC_E_ARG, "bad enable");
   if (max_launches < 1) return fail(LLAMPC_E_ARG, "max_launches must be >= 1");
   for (auto& v : b->ev) {
     v.resize(2 * (size_t)max_launches, nullptr);
     for (hipEvent_t& e : v) HIP_TRY(hipEventCreate(&e));
   }
   b->timing = true;
-  b->timing_stride = enable;
+  b->timing_stride = enable < 0 ? -(int64_t)enable : enable;
+  b->timing_sample = enable < 0;
   return LLAMPC_OK;
 }
 
@@ -654,8 +658,9 @@ int llampc_bank_timing_read(llampc_bank* b, double* avg_ms, int64_t* count) {
       HIP_TRY(hipEventElapsedTime(&ms, b->ev[k][2 * i], b->ev[k][2 * i + 1]));
       tot += ms;
     }
-    count[k] = (int64_t)b->ev_used[k] * b->timing_stride;
-    avg_ms[k] = b->ev_used[k] ? tot / ((double)b->ev_used[k] * b->timing_stride) : 0.0;
+    const int64_t per = b->timing_sample ? 1 : b->timing_stride;   // launches per pair
+    count[k] = (int64_t)b->ev_used[k] * per;
+    avg_ms[k] = b->ev_used[k] ? tot / ((double)b->ev_used[k] * per) : 0.0;
     b->ev_used[k] = 0;
     b->timing_seen[k] = 0;
   }

@@ -230,6 +230,9 @@ __device__ __forceinline__ double dpp_bcast(double v) {
 constexpr int kPair0 = 0xA0, kPair1 = 0xF5;
 constexpr int kQuad0 = 0x00, kQuad1 = 0x55, kQuad2 = 0xAA, kQuad3 = 0xFF;
 constexpr int kQuadX1 = 0xB1, kQuadX2 = 0x4E;
+// Position split (LPM = 4): lanes with pc = 0 (0, 2) carry X, pc = 1 (1, 3) carry Y.  A =
+// [3,2,3,2] (X lanes get h cos psi, Y lanes h sin psi), B = [2,3,2,3] (the other one).
+constexpr int kQuadPosA = 0xBB, kQuadPosB = 0xEE;
 
 // One tire's constants in this lane: front (lw = lf, sg = +1) or rear (lw = lr, sg = -1).
 struct Chain {
@@ -331,7 +334,9 @@ struct StageK {
   double fw;
   double k1, k2, k0, k3;   // Frx = (k1 - k2 vx) a - k0 - k3 vx^2; input_acc: (mass, 0, 0, 0)
   double pm, po;           // LPM = 4: the angle argument of chain_fold
+  double psg;              // LPM = 4 position split: -1 on X lanes, +1 on Y lanes
   int ra;
+  int pc;                  // LPM = 4 position split: the lane's component (0 = X, 1 = Y)
   bool sok;
 };
 
@@ -348,6 +353,8 @@ __device__ __forceinline__ StageK make_stage(const VehK& v, const Tire& t, int s
   s.pm = sub == 2 ? 1.0 : (sub == 3 ? -1.0 : 0.0);
   s.po = sub == 3 ? fm::kPio2 : 0.0;
   s.ra = sub == 3 ? 0x7FFFFFFF : -1;
+  s.pc = sub & 1;
+  s.psg = (sub & 1) ? 1.0 : -1.0;
   // dynamic.py:141 (input_acc: mass * a) as the :146 form with (mass, 0, 0, 0): equal for
   // finite vx (a non-finite vx is outside the chain domain -> the general rhs)
   s.k1 = v.input_acc ? v.mass : v.Cm1;
@@ -369,7 +376,9 @@ struct StageF {
   double Ffy, Fry, sp, cp;
 };
 // Bd = B d fw, the chain's steering term (LPM = 4 only; formed once per step).
-template <int LPM>
+// SPLIT (LPM = 4, position split): sp/cp carry the split's A/B operands instead (X lanes:
+// cos, sin; Y lanes: sin, cos — kQuadPosA/B).
+template <int LPM, bool SPLIT = false>
 __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, double vy, double om,
                                               double d, double psi, const fm::FmK& K, Dom& dm,
                                               double Bd = 0.0) {
@@ -379,8 +388,13 @@ __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, doub
     const double r = chain_fold(sk.ch[0], den, vy, om, Bd, psi, sk.ra, sk.pm, sk.po, dm, K);
     f.Ffy = dpp_bcast<kQuad0>(r);
     f.Fry = dpp_bcast<kQuad1>(r);
-    f.sp = dpp_bcast<kQuad2>(r);
-    f.cp = dpp_bcast<kQuad3>(r);
+    if constexpr (SPLIT) {
+      f.sp = dpp_bcast<kQuadPosA>(r);
+      f.cp = dpp_bcast<kQuadPosB>(r);
+    } else {
+      f.sp = dpp_bcast<kQuad2>(r);
+      f.cp = dpp_bcast<kQuad3>(r);
+    }
     return f;
   }
   if (LPM == 2) {
@@ -456,51 +470,68 @@ __device__ __forceinline__ FusedK make_fused(const VehK& v, const StageK& sk, do
   return q;
 }
 
-template <int LPM>
+// SPLIT (LPM = 4 only): the quad's lanes integrate ONE position component each — X on pc =
+// 0, Y on pc = 1 — in k[0]/x[0] (k[1]/x[1] unused): the position feeds nothing but the cost,
+// so the component's increment, stage sums and tracking term are formed once instead of
+// twice in every lane.  X: vx hcos - vy hsin; Y: vx hsin + vy hcos = fma(vx, A, psg vy B).
+template <int LPM, bool SPLIT = false>
 __device__ __forceinline__ void k_fused(const StageK& sk, const FusedK& q, double F0, double F1,
                                         double hmsd, double hmcd, double c5a, double d, double Bd,
                                         const double* y, double* k, const fm::FmK& K, Dom& dm) {
   const double vx = y[3], vy = y[4], om = y[5];
-  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, y[2], K, dm, Bd);
+  const StageF f = forces_fast<LPM, SPLIT>(sk, vx, vy, om, d, y[2], K, dm, Bd);
   // h sin(psi), h cos(psi): LPM = 4 lanes 2/3 scale their sine by h already (make_stage)
   const double hsp = (LPM == 4) ? f.sp : q.h * f.sp, hcp = (LPM == 4) ? f.cp : q.h * f.cp;
   const double hmFrx = fma(vx, fma(q.m3, vx, F1), F0);                     // hm Frx
   k[2] = q.h * om;
-  k[0] = fma(vx, hcp, -(vy * hsp));                                       // h (vx cos - vy sin)
-  k[1] = fma(vx, hsp, vy * hcp);
+  if constexpr (SPLIT) {
+    k[0] = fma(vx, hsp, (sk.psg * vy) * hcp);                             // (A, B) in (sp, cp)
+    k[1] = 0.0;
+  } else {
+    k[0] = fma(vx, hcp, -(vy * hsp));                                     // h (vx cos - vy sin)
+    k[1] = fma(vx, hsp, vy * hcp);
+  }
   k[3] = fma(-f.Ffy, hmsd, fma(vy, k[2], hmFrx));                         // h/m (Frx - Ffy sd) + h vy om
   k[4] = fma(f.Ffy, hmcd, fma(-vx, k[2], q.hm * f.Fry));                  // h/m (Fry + Ffy cd) - h vx om
   k[5] = fma(f.Ffy, c5a, -(f.Fry * q.hIlr));                              // h/Iz (Ffy lf cd - Fry lr)
 }
 
-template <int LPM>
+template <int LPM, bool SPLIT = false>
 __device__ __forceinline__ void step_fused(const StageK& sk, const FusedK& q, double* x,
                                            const Input& u, const fm::FmK& K, Dom& dm) {
+  static_assert(!SPLIT || LPM == 4, "the position split needs the quad");
   const double F0 = fma(q.m1, u.a, -q.m0), F1 = -(q.m2 * u.a);
   const double hmsd = q.hm * u.sd, hmcd = q.hm * u.cd, c5a = q.hIlf * u.cd;
   const double Bd = (LPM == 4) ? sk.ch[0].B * (u.d * sk.fw) : 0.0;
   double y[6], k[6], acc[6];
-  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, x, k, K, dm);
+  y[1] = acc[1] = 0.0;
+  k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, x, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
+    if (SPLIT && i == 1) continue;
     acc[i] = k[i];
     y[i] = fma(0.5, k[i], x[i]);
   }
-  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
+  k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
+    if (SPLIT && i == 1) continue;
     acc[i] = fma(2.0, k[i], acc[i]);
     y[i] = fma(0.5, k[i], x[i]);
   }
-  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
+  k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
+    if (SPLIT && i == 1) continue;
     acc[i] = fma(2.0, k[i], acc[i]);
     y[i] = x[i] + k[i];
   }
-  k_fused<LPM>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
+  k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) x[i] = fma(acc[i] + k[i], K.sixth, x[i]);
+  for (int i = 0; i < 6; ++i) {
+    if (SPLIT && i == 1) continue;
+    x[i] = fma(acc[i] + k[i], K.sixth, x[i]);
+  }
 }
 
 // One look-ahead step on the fast path.

@@ -503,16 +503,22 @@ __device__ __forceinline__ bool input_feasible(const CostK& q, double ua, double
 // the fast cores' domains.  !FAST: the general evaluation (rk4_step / euler / rk6 with the
 // general transcendentals) — the re-run of bad lanes, so every lane's result depends on its
 // own operands only.  Returns J (+inf when infeasible).
-template <int INTEG, bool STAGE, int LPM, int XM, bool FAST>
+// SPLIT (fused RK4 at LPM = 4, diagonal Q and P): each lane of the quad integrates one
+// position component (dyn.hpp k_fused) and accumulates its tracking term; the quad's J is
+// (J_X + J_Y) + act by two DPP broadcasts at the end.
+template <int INTEG, bool STAGE, int LPM, int XM, bool FAST, bool SPLIT = false>
 __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64_t n,
                                           const double* x0, const double* sx, const double* su, const VehK& veh,
                                           const Tire& t, const StageK& sk, const CostK& q,
                                           double Ts, double up0, double up1, const fm::FmK& K,
                                           const FusedK& fq, bool& bad) {
+  static_assert(!SPLIT || (FAST && INTEG == 0 && LPM == 4), "position split: fused RK4 quads only");
   const int H = a.H, C = a.C;
   double x[6];
 #pragma unroll
   for (int m = 0; m < 6; ++m) x[m] = x0[m];
+  if (SPLIT) x[0] = sk.pc ? x0[1] : x0[0];
+  const double Qd = sk.pc ? q.Q[3] : q.Q[0], Pd = sk.pc ? q.P[3] : q.P[0];   // SPLIT only
   double track = 0.0, act = 0.0;
   double p0 = up0, p1 = up1;
   bool feas = true;
@@ -542,25 +548,38 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     }
     const double d0 = ua - p0, d1 = ud - p1;          // nmpc.py:65-68
     if (!STAGE && q.enforce) feas = (int)feas & (int)input_feasible(q, ua, ud, d0, d1);
-    if (FAST && INTEG == 0) step_fused<LPM>(sk, fq, x, u, K, dm);
+    if (FAST && INTEG == 0) step_fused<LPM, SPLIT>(sk, fq, x, u, K, dm);
     else if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, dm);
     else step<INTEG>(veh, t, x, u, Ts);
-    if (XM) {
+    if (SPLIT) {                        // this lane's component of the reference and term
+      xr0 = XM ? xpm[2 * k + sk.pc] : sx[2 * (k + 1) + sk.pc];
+      const double e = x[0] - xr0;
+      track = track + e * (Qd * e);
+    } else if (XM) {
       xr0 = xpm[2 * k];
       xr1 = xpm[2 * k + 1];
     } else {
       xr0 = sx[2 * (k + 1)];
       xr1 = sx[2 * (k + 1) + 1];
     }
-    const double e0 = x[0] - xr0, e1 = x[1] - xr1;
-    track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
+    if (!SPLIT) {
+      const double e0 = x[0] - xr0, e1 = x[1] - xr1;
+      track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
+    }
     if (!STAGE) act = act + act_term(q, d0, d1);
     p0 = ua;
     p1 = ud;
   }
-  const double e0 = x[0] - xr0, e1 = x[1] - xr1;                   // nmpc.py:48 (xref_H)
-  const double term = e0 * (q.P[0] * e0 + q.P[1] * e1) + e1 * (q.P[2] * e0 + q.P[3] * e1);
-  double J = (term + track) + act;                                // nmpc.py:111
+  double J;
+  if (SPLIT) {                                                    // nmpc.py:48, :111
+    const double e = x[0] - xr0;
+    const double jl = e * (Pd * e) + track;                       // this component's part
+    J = (dpp_bcast<kQuad0>(jl) + dpp_bcast<kQuad1>(jl)) + act;    // X (lane 0) + Y (lane 1)
+  } else {
+    const double e0 = x[0] - xr0, e1 = x[1] - xr1;                 // nmpc.py:48 (xref_H)
+    const double term = e0 * (q.P[0] * e0 + q.P[1] * e1) + e1 * (q.P[2] * e0 + q.P[3] * e1);
+    J = (term + track) + act;                                     // nmpc.py:111
+  }
   // the domain, once per rollout: a NaN operand reaches x[0..1] (every chain output feeds
   // the later stages' positions, the last stage's feeds vx, vy, omega only through a NaN
   // state that the position update already carries), so a non-finite J is re-run too
@@ -676,6 +695,11 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   int64_t bc = kNoIndex;
   int nf = 0;
   LA_STAMP(blk, 1);
+  // position split of the quad (fused RK4, LPM = 4) when Q and P are diagonal (rt.py:60-62:
+  // Q = diag(1, 1), P = 0): tested on the unpinned kernel-argument copy, so the branch is
+  // scalar
+  constexpr bool kSplit = (INTEG == 0 && LPM == 4);
+  const bool diagQP = a.cost.Q[1] == 0.0 && a.cost.Q[2] == 0.0 && a.cost.P[1] == 0.0 && a.cost.P[2] == 0.0;
   if (live) {
     // LPM = 2: lane 0 of the pair evaluates the front chain, lane 1 the rear (dyn.hpp)
     const StageK sk = make_stage<LPM>(veh, t, sub, INTEG == 0 ? Ts : 1.0);
@@ -685,7 +709,11 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       const int c = g + j * G;
       if (c >= C) break;
       bool bad = false;
-      double J = rollout<INTEG, STAGE, LPM, XM, true>(a, c, n, x0, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, bad);
+      double J;
+      if (kSplit && diagQP)             // launch-uniform (kernel arguments)
+        J = rollout<INTEG, STAGE, LPM, XM, true, kSplit>(a, c, n, x0, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, bad);
+      else
+        J = rollout<INTEG, STAGE, LPM, XM, true>(a, c, n, x0, sx, su, veh, t, sk, q, Ts, up0, up1, K, fq, bad);
       if (LPM == 2) {                   // the pair shares one rollout: re-run both or neither
         const int bi = bad;
         bad = __builtin_amdgcn_mov_dpp(bi, kPair0, 0xF, 0xF, false) |

@@ -254,6 +254,33 @@ def test_lookahead_candidate_group_shapes(nat, C, H, N):
     assert r["best_model"] * C + r["best_cand"] == int(np.argmin(cm.ravel()))
 
 
+@pytest.mark.parametrize("Q,P", [(np.diag([2.0, 0.5]), np.diag([3.0, 0.25])),       # split quads
+                                 (np.array([[1.0, 0.3], [0.2, 2.0]]), np.array([[0.5, -0.1], [0.4, 1.0]]))])
+def test_lookahead_weighted_cost(nat, Q, P):
+    """nmpc.py:44-111 with other Q and terminal P than rt.py's: diagonal weights take the
+    position split of the LPM-4 quads (each lane one position component), full matrices the
+    unsplit path; both against the oracle's cost on the reference rollouts."""
+    from llampc import _native
+    from llampc.mpc import ModelBank, generate_bank
+    N, C, H = 500, 3, 20
+    p = generate_bank(N, seed=21)
+    rng = np.random.RandomState(21)
+    x0 = np.array([0.3, -0.2, 0.9, 1.7, -0.03, 0.5])
+    U = np.stack([rng.uniform(-0.1, 1.0, (C, H)), rng.uniform(-0.3, 0.3, (C, H))], axis=-1)
+    xref = np.vstack([0.3 + 0.02 * np.arange(H + 1), -0.2 + 0.03 * np.arange(H + 1)])
+    uprev = np.array([0.4, 0.05])
+    R = np.diag([5e-3, 1.0])
+    with np.errstate(all="ignore"):
+        traj = O.rollout_rk4(shared(), tuple(p), x0, U, TS)
+        cref = O.mpc_cost(traj, U, xref, uprev, Q, R, P)
+    cost = _native.cost_struct(Q=Q, R=R, P=P)
+    with ModelBank(p, device=0) as b:
+        r = b.lookahead(x0, U, xref, uprev, Ts=TS, cost=cost, return_costs=True, return_best_cand=True)
+    close(r["costs"].ravel(), cref, RTOL_ROLL)
+    cm = np.where(np.isnan(cref), np.inf, cref).reshape(N, C)
+    np.testing.assert_array_equal(r["best_cand_per_model"], np.argmin(cm, axis=1))
+
+
 def test_lookahead_feasibility_mask(nat):
     from llampc import _native
     from llampc.mpc import ModelBank, generate_bank
