@@ -34,6 +34,7 @@ for _p in (REPO, os.path.join(REPO, "lla-mpc_amd")):
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector spec
 TIMING_STRIDE = 8               # HIP-event pairs bracket groups of 8 consecutive plan launches
+TIMING_SAMPLE = 16              # with the exchange: one plan launch in 16 bracketed alone
 FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation (excl. transcendentals)
 # Issue roofline: instructions per rollout step of the fast look-ahead loop, per lane, by lane
 # split (tools/diag/isa_counts.py on the current sources), and the chip's fp64 VALU issue
@@ -207,10 +208,11 @@ def main():
         # event pairs bracket groups of TIMING_STRIDE consecutive launches of the timed loop:
         # the kernel's mean duration measured live, the events' own cost spread over a group.
         # With the exchange, a group would also hold the all-gathers and merges in between,
-        # so ONE plan launch in every TIMING_STRIDE gets its own pair (negative stride =
+        # so ONE plan launch in every TIMING_SAMPLE gets its own pair (negative stride =
         # sampling; the bracketed launch reads ~2 us high, the events' own cost, and only
-        # 1/TIMING_STRIDE of the timed ticks carry events)
-        stride = -TIMING_STRIDE if sb.exchange else TIMING_STRIDE
+        # 1/TIMING_SAMPLE of the timed ticks carry events: measured 0.8 us/tick of event
+        # cost at 1 in 8 on a forced 1-rank exchange, ~2 us with a pair on every tick)
+        stride = -TIMING_SAMPLE if sb.exchange else TIMING_STRIDE
         nat.check(lib.llampc_bank_timing(sb.bank.handle, stride, args.steps // abs(stride) + 8))
     torch.cuda.synchronize()
     if world > 1:
@@ -277,7 +279,7 @@ def main():
                      "note": "plain flops only; the 29 fp64 transcendentals per RK4 step are excluded"},
             "issue": issue_roofline(N_local, C, H, lpm_of(N_local, C), plan_ms),
             "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0]),
-                          "bracket": f"one plan launch in every {TIMING_STRIDE} per event pair" if sb.exchange else
+                          "bracket": f"one plan launch in every {TIMING_SAMPLE} per event pair" if sb.exchange else
                                      f"groups of {TIMING_STRIDE} consecutive plan launches"},
             "exchange": (("native RCCL all-gather on the tick stream (llampc_exchange_device)" if sb._comm is not None
                           else f"c10d all_gather_into_tensor ({sb.backend})") + " + merge_kernel") if sb.exchange else None,
