@@ -293,6 +293,7 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
     lbl.nan_first = in.nan_policy == LLAMPC_NAN_FIRST;
     lbl.err_out = d_err;
     lbl.wm_buf = d_wmean ? d_wmean : b->d_wmean;
+    lbl.wm_keep = d_wmean != nullptr;              // else only the R > 1 second pass reads it
     lbl.am_val = b->d_am_val;
     lbl.am_idx = b->d_am_idx;
     lbl.tk_val = b->d_tk_val;

@@ -427,7 +427,8 @@ __device__ __forceinline__ void rhs_fast(const VehK& v, const StageK& sk, const 
     vx = 0.05;
   }
   // den = vx: the fast atan2 takes |den| (Ref: atan2(., |vx|); Nlp: vx >= vmin after the clamp)
-  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, x[2], K, dm, sk.ch[0].B * (d * sk.fw));
+  const double Bd = sk.ch[0].B * (d * sk.fw);
+  const StageF f = forces_fast<LPM>(sk, vx, vy, om, d, x[2], K, dm, Bd);
   const double Frx = (sk.k1 - sk.k2 * vx) * u.a - sk.k0 - sk.k3 * (vx * vx);
   dx[0] = vx * f.cp - vy * f.sp;
   dx[1] = vx * f.sp + vy * f.cp;
@@ -496,12 +497,22 @@ __device__ __forceinline__ void k_fused(const StageK& sk, const FusedK& q, doubl
   k[5] = fma(f.Ffy, c5a, -(f.Fry * q.hIlr));                              // h/Iz (Ffy lf cd - Fry lr)
 }
 
+// The step's input terms of the fused stages: they depend on the input and the shared
+// constants only, so a staged look-ahead forms them once per (step, candidate) per block.
+struct FusedIn {
+  double F0, F1, hmsd, hmcd, c5a;
+};
+__device__ __forceinline__ FusedIn fused_in(const FusedK& q, const Input& u) {
+  return FusedIn{fma(q.m1, u.a, -q.m0), -(q.m2 * u.a), q.hm * u.sd, q.hm * u.cd, q.hIlf * u.cd};
+}
+
 template <int LPM, bool SPLIT = false>
 __device__ __forceinline__ void step_fused(const StageK& sk, const FusedK& q, double* x,
-                                           const Input& u, const fm::FmK& K, Dom& dm) {
+                                           const FusedIn& fi, double ud, const fm::FmK& K,
+                                           Dom& dm) {
   static_assert(!SPLIT || LPM == 4, "the position split needs the quad");
-  const double F0 = fma(q.m1, u.a, -q.m0), F1 = -(q.m2 * u.a);
-  const double hmsd = q.hm * u.sd, hmcd = q.hm * u.cd, c5a = q.hIlf * u.cd;
+  const double F0 = fi.F0, F1 = fi.F1, hmsd = fi.hmsd, hmcd = fi.hmcd, c5a = fi.c5a;
+  const Input u{0.0, ud, 0.0, 0.0};                       // k_fused reads u.d only
   const double Bd = (LPM == 4) ? sk.ch[0].B * (u.d * sk.fw) : 0.0;
   double y[6], k[6], acc[6];
   y[1] = acc[1] = 0.0;
@@ -532,6 +543,12 @@ __device__ __forceinline__ void step_fused(const StageK& sk, const FusedK& q, do
     if (SPLIT && i == 1) continue;
     x[i] = fma(acc[i] + k[i], K.sixth, x[i]);
   }
+}
+
+template <int LPM, bool SPLIT = false>
+__device__ __forceinline__ void step_fused(const StageK& sk, const FusedK& q, double* x,
+                                           const Input& u, const fm::FmK& K, Dom& dm) {
+  step_fused<LPM, SPLIT>(sk, q, x, fused_in(q, u), u.d, K, dm);
 }
 
 // One look-ahead step on the fast path.

@@ -284,7 +284,7 @@ __device__ __forceinline__ double window_mean(const double* ring, int64_t ld, in
 // G17): [0,64) sv[2][4] double | [64,128) si[2][4] int64 | [128,144) sn[4] int32 |
 // pad to 160 | role-specific region from 160.
 constexpr int kScratchBytes = 160;
-constexpr int kStageW = 6;              // doubles per staged (step, candidate) input
+constexpr int kStageW = 8;              // doubles per staged (step, candidate) input
 constexpr int kRankBytes = 64 * 8 + 64 * 4 + 256;   // wave_topk_rank: keys + ids per wave (+pad)
 constexpr int kWaves = kBlock / 64;     // look-back lists per block (one per wave)
 constexpr int kListsPerLane = 8;        // lb_final: lists per lane of the merging wave
@@ -424,7 +424,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     if (a.full) {
       const int o = (a.slot + 1 == a.W) ? 0 : a.slot + 1;   // oldest slot
       const double wm = window_mean(a.ring, a.n, n, o, a.W);   // rt.py:358
-      a.wm_buf[n] = wm;
+      if (a.R > 1 || a.wm_keep) a.wm_buf[n] = wm;         // launch-uniform
       if (r == 0) wm0 = wm;
     }
   }
@@ -530,16 +530,27 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   for (int k = 0; k < H; ++k) {
     double ua, ud;
     Input u;
-    if (STAGE) {                        // sincos(delta) staged with the fast/general rule
+    FusedIn fi{};
+    if (STAGE) {                        // staged per block (lookahead_block), layouts there
       const double* o = su + kStageW * (k * C + c);
-      ua = o[0];
-      ud = o[1];
-      u.a = ua;
-      u.d = ud;
-      u.sd = o[2];
-      u.cd = o[3];
-      act = act + o[4];                 // the candidate's input-rate term and feasibility,
-      feas_s = feas_s * o[5];           // formed once per block (lookahead_block)
+      if (INTEG == 0 && FAST) {         // the fused stages' input terms
+        fi = FusedIn{o[0], o[1], o[2], o[3], o[4]};
+        ua = 0.0;
+        ud = o[5];
+      } else if (INTEG == 0) {          // the general re-run: the candidate from U itself
+        ua = a.U[2 * ((int64_t)c * H + k)];
+        ud = a.U[2 * ((int64_t)c * H + k) + 1];
+        u = make_input(ua, ud);
+      } else {                          // sincos(delta) staged with the fast/general rule
+        ua = o[0];
+        ud = o[1];
+        u.a = ua;
+        u.d = ud;
+        u.sd = o[2];
+        u.cd = o[3];
+      }
+      act = act + o[6];                 // the candidate's input-rate term and feasibility
+      feas_s = feas_s * o[7];
     } else {
       ua = a.U[2 * ((int64_t)c * H + k)];
       ud = a.U[2 * ((int64_t)c * H + k) + 1];
@@ -548,7 +559,8 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     }
     const double d0 = ua - p0, d1 = ud - p1;          // nmpc.py:65-68
     if (!STAGE && q.enforce) feas = (int)feas & (int)input_feasible(q, ua, ud, d0, d1);
-    if (FAST && INTEG == 0) step_fused<LPM, SPLIT>(sk, fq, x, u, K, dm);
+    if (FAST && INTEG == 0 && STAGE) step_fused<LPM, SPLIT>(sk, fq, x, fi, ud, K, dm);
+    else if (FAST && INTEG == 0) step_fused<LPM, SPLIT>(sk, fq, x, u, K, dm);
     else if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, dm);
     else step<INTEG>(veh, t, x, u, Ts);
     if (SPLIT) {                        // this lane's component of the reference and term
@@ -593,7 +605,8 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
 // Look-ahead body.  Lane layout inside a block: sub = lane % LPM (LPM = 2: the lane pair
 // of one rollout, front/rear chain), cl = lane / LPM; G candidate-lanes per model (power of two); a model's
 // candidates c = g + j*G, j < cpl, run sequentially in its G*LPM lanes.
-//   LDS from kScratchBytes: xref as [k][2]; U as [k][c][kStageW] (pwm, delta, sin, cos,
+//   LDS from kScratchBytes: xref as [k][2]; U as [k][c][kStageW] (RK4: F0, F1, h/m sin,
+//   h/m cos, h lf/Iz cos, delta; else pwm, delta, sin, cos; then
 //   input-rate cost term, feasibility) when staged.
 // ------------------------------------------------------------------------------------
 template <int INTEG, bool STAGE, int LPM, int XM>
@@ -644,8 +657,11 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   if (STAGE) {
     // [k][c] -> (pwm, delta, sin delta, cos delta): the steering's sincos depends only on the
     // shared candidates, so it is formed once per block here (same evaluation as
-    // make_input_fast: the fast core on its domain, the general function off it)
+    // make_input_fast: the fast core on its domain, the general function off it).  RK4
+    // stages the fused stages' input terms instead: (F0, F1, h/m sin d, h/m cos d,
+    // h lf/Iz cos d, delta) — dyn.hpp fused_in, with the shared constants of make_fused.
     const fm::FmK K = fm::FmK::load();
+    const FusedK fq0 = make_fused(a.veh, make_stage<1>(a.veh, Tire{}, 0), a.Ts);
     for (int e = threadIdx.x; e < C * H; e += kBlock) {
       const int c = e / H, k = e - c * H;
       const double dl = a.U[2 * e + 1];
@@ -656,12 +672,22 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       const double ua = a.U[2 * e];
       const double p0 = k ? a.U[2 * e - 2] : a.uprev[0], p1 = k ? a.U[2 * e - 1] : a.uprev[1];
       const double d0 = ua - p0, d1 = dl - p1;
-      o[0] = ua;
-      o[1] = dl;
-      o[2] = sd;
-      o[3] = cd;
-      o[4] = act_term(a.cost, d0, d1);
-      o[5] = (!a.cost.enforce || input_feasible(a.cost, ua, dl, d0, d1)) ? 1.0 : 0.0;
+      if (INTEG == 0) {
+        const FusedIn fi = fused_in(fq0, Input{ua, dl, sd, cd});
+        o[0] = fi.F0;
+        o[1] = fi.F1;
+        o[2] = fi.hmsd;
+        o[3] = fi.hmcd;
+        o[4] = fi.c5a;
+        o[5] = dl;
+      } else {
+        o[0] = ua;
+        o[1] = dl;
+        o[2] = sd;
+        o[3] = cd;
+      }
+      o[6] = act_term(a.cost, d0, d1);
+      o[7] = (!a.cost.enforce || input_feasible(a.cost, ua, dl, d0, d1)) ? 1.0 : 0.0;
     }
   }
   __syncthreads();
@@ -1471,8 +1497,9 @@ int lookahead_blocks(int64_t n, int32_t C, int lpm) {
   return (int)((n + mpb - 1) / mpb);
 }
 
-// Staged inputs per (step, candidate): pwm, delta, sin delta, cos delta, the input-rate
-// cost term and the feasibility (1/0) — kStageW doubles.  One block per CU (the launch's LDS
+// Staged inputs per (step, candidate): RK4 the fused stages' input terms and delta, else pwm,
+// delta, sin delta, cos delta; then the input-rate cost term and the feasibility (1/0) —
+// kStageW doubles.  One block per CU (the launch's LDS
 // request), so the staging may use most of the CU's 160 KiB.
 constexpr size_t kStageLimit = 128 * 1024;
 

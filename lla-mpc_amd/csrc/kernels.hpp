@@ -29,8 +29,9 @@ struct LookbackLaunch {
   double* ring;          // [W][n]
   int32_t W, slot, full, K, nan_first;
   int32_t R;             // models per lane (set by launch_plan)
+  int32_t wm_keep;       // the caller reads wm_buf (else it is written only when R > 1)
   double* err_out;       // [n] or null
-  double* wm_buf;        // [n] window means (always written when the window is full)
+  double* wm_buf;        // [n] window means (when the window is full: R > 1 or wm_keep)
   double* am_val;  int64_t* am_idx;   // [blocks * kWaves] (one per look-back wave)
   double* tk_val;  int64_t* tk_idx;   // [blocks * kWaves][K]
 };
