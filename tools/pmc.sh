@@ -22,4 +22,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
      python3 tools/pmc_calib.py > gpurun_out/pmc/cal_$c.log 2>&1 || { echo "calibration $c failed"; tail -5 gpurun_out/pmc/cal_$c.log; }
 done
 python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.txt 2>&1; cat gpurun_out/pmc/summary.txt
-[ -n "$PMC_KEY" ] && python3 tools/pmc_traffic.py gpurun_out/pmc "$PMC_KEY"
+if [ -n "$PMC_KEY" ]; then python3 tools/pmc_traffic.py gpurun_out/pmc "$PMC_KEY"; fi
