@@ -75,6 +75,17 @@ VehK make_veh(const llampc_vehicle& v) {
   return k;
 }
 
+// The constants an integrator sees: the NLP transcription (Dynamic.casadi + Euler,
+// dynamic.py:214-218, nmpc.py:58-60) always uses the pwm motor model and the Pacejka tires,
+// so input_acc / approx apply to the batch (RK4 / RK6) forms only.
+VehK integrator_veh(VehK k, int32_t integrator) {
+  if (integrator == LLAMPC_EULER_NLP) {
+    k.input_acc = 0;
+    k.approx = 0;
+  }
+  return k;
+}
+
 CostK make_cost(const llampc_cost& c, double Ts) {
   CostK k;
   for (int i = 0; i < 4; ++i) {
@@ -262,6 +273,21 @@ void timing_free(llampc_bank* b) {
   b->timing_sample = false;
 }
 
+// The polled completion's wait bound in s_memrealtime ticks (100 MHz): a 2 s floor plus
+// 40 ns per look-ahead rollout step of the launch (a rate floor of 2.5e7 steps/s, ~10^3
+// below the fast path's, so the general-path re-runs, the raceline walker and launches
+// sharing the chip all fit).  A valid long tick (n = 1e7, C = 64, H = 40: ~4 s) therefore
+// never reads as a timeout; only a poll that could never finish does.
+// LLAMPC_POLL_BOUND_S overrides the floor and LLAMPC_POLL_STEP_NS the per-step term (tests).
+uint64_t poll_bound_ticks(int64_t n, int32_t C, int32_t H) {
+  double floor_s = 2.0, step_ns = 40.0;
+  if (const char* e = getenv("LLAMPC_POLL_BOUND_S")) floor_s = std::max(0.0, atof(e));
+  if (const char* e = getenv("LLAMPC_POLL_STEP_NS")) step_ns = std::max(0.0, atof(e));
+  const double steps = (double)n * (double)C * (double)H;    // <= 2^57 (check_plan_in)
+  const double ticks = 1e8 * floor_s + 0.1 * step_ns * steps;
+  return ticks >= 1.8e19 ? ~0ull : (uint64_t)ticks;
+}
+
 // The tick on device pointers: ONE launch (look-back + look-ahead + completion).
 // Advances the window bookkeeping when a look-back runs.
 int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out, double* d_err,
@@ -304,7 +330,7 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
     lal.params = b->d_params;
     lal.n = b->n;
     lal.goff = b->goff;
-    lal.veh = b->veh;
+    lal.veh = integrator_veh(b->veh, in.integrator);
     lal.x0 = in.x_now;
     lal.U = in.U;
     lal.xref = in.xref;
@@ -362,6 +388,7 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   f.blk_tag = b->d_blk_tag;
   f.seq = b->seq;
   f.poll = poll;
+  f.poll_bound = poll_bound_ticks(la ? b->n : 0, la ? in.C : 0, la ? in.H : 0);
   f.host_tag = host_tag;
   f.host_seq = host_seq;
   if (la) {
@@ -791,6 +818,8 @@ int llampc_plan_device(llampc_bank* b, const llampc_plan_in* in, void* d_out, do
   int rc = check_plan_in(b, in);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(b->mu);
+  // an outstanding async tick shares the tickets, tags, ring slot and window count
+  if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
   DeviceGuard g(b->device);
   return plan_launch(b, *in, (llampc_plan_out*)d_out, d_err, d_wmean, d_cost, pick_stream(b, stream));
 }
@@ -987,7 +1016,7 @@ extern "C" int llampc_integrate_batch(const double* x0, const double* u, int64_t
   int dev, rc;
   if ((rc = resolve_device(device, &dev))) return rc;
   DeviceGuard g(dev);
-  const VehK vk = make_veh(*veh);
+  const VehK vk = integrator_veh(make_veh(*veh), integrator);
   const size_t out_n = (final_only ? 1 : (size_t)(S + 1)) * n * 6;
   if (device_ptrs) {
     HIP_TRY(launch_integrate(x0, u, u_stride_lane, h, S, params, P, vk, n, integrator, traj_out,

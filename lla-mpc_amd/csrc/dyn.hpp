@@ -53,7 +53,9 @@ __device__ __host__ __forceinline__ Forces forces(const VehK& v, const Tire& t, 
                                                   double vy, double om, double pwm,
                                                   double delta) {
   Forces f;
-  if (v.approx) {                      // dynamic.py:126-136 (Rajamani linear tires)
+  // Dynamic.casadi (Form::Nlp) always uses the pwm motor model and the Pacejka tires
+  // (dynamic.py:214-218), whatever input_acc / approx say
+  if (F == Form::Ref && v.approx) {    // dynamic.py:126-136 (Rajamani linear tires)
     f.Frx = v.mass * pwm;
     f.af = delta - (v.lf * om + vy) / vx;
     f.ar = (v.lr * om - vy) / vx;
@@ -61,7 +63,7 @@ __device__ __host__ __forceinline__ Forces forces(const VehK& v, const Tire& t, 
     f.Fry = 2 * t.Cr * f.ar;
     return f;
   }
-  f.Frx = v.input_acc ? v.mass * pwm                                   // dynamic.py:141
+  f.Frx = (F == Form::Ref && v.input_acc) ? v.mass * pwm              // dynamic.py:141
                       : (v.Cm1 - v.Cm2 * vx) * pwm - v.Cr0 - v.Cr2 * (vx * vx);  // :146
   // Ref form: atan2(., |vx|) (dynamic.py:149-150); NLP form: atan2(., vx) (:215-216)
   const double den = (F == Form::Ref) ? fabs(vx) : vx;

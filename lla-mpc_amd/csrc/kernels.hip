@@ -1103,11 +1103,11 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
 // spins on its share of the tagged words — the look-ahead blocks' partials (5 words each),
 // the top-K models' and the selected model's results (3 words each) — until every word it
 // loads carries this launch's tag; one block barrier then joins them.  The blocks it waits
-// for never wait, so it cannot deadlock; a 2 s bound (s_memrealtime, 100 MHz) ends a poll
-// that could never finish (a bug) with status LLAMPC_STATUS_POLL_TIMEOUT in the record
+// for never wait, so it cannot deadlock; a bound (f.poll_bound s_memrealtime ticks, 100 MHz,
+// scaled by the host with the launch's rollout steps: poll_bound_ticks in capi.hip) ends a
+// poll that could never finish (a bug) with status LLAMPC_STATUS_POLL_TIMEOUT in the record
 // instead of a hang.
 constexpr int kPollTimeoutStatus = LLAMPC_STATUS_POLL_TIMEOUT;
-constexpr uint64_t kPollBound = 200000000ull;   // 2 s of s_memrealtime (100 MHz)
 __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& sc) {
   STAMP(3);
   const int tid = threadIdx.x;
@@ -1135,7 +1135,7 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
 #pragma unroll
       for (int w = 0; w < 3; ++w) kw[w] = ld_wt(&f.la_tag[w * f.n + mk]);
       if ((int)tag_ok(kw[0], f.seq) & (int)tag_ok(kw[1], f.seq) & (int)tag_ok(kw[2], f.seq)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kPollBound) { late = true; break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > f.poll_bound) { late = true; break; }
     }
   }
   if (ms >= 0) {
@@ -1143,7 +1143,7 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
 #pragma unroll
       for (int w = 0; w < 3; ++w) sw[w] = ld_wt(&f.la_tag[w * f.n + ms]);
       if ((int)tag_ok(sw[0], f.seq) & (int)tag_ok(sw[1], f.seq) & (int)tag_ok(sw[2], f.seq)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kPollBound) { late = true; break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > f.poll_bound) { late = true; break; }
     }
   }
   for (int j = 0; j < nbt; ++j) {
@@ -1156,7 +1156,7 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
         if ((int)tag_ok(r[0], f.seq) & (int)tag_ok(r[1], f.seq) & (int)tag_ok(r[2], f.seq) &
             (int)tag_ok(r[3], f.seq) & (int)tag_ok(r[4], f.seq))
           break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kPollBound) { late = true; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > f.poll_bound) { late = true; break; }
       }
       const double pv = __longlong_as_double((long long)join_words(r[0], r[1]));
       const int64_t pi = (int64_t)join_words(r[2], r[3]);

@@ -74,6 +74,7 @@ struct FinalLaunch {
   const uint64_t* la_tag; const uint64_t* blk_tag;
   uint32_t seq;
   int32_t poll;
+  uint64_t poll_bound;                    // the poller's wait bound, s_memrealtime ticks (100 MHz)
   // host completion (llampc_plan / llampc_plan_wait): `out` is then the device alias of a
   // pinned host record, and the block that completes it stores host_seq to host_tag (pinned,
   // system scope) after a system-scope fence — the host spins on that word instead of a D2H

@@ -8,7 +8,11 @@ Host logic restated from the reference driver (llampc/mpc/run_nmpc_orca_llampc_r
                              the per-tick IPOPT solve of nmpc.py:161-203 by candidate search)
   * ``LLAMPC.tick``          one tick in rt.py order: look-back on the newest transition,
                              mu-hat, ConstantSpeed reference with mu-hat (rt.py:278-282),
-                             look-ahead of every (model, candidate), chosen control.
+                             look-ahead of every (model, candidate), chosen control.  While
+                             the window fills (tick <= W) the look-ahead plans with the
+                             NOMINAL model, as the reference's nlp_initial (rt.py:207,
+                             300-301); afterwards with the bank's selected model
+                             (nlp_bank[current_model_idx], rt.py:303).
 """
 from __future__ import annotations
 
@@ -17,7 +21,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from llampc import _native as nat
-from llampc.mpc.bank import ModelBank
+from llampc.mpc.bank import BANK_ORDER, ModelBank
 from llampc.mpc.plan import PlanResult, result_from_out
 from llampc.mpc.planner import ConstantSpeed
 
@@ -129,12 +133,20 @@ class CandidateGenerator:
 
 
 class LLAMPC:
-    """Stateful LLA-MPC tick loop over a ``ModelBank`` (rt.py:269-366 without IPOPT)."""
+    """Stateful LLA-MPC tick loop over a ``ModelBank`` (rt.py:269-366 without IPOPT).
+
+    ``nominal``: the Pacejka parameters the warm-up ticks plan with (default ORCA(),
+    the reference's true_model / params at setup, rt.py:78-79, 207)."""
 
     def __init__(self, bank: ModelBank, track, H=20, Ts=0.02, K=10, C=64, v_factor=0.9,
                  mu_init=1.0, S=20, alpha=0.08, cost=None, integrator="rk4", seed=2,
-                 nan_policy=nat.NAN_FIRST):
+                 nan_policy=nat.NAN_FIRST, nominal: dict | None = None):
+        from llampc.params import ORCA
         self.bank, self.track = bank, track
+        nominal = ORCA(control='pwm') if nominal is None else nominal
+        col = np.array([[float(nominal[k])] for k in BANK_ORDER])
+        # a one-model bank: the warm-up look-ahead runs the same kernel on the nominal model
+        self.nominal_bank = ModelBank(col, shared=bank.shared, W=1, device=bank.device)
         self.H, self.Ts, self.K, self.W = H, Ts, K, bank.W
         self.v_factor = v_factor
         sh = bank.shared
@@ -180,17 +192,26 @@ class LLAMPC:
         else:
             p = self.bank.params
             loc = self.last_topk - self.bank.global_offset
+            loc = loc[self.last_topk >= 0]           # -1 pads a bank of fewer than K models
             self.mu.update(p[5][loc], p[2][loc])
-        # 4. look-ahead of every (model, candidate) and the chosen control
+        # 4. look-ahead of every (model, candidate) and the chosen control: the nominal
+        #    model while the window fills (rt.py:300-301), the selected bank model after
+        #    (rt.py:303)
         uprev = np.zeros(2) if self.u_prev is None else self.u_prev
         U = self.gen(self.u_seq, uprev)
-        o, _, _, _ = self.bank.plan_raw(np.zeros(6), np.zeros(2), x_t, U, xref, uprev, Ts=self.Ts,
-                                        K=self.K, integrator=self.integrator, do_lookback=False,
-                                        do_lookahead=True, current_model=self.current_model,
-                                        cost=self.cost)
+        warm = t <= self.W
+        planner = self.nominal_bank if warm else self.bank
+        o, _, _, _ = planner.plan_raw(np.zeros(6), np.zeros(2), x_t, U, xref, uprev, Ts=self.Ts,
+                                      K=self.K, integrator=self.integrator, do_lookback=False,
+                                      do_lookahead=True, current_model=0 if warm else self.current_model,
+                                      cost=self.cost)
         res = result_from_out(o, U, mu_hat=self.mu.mu_pred)
+        res.nominal = warm
+        if warm:
+            res.best_model = self.current_model
         if lb is not None and lb["full"]:
-            res.window_full, res.topk, res.topk_err = True, lb["topk"], lb["topk_val"]
+            kk = lb["topk"] >= 0                     # argsort()[:K] has min(n, K) entries
+            res.window_full, res.topk, res.topk_err = True, lb["topk"][kk], lb["topk_val"][kk]
         res.window_count = self.bank.window_count
         if res.u_seq is None:                       # selected model lives on another shard
             res.u_seq = np.ascontiguousarray(U[0].T)
@@ -199,3 +220,12 @@ class LLAMPC:
         self.u_prev = res.u_seq[:, 0].copy()
         self.t += 1
         return res
+
+    def close(self):
+        self.nominal_bank.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -41,6 +41,7 @@ class PlanResult:
     window_mean: np.ndarray | None = None
     costs: np.ndarray | None = None
     raw: object = None              # the llampc_plan_out record
+    nominal: bool = False           # LLAMPC warm-up tick: planned with the nominal model
 
 
 def result_from_out(o: nat.PlanOut, U=None, **extra) -> PlanResult:
@@ -48,13 +49,16 @@ def result_from_out(o: nat.PlanOut, U=None, **extra) -> PlanResult:
     if d.get("status", 0):
         raise nat.NativeError(f"tick record status {d['status']}: the in-launch completion timed out")
     full = d["window_full"] and d["lb_best"] >= 0
+    # the record pads top-K with -1 when the bank holds fewer than K models; argsort()[:K]
+    # (rt.py:360) returns only those n entries
+    kk = int(np.count_nonzero(d["topk"] >= 0)) if full else 0
     u_seq = None
     if U is not None and d["sel_cand"] >= 0:
         u_seq = np.ascontiguousarray(np.asarray(U)[d["sel_cand"]].T)
     return PlanResult(
         best_model=int(d["sel_model"]), window_full=full, window_count=d["window_count"],
-        topk=d["topk"] if full else None, topk_err=d["topk_val"] if full else None,
-        topk_Df=d["topk_Df"] if full else None, topk_Dr=d["topk_Dr"] if full else None,
+        topk=d["topk"][:kk] if full else None, topk_err=d["topk_val"][:kk] if full else None,
+        topk_Df=d["topk_Df"][:kk] if full else None, topk_Dr=d["topk_Dr"][:kk] if full else None,
         best_cand=int(d["sel_cand"]), u_seq=u_seq, cost=float(d["sel_cost"]),
         global_best=(int(d["la_best_model"]), int(d["la_best_cand"]), float(d["la_best_cost"])),
         n_nonfinite=int(d["n_nonfinite"]), raw=o, **extra)

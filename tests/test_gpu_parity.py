@@ -319,6 +319,12 @@ def test_lookahead_euler_nlp_and_rk6(nat):
         close(r["costs"].ravel(), O.mpc_cost(traj, U, xref, np.zeros(2), Q, R, P), RTOL_ROLL)
         x0b = np.array([0.1, 0.2, 0.3, 1.0, 0.01, 0.2])
         r6 = b.lookahead(x0b, U, xref, np.zeros(2), Ts=TS, integrator="rk6", return_costs=True)
+    # Dynamic.casadi always uses the pwm motor model and the Pacejka tires
+    # (dynamic.py:214-218): the NLP-form look-ahead ignores input_acc / approx
+    for flags in ({"input_acc": True}, {"approx": True}):
+        with ModelBank(p, device=0, **flags) as b2:
+            r2 = b2.lookahead(x0, U, xref, np.zeros(2), Ts=TS, integrator="euler_nlp", return_costs=True)
+        np.testing.assert_array_equal(r2["costs"], r["costs"], err_msg=str(flags))
     # RK6 reference: the oracle's scalar odeintRK6 restatement per model (first 20 models)
     for n in range(20):
         v = O.Vehicle.from_params(O.orca_params(), **{k: p[i, n] for i, k in enumerate(O.BANK_ORDER)})
@@ -430,6 +436,64 @@ def test_closed_loop_lookback_and_mu_vs_golden(nat):
                     cur, topk = r["best"], r["topk"]
                     np.testing.assert_array_equal(topk, g["topk"][idt])
             assert cur == g["current"][idt]
+
+
+@pytest.mark.parametrize("N", [300, 6])
+def test_llampc_controller_closed_loop_vs_oracle(nat, monkeypatch, N):
+    """The LLAMPC tick loop in closed loop with an RK6 plant (friction dropping): while the
+    window fills (tick <= W) every tick plans with the NOMINAL model (the reference's
+    nlp_initial, rt.py:207, 300-301), afterwards with the look-back's selection
+    (nlp_bank[current_model_idx], rt.py:303).  Each tick's chosen candidate and cost equal
+    the oracle's (rollout_rk4 + mpc_cost + feasibility on the same xref and candidates);
+    mu-hat follows the oracle window's top-K.  N = 6 < K checks that the -1 padding of
+    top-K never enters mu-hat (argsort()[:K] has n entries, rt.py:360)."""
+    import llampc.mpc.controller as ctl_mod
+    from llampc.mpc import LLAMPC, ModelBank, generate_bank
+    from llampc.tracks import ETHZ
+    d = golden("dyn_slice.npz")
+    p = O.orca_params()
+    C, H, W, K = 8, 20, 4, 10
+    bank_p = generate_bank(N, seed=21)
+    nominal = np.array([[p[k]] for k in O.BANK_ORDER])
+    xrefs, Us = [], []
+    cs = ctl_mod.ConstantSpeed
+    monkeypatch.setattr(ctl_mod, "ConstantSpeed", lambda *a, **k: (lambda r: (xrefs.append(r[0]), r)[1])(cs(*a, **k)))
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    plant = O.Vehicle.from_params(p)
+    win = O.LookbackWindow(N, W, K)
+    x = d["states"][:, 0].copy()
+    cur = 0
+    with ModelBank(bank_p, W=W, device=0) as b, LLAMPC(b, ETHZ(), H=H, C=C, K=K) as ctl:
+        gen = ctl.gen
+        ctl.gen = lambda prev, up: (lambda U: (Us.append(U), U)[1])(gen(prev, up))
+        x_prev = u_prev = None
+        for t in range(W + 6):
+            res = ctl.tick(x)
+            if t >= 2:                                   # oracle look-back on (x_{t-1}, u_{t-1}) -> x_t
+                pred = O.evaluate_models_vectorized(shared(), tuple(bank_p), x_prev, u_prev, TS)
+                win.push(O.lookback_errors(pred, x))
+                if win.count >= W:
+                    cur = win.current
+                    kk = min(N, K)
+                    np.testing.assert_array_equal(res.topk, win.best_k[:kk])
+            assert res.nominal == (t <= W)
+            cols = nominal if t <= W else bank_p[:, cur:cur + 1]
+            U, xref = Us[-1], xrefs[-1]
+            uprev = np.zeros(2) if u_prev is None else u_prev
+            cref = O.mpc_cost(O.rollout_rk4(shared(), tuple(cols), x, U, TS), U, xref, uprev, Q, R, P)
+            ok = O.candidates_feasible(U, uprev, [-0.1, -0.35], [1.0, 0.35], 5.0, TS)
+            cref = np.where(ok & ~np.isnan(cref), cref, np.inf)
+            assert res.best_cand == int(np.argmin(cref)), (t, res.best_cand, cref)
+            np.testing.assert_allclose(res.cost, cref[res.best_cand], rtol=RTOL_ROLL)
+            if t > W:
+                assert res.best_model == cur
+                np.testing.assert_allclose(ctl.mu.dr_hist[-1], np.mean(bank_p[5][win.best_k[:min(N, K)]]), rtol=1e-12)
+            u = res.u_seq[:, 0]
+            np.testing.assert_array_equal(u, U[res.best_cand, 0])
+            plant.Df *= 1 - 1 / 260.0
+            plant.Dr *= 1 - 1 / 260.0
+            xn, _ = O.sim_continuous(plant, x, u.reshape(2, 1), [0, TS])
+            x_prev, u_prev, x = x, u.copy(), xn[:, -1]
 
 
 @pytest.mark.parametrize("N,H,track", [(10000, 20, "ETHZ"), (10000, 40, "ETHZMobil"), (80000, 20, "ETHZ")])
@@ -637,6 +701,39 @@ def test_polled_completion_equals_ticket_completion(nat):
         finally:
             a_bank.close()
             b_bank.close()
+
+
+def test_poll_bound_scales_with_launch_work(nat, monkeypatch):
+    """The polled completion's wait bound grows with the launch's rollout steps
+    (poll_bound_ticks: floor + 40 ns per step), so a valid long look-ahead is never reported
+    as a timeout.  With the floor cut to 1 ms (LLAMPC_POLL_BOUND_S) a ~10 ms tick (N=1e5,
+    C=64, H=40) still returns status 0 through the default per-step term; with the per-step
+    term off as well it reports LLAMPC_STATUS_POLL_TIMEOUT — the bound is live — and the
+    bank keeps working afterwards."""
+    from llampc import _native
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    N, C, H = 100_000, 64, 40
+    rng = np.random.RandomState(11)
+    U = np.repeat(u[:, 1:1 + H].T[None], C, axis=0)
+    U[1:] += rng.uniform(-0.02, 0.02, U[1:].shape)
+    xref = s[:2, 1:H + 2]
+    args = (s[:, 0], u[:, 0], s[:, 1], U, xref, u[:, 0])
+    with ModelBank(generate_bank(N, seed=12), W=3, device=0) as b:
+        ref = b.plan_raw(*args, K=5, current_model=1)[0]
+        monkeypatch.setenv("LLAMPC_POLL_BOUND_S", "0.001")
+        b.reset()
+        o = b.plan_raw(*args, K=5, current_model=1)[0]
+        _same_records(o, ref)
+        monkeypatch.setenv("LLAMPC_POLL_STEP_NS", "0")
+        b.reset()
+        with pytest.raises(_native.NativeError, match="status 1"):
+            b.plan_raw(*args, K=5, current_model=1)
+        monkeypatch.delenv("LLAMPC_POLL_BOUND_S")
+        monkeypatch.delenv("LLAMPC_POLL_STEP_NS")
+        b.reset()
+        _same_records(b.plan_raw(*args, K=5, current_model=1)[0], ref)
 
 
 def _same_records(o, w):
