@@ -170,6 +170,16 @@ constexpr double kSinWQ[11] = {
     2.755731922398403e-06,  -2.5052108385275923e-08, 1.6059043828214877e-10,
     -7.647163453155476e-13, 2.8114514557344955e-15, -8.21985910722077e-18,
     1.950826068108976e-20,  -3.56150612064771e-23};
+// atan(t) = t + t*s*QR(s) for |t| <= tan(pi/8) (11 terms): the fast cores reduce their
+// ratio r in [0, 1] by atan(r) = pi/4 + atan((r - 1)/(r + 1)) when r > tan(pi/8), so the
+// polynomial is half as long as QA's on [0, 1] for 6 more instructions
+// (tools/fit_fastmath.py; -DLLAMPC_ATAN_FULL keeps the 22-term core for A/B runs).
+constexpr double kAtanR[11] = {
+    -0.3333333333333333,    0.1999999999999552,     -0.14285714284666542,
+    0.11111111015256361,    -0.09090904578123903,   0.07692183190826087,
+    -0.06664511447381948,   0.0585814891280221,     -0.0508544973794026,
+    0.03923165829558719,    -0.01917688711906226};
+constexpr double kTanPi8 = 0.41421356237309503;
 constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 4 ulp up to
                                        // |a| = 2, then <= 2^-49 absolute (cancellation)
 
@@ -178,14 +188,29 @@ constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 4 
 // VGPR constant for free, while a rematerialised 64-bit constant costs two v_mov/s_mov
 // issue slots per use — 2.5x on a Horner chain in the one-wave-per-SIMD regime.
 struct FmK {
-  double at[22], sw[11], sq[7], cq[7];
+#ifdef LLAMPC_ATAN_FULL
+  double at[22];
+#else
+  double ar[11];
+  double tp8, pio4;
+#endif
+  double sw[11], sq[7], cq[7];
   double pio2, two_pi, cw0, cw1, cw2, sixth, six, rmagic, rmagic2, one;
 
   __device__ __forceinline__ static void pin(double& x) { asm volatile("" : "+v"(x)); }
   __device__ __forceinline__ static FmK load() {
     FmK k;
+#ifdef LLAMPC_ATAN_FULL
 #pragma unroll
     for (int i = 0; i < 22; ++i) { k.at[i] = kAtanQ[i]; pin(k.at[i]); }
+#else
+#pragma unroll
+    for (int i = 0; i < 11; ++i) { k.ar[i] = kAtanR[i]; pin(k.ar[i]); }
+    k.tp8 = kTanPi8;
+    k.pio4 = kPio4;
+    pin(k.tp8);
+    pin(k.pio4);
+#endif
 #pragma unroll
     for (int i = 0; i < 11; ++i) { k.sw[i] = kSinWQ[i]; pin(k.sw[i]); }
 #pragma unroll
@@ -287,9 +312,23 @@ __device__ __forceinline__ double vmin_abs2(double a, double b) {  // min(|a|, |
   return r;
 }
 
-__device__ __forceinline__ double atan_core_k(double t, const FmK& K) {
+// atan(n / d) for 0 <= n <= d, d in [2^-1001, 2^1000].  Reduced form: s = n > tan(pi/8) d
+// selects t = (n - d)/(n + d) and the offset pi/4 (sf = 1.0 or 0.0: the select is the high
+// word only), so the polynomial covers |t| <= tan(pi/8).  n - d and n + d are rounded once
+// each (relative 2^-53 on t); the offset add rounds once: <= 2 ulp before the callers'
+// fix-ups (tests: test_fast_cores_ulp_on_domain).
+__device__ __forceinline__ double atan_ratio_k(double n, double d, const FmK& K) {
+#ifdef LLAMPC_ATAN_FULL
+  const double t = div_fast(n, d);
   const double s = t * t;
   return fma(t * s, horner<22>(K.at, s), t);
+#else
+  const bool red = n > K.tp8 * d;
+  const double sf = __hiloint2double(red ? 0x3FF00000 : 0, 0);
+  const double t = div_fast(fma(-sf, d, n), fma(sf, n, d));
+  const double s = t * t;
+  return fma(sf, K.pio4, fma(t * s, horner<11>(K.ar, s), t));
+#endif
 }
 
 // atan2(y, x) for x >= 0 on the domain atan2_fast_ok(y, x): the sum |y| + x in
@@ -304,7 +343,7 @@ __device__ __host__ __forceinline__ bool atan2_fast_ok(double y, double x) {
 __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K, double& hi) {
   const double ay = fabs(y);
   hi = vmax_abs2(y, x);
-  const double r = atan_core_k(div_fast(vmin_abs2(y, x), hi), K);
+  const double r = atan_ratio_k(vmin_abs2(y, x), hi, K);
   const double o = (ay > fabs(x)) ? K.pio2 - r : r;   // no pi/2 tail: <= 2 ulp (measured)
   return copysign(o, y);
 }
@@ -320,7 +359,7 @@ __device__ __host__ __forceinline__ bool atan_fast_ok(double z) { return fabs(z)
 __device__ __forceinline__ double atan_fast(double z, const FmK& K, double& hz) {
   const double az = fabs(z);
   hz = vmax_abs(z, K.one);
-  const double r = atan_core_k(div_fast(vmin_abs(z, K.one), hz), K);
+  const double r = atan_ratio_k(vmin_abs(z, K.one), hz, K);
   const double o = (az > 1.0) ? K.pio2 - r : r;   // no pi/2 tail: <= 2 ulp (measured)
   return copysign(o, z);
 }

@@ -69,6 +69,14 @@ for nS in (7, 8, 9):
 cS, _ = fit(QS, 0, r4 * r4, 8)
 cC, _ = fit(QC, 0, r4 * r4, 8)
 
+# reduced atan of the rollout's fast cores: |t| <= tan(pi/8) after
+# atan(r) = pi/4 + atan((r - 1)/(r + 1)) for r > tan(pi/8) (fastmath.hpp atan_red)
+T8 = mp.tan(mp.pi / 8)
+for nR in (9, 10, 11, 12):
+    cR, eR = fit(QA, 0, T8 * T8, nR)
+    print(f"QR n={nR} chebyfit err {float(eR):.3e}", file=sys.stderr)
+cR, _ = fit(QA, 0, T8 * T8, 11)
+
 cW, eW = fit(QS, 0, 9.0, 11)
 print(f"QW n=11 chebyfit err {float(eW):.3e}", file=sys.stderr)
 
@@ -76,6 +84,18 @@ atan_f = lambda t, c: t + t * (t * t) * horner(c, t * t)
 sin_f = lambda r, c: r + r * (r * r) * horner(c, r * r)
 cos_f = lambda r, c: 1 - (r * r) / 2 + (r * r) ** 2 * horner(c, r * r)
 check("atan [0,1]", cA, atan_f, mp.atan, 1e-8, 1.0)
+check("atan_red [0,tan(pi/8)]", cR, atan_f, mp.atan, 1e-8, float(T8))
+
+
+def atan_red_f(r, c):
+    s = r > float(T8)
+    num = np.where(s, r - 1.0, r)
+    den = np.where(s, r + 1.0, 1.0)
+    t = num / den
+    return np.where(s, float(mp.pi / 4), 0.0) + atan_f(t, c)
+
+
+check("atan_red reduced [0,1]", cR, atan_red_f, mp.atan, 1e-8, 1.0)
 check("sin [0,pi/4]", cS, sin_f, mp.sin, 1e-8, r4)
 check("cos [0,pi/4]", cC, cos_f, mp.cos, 0.0, r4)
 check("sin [0,2]", cW, sin_f, mp.sin, 1e-8, 2.0)
@@ -86,6 +106,8 @@ def emit(name, c):
     print(f"constexpr double {name}[{len(c)}] = {{\n    {body}}};")
 
 emit("kAtanQ", cA)
+emit("kAtanR", cR)
+print(f"constexpr double kTanPi8 = {float(T8)!r};")
 emit("kSinQ", cS)
 emit("kCosQ", cC)
 emit("kSinWQ", cW)
