@@ -227,6 +227,23 @@ __device__ __forceinline__ double dpp_bcast(double v) {
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
+// The same quad_perm through the LDS crossbar (ds_swizzle_b32, QDMode: offset bit 15 set,
+// bits 7:0 = the quad_perm selector, the DPP encoding): issued to the LDS pipe instead of
+// the VALU (a v_mov_b32_dpp costs ~8 VALU cycles), longer latency.  LLAMPC_SWZ_MASK selects
+// which of the quad's four broadcasts (bit 0 Ffy, 1 Fry, 2 sp, 3 cp) take this route (A/B).
+#ifndef LLAMPC_SWZ_MASK
+#define LLAMPC_SWZ_MASK 0
+#endif
+template <int CTRL, int BIT>
+__device__ __forceinline__ double quad_bcast(double v) {
+  if constexpr (((LLAMPC_SWZ_MASK >> BIT) & 1) != 0) {
+    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x8000 | CTRL);
+    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x8000 | CTRL);
+    return __hiloint2double(hi, lo);
+  } else {
+    return dpp_bcast<CTRL>(v);
+  }
+}
 // quad_perm broadcasts within lane pairs: [0,0,2,2] = 0xA0, [1,1,3,3] = 0xF5; within a
 // quad: lane q to all four = 0x00, 0x55, 0xAA, 0xFF; xor-1 / xor-2 swaps = 0xB1, 0x4E.
 constexpr int kPair0 = 0xA0, kPair1 = 0xF5;
@@ -257,12 +274,14 @@ __device__ __host__ __forceinline__ bool chain_static_ok(const Chain& c) {
 
 // Running extremes of the fast cores' operands over a rollout (or a look-back step): the
 // domain is judged once at the end instead of per stage (a compare + mask OR per operand
-// cost ~15 issue slots per stage).  hi = max of the atan2 divisors max(|y|, x) and of the
-// atan divisors max(|z|, 1); lo = min of the atan2 divisors; ps = max |psi|.  ok(): every
-// operand inside the fast domains (atan2: hi in [2^-1000, 2^999] implies |y| + x in
-// [2^-1000, 2^1000]; atan: |z| <= 2^999; sincos: |psi| <= kSinCosMax).  fmax/fmin skip a
-// NaN operand, but a NaN operand comes from a NaN state, input or parameter and reaches the
-// lane's result (the caller also requires a finite result).
+// cost ~15 issue slots per stage).  hi / lo = max / min of the atan2 divisors max(|y|, x);
+// ps = max |psi|.  ok(): hi in [2^-1000, 2^999] (a larger divisor's reciprocal may flush to
+// zero: a wrong finite angle; a smaller one — 0/0 at standstill — gives a NaN that the atan
+// core's min/max would swallow) and |psi| <= kSinCosMax (the fold's range).  The atan
+// divisor max(|z|, 1) needs no record: |z| > 2^1000 yields pi/2 exactly as atan does and an
+// infinite z a NaN that reaches the state (and, through the positions, the cost); the
+// callers re-run every lane whose result is not finite.  fmax/fmin skip a NaN operand, but
+// a NaN operand comes from a NaN state, input or parameter and reaches the lane's result.
 struct Dom {
   double hi, lo, ps;
   __device__ __forceinline__ void init() {
@@ -281,12 +300,12 @@ struct Dom {
 __device__ __forceinline__ double chain_fast(const Chain& c, double den, double vy, double om,
                                              double dsel, Dom& dm, const fm::FmK& K) {
   const double yy = fma(c.lw, om, c.sg * vy);
-  double h2, hz;
+  double h2;
   const double a2 = fm::atan2_fast(yy, den, K, h2);
   const double z = c.B * fma(-c.sg, a2, dsel);
-  const double at = fm::atan_fast(z, K, hz);
+  const double at = fm::atan_fast(z, K);
   dm.lo = fm::vmin(dm.lo, h2);
-  dm.hi = fm::vmax(dm.hi, fm::vmax(h2, hz));
+  dm.hi = fm::vmax(dm.hi, h2);
   return c.D * fm::sin_wide(c.C * at, K);
 }
 
@@ -318,12 +337,12 @@ __device__ __forceinline__ double chain_fold(const Chain& c, double den, double 
   {
 #endif
     const double yy = fma(c.lw, om, c.sg * vy);
-    double h2, hz;
+    double h2;
     const double a2 = fm::atan2_fast(yy, den, K, h2);
     const double z = fma(c.nsB, a2, Bd);                  // B (dsel - sg a2)
-    at = fm::atan_fast(z, K, hz);
+    at = fm::atan_fast(z, K);
     dm.lo = fm::vmin(dm.lo, h2);
-    dm.hi = fm::vmax(dm.hi, fm::vmax(h2, hz));
+    dm.hi = fm::vmax(dm.hi, h2);
   }
   return c.D * fm::sin_wide(fma(c.C, at, arg_psi), K);
 }
@@ -388,14 +407,14 @@ __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, doub
   dm.ps = fm::vmax_abs(psi, dm.ps);
   if (LPM == 4) {
     const double r = chain_fold(sk.ch[0], den, vy, om, Bd, psi, sk.ra, sk.pm, sk.po, dm, K);
-    f.Ffy = dpp_bcast<kQuad0>(r);
-    f.Fry = dpp_bcast<kQuad1>(r);
+    f.Ffy = quad_bcast<kQuad0, 0>(r);
+    f.Fry = quad_bcast<kQuad1, 1>(r);
     if constexpr (SPLIT) {
-      f.sp = dpp_bcast<kQuadPosA>(r);
-      f.cp = dpp_bcast<kQuadPosB>(r);
+      f.sp = quad_bcast<kQuadPosA, 2>(r);
+      f.cp = quad_bcast<kQuadPosB, 3>(r);
     } else {
-      f.sp = dpp_bcast<kQuad2>(r);
-      f.cp = dpp_bcast<kQuad3>(r);
+      f.sp = quad_bcast<kQuad2, 2>(r);
+      f.cp = quad_bcast<kQuad3, 3>(r);
     }
     return f;
   }
