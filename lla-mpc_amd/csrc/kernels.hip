@@ -351,21 +351,61 @@ __device__ __forceinline__ double sq_err4(const double* x, const double* xn) {
   return s;
 }
 
+// Order-preserving u64 of a window mean for the argsort order (rt.py:360): -0 -> +0 and
+// every NaN -> one canonical NaN above +inf.
+__device__ __forceinline__ uint64_t order_key(double w) {
+  const double wc = (w != w) ? __builtin_nan("") : w + 0.0;
+  const uint64_t b = (uint64_t)__double_as_longlong(wc);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+// A top-K entry in LDS: its key, its local model index (ids from kNoModelId up mark lanes
+// without a model: unique per slot, above every real index since n <= INT32_MAX) and value.
+constexpr uint32_t kNoModelId = 0xFFFFFE00u;
+struct BEnt {
+  uint64_t key;
+  uint32_t id;
+  uint32_t pos;
+  double v;
+};
+// (key, id, pos) order: total, so every rank below is unique.
+__device__ __forceinline__ bool bless(const BEnt& a, const BEnt& b) {
+  return (int)(a.key < b.key) |
+         ((int)(a.key == b.key) & ((int)(a.id < b.id) | ((int)(a.id == b.id) & (int)(a.pos < b.pos))));
+}
+constexpr int kBlockMergeBytes = kWaves * LLAMPC_KMAX * (int)sizeof(BEnt);
+
+// The block's sorted top-K from its waves' lists (kWaves x K entries staged in LDS by
+// wave_topk_rank or the R > 1 rounds): the first kWaves*K threads rank their entry among
+// them and the ones ranked below K store it in the block's list tk_val/tk_idx[blk][K] —
+// one list per block for lb_final (its merge cost grows with the lists' count).
+__device__ __forceinline__ void block_topk_merge(const LookbackLaunch& a, int blk, const BEnt* e) {
+  const int M = kWaves * a.K;
+  const int t = threadIdx.x;
+  if (t < M) {
+    const BEnt me = e[t];
+    int rank = 0;
+    for (int j = 0; j < M; ++j) rank += (int)bless(e[j], me);
+    if (rank < a.K) {
+      st_wt(&a.tk_val[(int64_t)blk * a.K + rank], me.v);
+      st_wt(&a.tk_idx[(int64_t)blk * a.K + rank], me.id >= kNoModelId ? kNoIndex : a.goff + (int64_t)me.id);
+    }
+  }
+}
+
 // The sorted top-K of one wave's 64 window means (R == 1) by rank: every lane counts the
 // lanes whose (value, index) key precedes its own — NaN last, ties to the lower index
 // (rt.py:360 argsort order) — and the lanes ranked below K store their entry at that rank.
 // Keys as order-preserving u64 (+0 for -0, one canonical NaN above +inf); lanes without a
 // model take a key above every model's (kNoIndex entries at the end of a short list).
-__device__ __forceinline__ void wave_topk_rank(const LookbackLaunch& a, int64_t list, double w,
-                                               int64_t n, unsigned char* lds) {
+// The wave's list goes to out[rank] (LDS, block_topk_merge).
+__device__ __forceinline__ void wave_topk_rank(const LookbackLaunch& a, double w, int64_t n,
+                                               unsigned char* lds, BEnt* out) {
   const int lane = threadIdx.x & 63;
   uint64_t* keys = reinterpret_cast<uint64_t*>(lds + (threadIdx.x >> 6) * kRankBytes);
   uint32_t* ids = reinterpret_cast<uint32_t*>(keys + 64);
   const bool valid = n < a.n;
-  const double wc = (w != w) ? __builtin_nan("") : w + 0.0;
-  const uint64_t b = (uint64_t)__double_as_longlong(wc);
-  const uint64_t key = !valid ? ~0ull : ((b >> 63) ? ~b : (b | 0x8000000000000000ull));
-  const uint32_t id = valid ? (uint32_t)n : 0xFFFFFF00u + (uint32_t)lane;
+  const uint64_t key = valid ? order_key(w) : ~0ull;
+  const uint32_t id = valid ? (uint32_t)n : kNoModelId + (uint32_t)threadIdx.x;
   keys[lane] = key;
   ids[lane] = id;
   __syncthreads();
@@ -376,10 +416,7 @@ __device__ __forceinline__ void wave_topk_rank(const LookbackLaunch& a, int64_t 
     const uint32_t ij = ids[j];
     rank += (int)(kj < key) | ((int)(kj == key) & (int)(ij < id));
   }
-  if (rank < a.K) {
-    st_wt(&a.tk_val[list * a.K + rank], valid ? w : __builtin_nan(""));
-    st_wt(&a.tk_idx[list * a.K + rank], valid ? a.goff + n : kNoIndex);
-  }
+  if (rank < a.K) out[rank] = BEnt{key, id, 0u, valid ? w : __builtin_nan("")};
 }
 
 // ------------------------------------------------------------------------------------
@@ -454,8 +491,13 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     st_wt(&a.am_idx[list], li == kNoLocal ? kNoIndex : a.goff + li);
   }
   LB_STAMP(blk, 2);
+  unsigned char* rank_lds = reinterpret_cast<unsigned char*>(sc.sv) + kScratchBytes;
+  BEnt* wl = reinterpret_cast<BEnt*>(rank_lds + kWaves * kRankBytes);   // [kWaves][K]
+  BEnt* mine = wl + (threadIdx.x >> 6) * a.K;
   if (a.R == 1) {                       // launch-uniform
-    wave_topk_rank(a, list, wm0, base + threadIdx.x, reinterpret_cast<unsigned char*>(sc.sv) + kScratchBytes);
+    wave_topk_rank(a, wm0, base + threadIdx.x, rank_lds, mine);
+    __syncthreads();
+    block_topk_merge(a, blk, wl);
     LB_STAMP(blk, 3);
     return;
   }
@@ -476,12 +518,15 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     }
     wave_pick_nl(cv, cl);
     if (lane == 0) {
-      st_wt(&a.tk_val[list * a.K + k], cv);
-      st_wt(&a.tk_idx[list * a.K + k], cl == kNoLocal ? kNoIndex : a.goff + cl);
+      const bool none = cl == kNoLocal;
+      mine[k] = BEnt{none ? ~0ull : order_key(cv), none ? kNoModelId + (uint32_t)((threadIdx.x >> 6) * a.K + k) : cl,
+                     0u, none ? __builtin_nan("") : cv};
     }
     lv = cv;
     ll = cl;
   }
+  __syncthreads();
+  block_topk_merge(a, blk, wl);
   LB_STAMP(blk, 3);
 }
 
@@ -903,21 +948,97 @@ __device__ __forceinline__ E* tree_merge(E* buf0, E* buf1, int L, int K) {
 __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* smem) {
   STAMP(0);
   const int tid = threadIdx.x;
-  const int L = f.nb_lb * kWaves;          // one sorted K-list + argmin per look-back wave
-  const int K = f.K;
-  Ent* buf = reinterpret_cast<Ent*>(smem + kScratchBytes);
-  Ent* am = buf + L * K;                   // the lists' argmins, loaded in the same round trip
-  for (int e = tid; e < L * K; e += kBlock) buf[e] = Ent{ld_wt(&f.tk_val[e]), ld_wt(&f.tk_idx[e])};
-  for (int b = tid; b < L; b += kBlock) am[b] = Ent{ld_wt(&f.am_val[b]), ld_wt(&f.am_idx[b])};
+  const int L = f.nb_lb;                   // one sorted K-list per look-back block
+  const int La = f.nb_lb * kWaves;         // one argmin per look-back wave
+  const int K = f.K, M = L * K;
+  // LDS (SoA, contiguous scans): thr[2] | key[M] | val[M] | hk[L] | ck[M] | am[La] | id[M] |
+  // hid[L] | cid[M] | ce[M] | top[KMAX] | cnt.  Missing entries
+  // take ids above every model's, unique per position, so (key, id) is a total order.
+  uint64_t* thr = reinterpret_cast<uint64_t*>(smem + kScratchBytes);   // T: key, id
+  uint64_t* key = thr + 2;
+  double* val = reinterpret_cast<double*>(key + M);
+  uint64_t* hk = reinterpret_cast<uint64_t*>(val + M);
+  uint64_t* ck = hk + L;
+  Ent* am = reinterpret_cast<Ent*>(ck + M);    // the waves' argmins, same round trip
+  uint32_t* id = reinterpret_cast<uint32_t*>(am + La);
+  uint32_t* hid = id + M;
+  uint32_t* cid = hid + L;
+  int* ce = reinterpret_cast<int*>(cid + M);
+  int* top = ce + M;                           // [K] entry of each output rank
+  int* cnt = top + LLAMPC_KMAX;
+  auto local = [&](int64_t gi) { return gi == kNoIndex ? kNoLocal : (uint32_t)(gi - f.goff); };
+  for (int e = tid; e < M; e += kBlock) {
+    const double v = ld_wt(&f.tk_val[e]);
+    const uint32_t l = local(ld_wt(&f.tk_idx[e]));
+    const uint64_t k = l == kNoLocal ? ~0ull : order_key(v);
+    const uint32_t i = l == kNoLocal ? kNoModelId + (uint32_t)e : l;
+    key[e] = k;
+    val[e] = v;
+    id[e] = i;
+    if (e % K == 0) {
+      hk[e / K] = k;
+      hid[e / K] = i;
+    }
+  }
+  for (int b = tid; b < La; b += kBlock) am[b] = Ent{ld_wt(&f.am_val[b]), ld_wt(&f.am_idx[b])};
+  if (tid == 0) {
+    *cnt = 0;
+    thr[0] = ~0ull;                          // L < K: every entry is a candidate
+    thr[1] = 0xFFFFFFFFull;
+  }
   __syncthreads();
   STAMP(1);
-  if (tid >= 64) return;                   // one wave merges; the caller re-converges
+  // top-K of the L sorted lists without serial rounds (a wave pick per output rank cost
+  // ~1 us per rank): T = the K-th smallest list head bounds the K-th smallest entry (the K
+  // smallest heads are K entries <= T), so the top-K lies in {entries <= T} — K to a few K
+  // entries on real banks — and each candidate's rank among the candidates is its output
+  // rank.  The scans read contiguous LDS (broadcast), unrolled so loads overlap.
+  auto lt = [](uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
+    return (int)(ka < kb) | ((int)(ka == kb) & (int)(ia < ib));
+  };
+  if (L >= K) {
+    for (int h = tid; h < L; h += kBlock) {
+      const uint64_t mk = hk[h];
+      const uint32_t mi = hid[h];
+      int r = 0;
+#pragma unroll 8
+      for (int j = 0; j < L; ++j) r += lt(hk[j], hid[j], mk, mi);
+      if (r == K - 1) {
+        thr[0] = mk;
+        thr[1] = mi;
+      }
+    }
+    __syncthreads();
+  }
+  const uint64_t tk = thr[0];
+  const uint32_t ti = (uint32_t)thr[1];
+  for (int e = tid; e < M; e += kBlock) {
+    const uint64_t k = key[e];
+    const uint32_t i = id[e];
+    if (!lt(tk, ti, k, i)) {
+      const int slot = atomicAdd(cnt, 1);
+      ck[slot] = k;
+      cid[slot] = i;
+      ce[slot] = e;
+    }
+  }
+  __syncthreads();
+  const int c = *cnt;                      // >= K (the K smallest heads, or all M >= K)
+  for (int q = tid; q < c; q += kBlock) {
+    const uint64_t mk = ck[q];
+    const uint32_t mi = cid[q];
+    int r = 0;
+#pragma unroll 8
+    for (int j = 0; j < c; ++j) r += lt(ck[j], cid[j], mk, mi);
+    if (r < K) top[r] = ce[q];
+  }
+  __syncthreads();
+  if (tid >= 64) return;                   // one wave finishes; the caller re-converges
   const int lane = tid;
-  auto local = [&](int64_t id) { return id == kNoIndex ? kNoLocal : (uint32_t)(id - f.goff); };
-  // argmin over the lists' argmins (rt.py:359)
+  // argmin over the waves' argmins (rt.py:359)
   double v = f.nan_first ? __builtin_inf() : __builtin_nan("");
   uint32_t li = kNoLocal;
-  for (int b = lane; b < L; b += 64) {
+  for (int b = lane; b < La; b += 64) {
     const double bv = am[b].v;
     const uint32_t bl = local(am[b].i);
     const bool t = (int)(bl != kNoLocal) &
@@ -927,46 +1048,12 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
   }
   if (f.nan_first) wave_pick_nf(v, li);
   else wave_pick_nl(v, li);
-  // top-K: K rounds of a wave pick over the list heads.  Lane owns lists lane + 64 j
-  // (j < kListsPerLane); its read positions are 8-bit fields of one register.
-  uint64_t pos = 0;
-  double hv;
-  uint32_t hl;
-  int hj;
-  auto head = [&]() {
-    hv = __builtin_nan("");
-    hl = kNoLocal;
-    hj = 0;
-#pragma unroll
-    for (int j = 0; j < kListsPerLane; ++j) {
-      const int l = lane + 64 * j;
-      const int p = (int)((pos >> (8 * j)) & 0xFF);
-      if (l < L && p < K) {
-        const Ent e = buf[l * K + p];
-        const uint32_t el = local(e.i);
-        const bool t = (int)(el != kNoLocal) & (int)less_bf<0>(e.v, el, hv, hl);
-        hv = t ? e.v : hv;
-        hl = t ? el : hl;
-        hj = t ? j : hj;
-      }
-    }
-  };
-  head();
   double kv = __builtin_nan("");
   uint32_t kl = kNoLocal;
-  for (int k = 0; k < K; ++k) {
-    double m = hv;
-    uint32_t w = hl;
-    wave_pick_nl(m, w);
-    if (lane == k) {
-      kv = m;
-      kl = w;
-    }
-    if (w == kNoLocal) break;              // wave-uniform: every list is exhausted
-    if (hl == w) {                         // the owner (local indices are unique)
-      pos += 1ull << (8 * hj);
-      head();
-    }
+  if (lane < K) {
+    const int e = top[lane];
+    kl = id[e] >= kNoModelId ? kNoLocal : id[e];
+    kv = val[e];
   }
   STAMP(2);
   llampc_plan_out* o = f.out;
@@ -1595,8 +1682,10 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
     lbv.R = lookback_r(lb->n, std::max(1, lb->K));
     f.nb_lb = lookback_blocks_r(lb->n, lbv.R);
     if (lb->full) {
-      lds = std::max(lds, kScratchBytes + (size_t)f.nb_lb * kWaves * (lb->K + 1) * sizeof(Ent));  // lb_final
-      lds = std::max(lds, kScratchBytes + (size_t)kWaves * kRankBytes);                         // wave_topk_rank
+      const size_t M = (size_t)f.nb_lb * lb->K, L = f.nb_lb;   // lb_final (layout there)
+      lds = std::max(lds, kScratchBytes + 8 * (3 * M + L) + sizeof(Ent) * L * kWaves +
+                              4 * (3 * M + L + LLAMPC_KMAX + 2) + 8 + 16);
+      lds = std::max(lds, kScratchBytes + (size_t)kWaves * kRankBytes + kBlockMergeBytes);  // wave lists
     }
   }
   if (la) {
@@ -1616,6 +1705,7 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
   f.do_lb = lb != nullptr;
   f.do_la = la != nullptr;
   if (f.nb_lb + f.nb_la == 0) return hipErrorInvalidValue;
+
   if (pk) {
     if (!la || !plan_inline_ok(la->C, la->H, integ, la->xref_mode) || !stage) return hipErrorInvalidValue;
     if (lpm == 4) launch_plan_inl<4>(lbv, lav, f, G, cpl, lds, s, *pk);
