@@ -317,14 +317,25 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
 // c.C = C (lanes 0/1) or 0 (2/3), c.D = D or 1, ra = the |r| mask of the high word (lane 3
 // clears the sign), pm = 0 / 1 / -1 and po = 0 / 0 / pi/2 place the angle argument
 // po + pm r' (exactly 0 in lanes 0/1, so their argument is C atan(.) as at LPM 1/2).
+// SCALED: psi arrives as Psi = (2/pi) psi (the fused quad's state, step_fused): k2 = the
+// even integer nearest Psi, r = (Psi - k2) pi/2 — the subtraction is exact (|Psi| < 2^51),
+// so the fold is 4 instructions instead of the 3-part Cody-Waite's 5.
+template <bool SCALED = false>
 __device__ __forceinline__ double chain_fold(const Chain& c, double den, double vy, double om,
                                              double Bd, double psi, int ra, double pm,
                                              double po, Dom& dm, const fm::FmK& K) {
-  const double t2 = fma(psi, K.two_pi, K.rmagic2);       // 2^53 (1.5 + 2k 2^-53): ulp 2
-  const double k2 = t2 - K.rmagic2;
-  double r = fma(-k2, K.cw0, psi);
-  r = fma(-k2, K.cw1, r);
-  r = fma(-k2, K.cw2, r);
+  double t2, r;
+  if constexpr (SCALED) {
+    t2 = psi + K.rmagic2;                                // 2^53 (1.5 + 2k 2^-53): ulp 2
+    const double k2 = t2 - K.rmagic2;
+    r = (psi - k2) * K.pio2;
+  } else {
+    t2 = fma(psi, K.two_pi, K.rmagic2);
+    const double k2 = t2 - K.rmagic2;
+    r = fma(-k2, K.cw0, psi);
+    r = fma(-k2, K.cw1, r);
+    r = fma(-k2, K.cw2, r);
+  }
   const double rr = __hiloint2double(__double2hiint(r) & ra, __double2loint(r));
   const double pa = fma(pm, rr, po);
   const int fs = __double2loint(t2) << 31;               // (-1)^k on the argument
@@ -399,14 +410,14 @@ struct StageF {
 // Bd = B d fw, the chain's steering term (LPM = 4 only; formed once per step).
 // SPLIT (LPM = 4, position split): sp/cp carry the split's A/B operands instead (X lanes:
 // cos, sin; Y lanes: sin, cos — kQuadPosA/B).
-template <int LPM, bool SPLIT = false>
+template <int LPM, bool SPLIT = false, bool SCALED = false>
 __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, double vy, double om,
                                               double d, double psi, const fm::FmK& K, Dom& dm,
                                               double Bd = 0.0) {
   StageF f;
   dm.ps = fm::vmax_abs(psi, dm.ps);
   if (LPM == 4) {
-    const double r = chain_fold(sk.ch[0], den, vy, om, Bd, psi, sk.ra, sk.pm, sk.po, dm, K);
+    const double r = chain_fold<SCALED>(sk.ch[0], den, vy, om, Bd, psi, sk.ra, sk.pm, sk.po, dm, K);
     f.Ffy = quad_bcast<kQuad0, 0>(r);
     f.Fry = quad_bcast<kQuad1, 1>(r);
     if constexpr (SPLIT) {
@@ -479,12 +490,23 @@ __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::F
 struct FusedK {
   double h, hm, hIlf, hIlr, m1, m0, m2, m3;   // hm = h/m; m1 = hm k1, m0 = hm k0,
 };                                            // m2 = hm k2, m3 = -hm k3 (StageK)
-__device__ __forceinline__ FusedK make_fused(const VehK& v, const StageK& sk, double h) {
+// SCALED (the LPM = 4 quad): the rollout state carries W = h omega and Psi = (2/pi) psi
+// instead of omega and psi.  Then the yaw increment IS W (no h omega product), vy W and vx W
+// are the h vy omega / h vx omega terms of the velocity increments, the omega increment
+// takes one more factor h (hIlf, hIlr), the chains' lw / h turns W back into omega for the
+// slip angles, and the yaw's RK4 weights carry 2/pi (FmK inv_pi, two_pi, inv_3pi) — the
+// fold then needs no Cody-Waite (chain_fold<true>).  Same arithmetic up to roundings.
+__device__ __forceinline__ FusedK make_fused(const VehK& v, const StageK& sk, double h,
+                                             bool scaled = false) {
   FusedK q;
   q.h = h;
   q.hm = h * v.inv_mass;
   q.hIlf = h * v.inv_Iz * v.lf;
   q.hIlr = h * v.inv_Iz * v.lr;
+  if (scaled) {
+    q.hIlf *= h;
+    q.hIlr *= h;
+  }
   q.m1 = q.hm * sk.k1;
   q.m0 = q.hm * sk.k0;
   q.m2 = q.hm * sk.k2;
@@ -501,11 +523,12 @@ __device__ __forceinline__ void k_fused(const StageK& sk, const FusedK& q, doubl
                                         double hmsd, double hmcd, double c5a, double d, double Bd,
                                         const double* y, double* k, const fm::FmK& K, Dom& dm) {
   const double vx = y[3], vy = y[4], om = y[5];
-  const StageF f = forces_fast<LPM, SPLIT>(sk, vx, vy, om, d, y[2], K, dm, Bd);
+  constexpr bool kScaled = (LPM == 4);    // om = W = h omega, y[2] = Psi (make_fused)
+  const StageF f = forces_fast<LPM, SPLIT, kScaled>(sk, vx, vy, om, d, y[2], K, dm, Bd);
   // h sin(psi), h cos(psi): LPM = 4 lanes 2/3 scale their sine by h already (make_stage)
   const double hsp = (LPM == 4) ? f.sp : q.h * f.sp, hcp = (LPM == 4) ? f.cp : q.h * f.cp;
   const double hmFrx = fma(vx, fma(q.m3, vx, F1), F0);                     // hm Frx
-  k[2] = q.h * om;
+  k[2] = kScaled ? om : q.h * om;
   if constexpr (SPLIT) {
     k[0] = fma(vx, hsp, (sk.psg * vy) * hcp);                             // (A, B) in (sp, cp)
     k[1] = 0.0;
@@ -538,31 +561,35 @@ __device__ __forceinline__ void step_fused(const StageK& sk, const FusedK& q, do
   double y[6], k[6], acc[6];
   y[1] = acc[1] = 0.0;
   k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, x, k, K, dm);
+  // the quad's yaw is Psi = (2/pi) psi with increment W (make_fused): weights x 2/pi
+  constexpr bool kScaled = (LPM == 4);
+  const double c2 = kScaled ? K.inv_pi : 0.5, c4 = kScaled ? K.two_pi : 1.0,
+               c6 = kScaled ? K.inv_3pi : K.sixth;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (SPLIT && i == 1) continue;
     acc[i] = k[i];
-    y[i] = fma(0.5, k[i], x[i]);
+    y[i] = fma(i == 2 ? c2 : 0.5, k[i], x[i]);
   }
   k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (SPLIT && i == 1) continue;
     acc[i] = fma(2.0, k[i], acc[i]);
-    y[i] = fma(0.5, k[i], x[i]);
+    y[i] = fma(i == 2 ? c2 : 0.5, k[i], x[i]);
   }
   k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (SPLIT && i == 1) continue;
     acc[i] = fma(2.0, k[i], acc[i]);
-    y[i] = x[i] + k[i];
+    y[i] = (i == 2 && kScaled) ? fma(c4, k[i], x[i]) : x[i] + k[i];
   }
   k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, y, k, K, dm);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (SPLIT && i == 1) continue;
-    x[i] = fma(acc[i] + k[i], K.sixth, x[i]);
+    x[i] = fma(acc[i] + k[i], i == 2 ? c6 : K.sixth, x[i]);
   }
 }
 

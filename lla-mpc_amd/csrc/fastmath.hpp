@@ -196,6 +196,7 @@ struct FmK {
 #endif
   double sw[11], sq[7], cq[7];
   double pio2, two_pi, cw0, cw1, cw2, sixth, six, rmagic, rmagic2, one;
+  double inv_pi, inv_3pi;                 // (2/pi)/2, (2/pi)/6: the scaled yaw's RK4 weights
 
   __device__ __forceinline__ static void pin(double& x) { asm volatile("" : "+v"(x)); }
   __device__ __forceinline__ static FmK load() {
@@ -232,6 +233,9 @@ struct FmK {
     k.one = 1.0;
     pin(k.pio2); pin(k.two_pi); pin(k.cw0); pin(k.cw1); pin(k.cw2);
     pin(k.sixth); pin(k.six); pin(k.rmagic); pin(k.rmagic2); pin(k.one);
+    k.inv_pi = kTwoOverPi * 0.5;
+    k.inv_3pi = kTwoOverPi / 6.0;
+    pin(k.inv_pi); pin(k.inv_3pi);
     return k;
   }
 };

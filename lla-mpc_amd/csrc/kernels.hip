@@ -563,6 +563,10 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
 #pragma unroll
   for (int m = 0; m < 6; ++m) x[m] = x0[m];
   if (SPLIT) x[0] = sk.pc ? x0[1] : x0[0];
+  if (FAST && INTEG == 0 && LPM == 4) {   // the quad's scaled yaw and yaw rate (make_fused)
+    x[2] = x0[2] * K.two_pi;
+    x[5] = x0[5] * Ts;
+  }
   const double Qd = sk.pc ? q.Q[3] : q.Q[0], Pd = sk.pc ? q.P[3] : q.P[0];   // SPLIT only
   double track = 0.0, act = 0.0;
   double p0 = up0, p1 = up1;
@@ -706,7 +710,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     // stages the fused stages' input terms instead: (F0, F1, h/m sin d, h/m cos d,
     // h lf/Iz cos d, delta) — dyn.hpp fused_in, with the shared constants of make_fused.
     const fm::FmK K = fm::FmK::load();
-    const FusedK fq0 = make_fused(a.veh, make_stage<1>(a.veh, Tire{}, 0), a.Ts);
+    const FusedK fq0 = make_fused(a.veh, make_stage<1>(a.veh, Tire{}, 0), a.Ts, LPM == 4);
     for (int e = threadIdx.x; e < C * H; e += kBlock) {
       const int c = e / H, k = e - c * H;
       const double dl = a.U[2 * e + 1];
@@ -773,8 +777,12 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   const bool diagQP = a.cost.Q[1] == 0.0 && a.cost.Q[2] == 0.0 && a.cost.P[1] == 0.0 && a.cost.P[2] == 0.0;
   if (live) {
     // LPM = 2: lane 0 of the pair evaluates the front chain, lane 1 the rear (dyn.hpp)
-    const StageK sk = make_stage<LPM>(veh, t, sub, INTEG == 0 ? Ts : 1.0);
-    const FusedK fq = make_fused(veh, sk, Ts);
+    // fused RK4 quads carry W = h omega and Psi = (2/pi) psi (make_fused): the chains'
+    // lw / h turns W back into omega
+    constexpr bool kScaled = (INTEG == 0 && LPM == 4);
+    StageK sk = make_stage<LPM>(veh, t, sub, INTEG == 0 ? Ts : 1.0);
+    if (kScaled) sk.ch[0].lw = sk.ch[0].lw / Ts;
+    const FusedK fq = make_fused(veh, sk, Ts, kScaled);
     const fm::FmK K = fm::FmK::load();
     for (int j = 0; j < cpl; ++j) {
       const int c = g + j * G;
