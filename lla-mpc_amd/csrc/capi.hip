@@ -387,8 +387,12 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   f.la_tag = b->d_la_tag;
   f.blk_tag = b->d_blk_tag;
   f.seq = b->seq;
-  f.poll = poll;
-  f.poll_bound = poll_bound_ticks(la ? b->n : 0, la ? in.C : 0, la ? in.H : 0);
+  if (poll) {                           // the bound in 2^16-tick units, at least one
+    const uint64_t units = (poll_bound_ticks(b->n, in.C, in.H) + 0xFFFF) >> 16;
+    f.poll = (int32_t)std::min<uint64_t>(std::max<uint64_t>(units, 1), INT32_MAX);
+  } else {
+    f.poll = 0;
+  }
   f.host_tag = host_tag;
   f.host_seq = host_seq;
   if (la) {

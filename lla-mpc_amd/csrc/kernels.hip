@@ -1207,7 +1207,7 @@ __device__ __forceinline__ void final_select(const FinalLaunch& f, const Scratch
 // spins on its share of the tagged words — the look-ahead blocks' partials (5 words each),
 // the top-K models' and the selected model's results (3 words each) — until every word it
 // loads carries this launch's tag; one block barrier then joins them.  The blocks it waits
-// for never wait, so it cannot deadlock; a bound (f.poll_bound s_memrealtime ticks, 100 MHz,
+// for never wait, so it cannot deadlock; a bound (f.poll x 2^16 s_memrealtime ticks, 100 MHz,
 // scaled by the host with the launch's rollout steps: poll_bound_ticks in capi.hip) ends a
 // poll that could never finish (a bug) with status LLAMPC_STATUS_POLL_TIMEOUT in the record
 // instead of a hang.
@@ -1233,13 +1233,14 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
   // every thread spins on its own words (no block barrier per round: a thread's next loads
   // issue as soon as its previous ones return); one barrier after all are current
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t bound = (uint64_t)(uint32_t)f.poll << 16;
   bool late = false;
   if (mk >= 0) {
     for (;;) {
 #pragma unroll
       for (int w = 0; w < 3; ++w) kw[w] = ld_wt(&f.la_tag[w * f.n + mk]);
       if ((int)tag_ok(kw[0], f.seq) & (int)tag_ok(kw[1], f.seq) & (int)tag_ok(kw[2], f.seq)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > f.poll_bound) { late = true; break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > bound) { late = true; break; }
     }
   }
   if (ms >= 0) {
@@ -1247,7 +1248,7 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
 #pragma unroll
       for (int w = 0; w < 3; ++w) sw[w] = ld_wt(&f.la_tag[w * f.n + ms]);
       if ((int)tag_ok(sw[0], f.seq) & (int)tag_ok(sw[1], f.seq) & (int)tag_ok(sw[2], f.seq)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > f.poll_bound) { late = true; break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > bound) { late = true; break; }
     }
   }
   for (int j = 0; j < nbt; ++j) {
@@ -1260,7 +1261,7 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
         if ((int)tag_ok(r[0], f.seq) & (int)tag_ok(r[1], f.seq) & (int)tag_ok(r[2], f.seq) &
             (int)tag_ok(r[3], f.seq) & (int)tag_ok(r[4], f.seq))
           break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > f.poll_bound) { late = true; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > bound) { late = true; break; }
       }
       const double pv = __longlong_as_double((long long)join_words(r[0], r[1]));
       const int64_t pi = (int64_t)join_words(r[2], r[3]);

@@ -73,8 +73,10 @@ struct FinalLaunch {
   // blocks that never wait.  Needs look-back blocks (do_lb) to host the poller.
   const uint64_t* la_tag; const uint64_t* blk_tag;
   uint32_t seq;
+  // 0: no polling; else the poller's wait bound in units of 2^16 s_memrealtime ticks (100 MHz:
+  // 655 us per unit) — one 32-bit field, as a separate 64-bit bound cost the raceline
+  // variants SGPRs they spilled
   int32_t poll;
-  uint64_t poll_bound;                    // the poller's wait bound, s_memrealtime ticks (100 MHz)
   // host completion (llampc_plan / llampc_plan_wait): `out` is then the device alias of a
   // pinned host record, and the block that completes it stores host_seq to host_tag (pinned,
   // system scope) after a system-scope fence — the host spins on that word instead of a D2H
