@@ -204,6 +204,42 @@ def test_lookback_selection_ties_nans_many_lists(nat, N, K):
         np.testing.assert_array_equal(r["topk"][:K], g.argsort(kind="stable")[:K])
 
 
+@pytest.mark.parametrize("case", ["all_equal", "mostly_nan", "few_finite"])
+def test_lookback_topk_degenerate_banks(nat, case):
+    """lb_final's threshold merge (T = the K-th smallest block head) on degenerate banks:
+    every model identical (every key ties across all block lists: the top-K is indices
+    0..K-1), 6 of 7 models NaN (the NaN entries fill the lists' tails and, under NaN-first,
+    the argmin is the first NaN), and fewer finite models than K (NaN entries enter the
+    top-K in index order, np.argsort's NaN-last order)."""
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    N, K = 3000, 10
+    p = generate_bank(N, seed=8)
+    if case == "all_equal":
+        p[:] = p[:, [17]]
+    elif case == "mostly_nan":
+        p[2, np.arange(N) % 7 != 3] = np.nan
+    else:
+        p[2, np.arange(N) % 600 != 599] = np.nan          # 5 finite models
+    for policy in (0, 1):
+        with ModelBank(p, W=2, device=0) as b:
+            for t in range(2):
+                r = b.lookback(s[:, t], u[:, t], s[:, t + 1], Ts=TS, K=K, nan_policy=policy,
+                               return_errors=True, return_window_mean=True)
+        wm = r["window_mean"]
+        with np.errstate(all="ignore"):
+            e = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), s[:, 1], u[:, 1], TS), s[:, 2])
+        close(r["errors"], e, RTOL_STEP)
+        np.testing.assert_array_equal(r["topk"], wm.argsort(kind="stable")[:K])
+        if policy == 0:
+            assert r["best"] == int(np.argmin(wm))
+        else:
+            assert r["best"] == (int(np.nanargmin(wm)) if np.isfinite(wm).any() else 0)
+        if case == "all_equal":
+            np.testing.assert_array_equal(r["topk"], np.arange(K))
+
+
 # ----------------------------------------------------------------- look-ahead (a8-a10)
 def test_lookahead_rk4_rollout_and_cost_vs_golden(nat):
     from llampc import _native
