@@ -41,6 +41,7 @@ __device__ unsigned long long g_lb_stamps[8][8][2];   // first 8 look-back block
     }                                                                                    \
   } while (0)
 __device__ unsigned long long g_la_all[1024][4][2];    // every look-ahead block, last launch
+__device__ unsigned long long g_la_wave[1024][4];      // rollout end of every look-ahead wave
 #define LA_STAMP(blk, slot)                                                              \
   do {                                                                                   \
     if (threadIdx.x == 0) {                                                              \
@@ -235,6 +236,7 @@ __device__ __forceinline__ int wave_sum(int x) {
 // constants; left in SGPRs they overflow the 102-SGPR budget together with the
 // polynomial constants and get spilled to VGPR lanes (v_readlane reloads in the loop).
 __device__ __forceinline__ void pin_vgpr(double& x) { asm volatile("" : "+v"(x)); }
+
 
 __device__ __forceinline__ Tire load_tire(const double* p, int64_t ld, int64_t i) {
   Tire t;
@@ -827,6 +829,9 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     }
   }
   LA_STAMP(blk, 2);
+#ifdef LLAMPC_STAMPS
+  if ((threadIdx.x & 63) == 0 && blk < 1024) g_la_wave[blk][threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
+#endif
   // per-model argmin over its candidates: xor-shuffles across the model's lanes inside a
   // wave, then (a model spanning 2 or 4 waves: G*LPM in {128, 256}) across its waves in LDS
   const int span = G * LPM;
@@ -1752,6 +1757,9 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
 #ifdef LLAMPC_STAMPS
 extern "C" int llampc_debug_lb_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lb_stamps), sizeof(g_lb_stamps)) == hipSuccess ? 0 : -2;
+}
+extern "C" int llampc_debug_la_wave(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_wave), sizeof(g_la_wave)) == hipSuccess ? 0 : -2;
 }
 extern "C" int llampc_debug_la_all(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_all), sizeof(g_la_all)) == hipSuccess ? 0 : -2;

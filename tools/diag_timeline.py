@@ -57,3 +57,13 @@ rt = (Z[:, 2, 1] - Z[:, 1, 1]) / 100.0
 print(f"rollout per block: {q(rt)} us, {q(cyc)} shader cycles, clock {np.median(cyc / rt) / 1e3:.2f} GHz")
 print(f"lb_final: {us(R[0]):.2f} -> {us(R[1]):.2f} -> {us(R[2]):.2f}")
 print(f"final_select: {us(R[3]):.2f} -> {us(R[4]):.2f} -> {us(R[5]):.2f}")
+
+WV = (ctypes.c_ulonglong * (1024 * 4))()
+if hasattr(lib, "llampc_debug_la_wave"):
+    lib.llampc_debug_la_wave.argtypes = [ctypes.c_void_p]
+    lib.llampc_debug_la_wave(WV)
+    V = np.frombuffer(WV, dtype=np.uint64).reshape(1024, 4).astype(np.int64)[:nla]
+    sk = (V.max(axis=1) - V.min(axis=1)) / 100.0
+    w0 = (V - V.min(axis=1, keepdims=True)) / 100.0
+    print(f"wave rollout-end skew per block (us): {q(sk)}; mean offset of waves 0..3 from the block's first: "
+          + ", ".join(f"{x:.2f}" for x in w0.mean(axis=0)))
