@@ -217,7 +217,8 @@ int llampc_plan_async(llampc_bank* bank, const llampc_plan_in* in);
 int llampc_plan_wait(llampc_bank* bank, llampc_plan_out* out);
 /* Device pointers in `in`; d_out is a device llampc_plan_out; asynchronous on
  * `stream` (hipStream_t, NULL = the bank's stream).  d_err/d_wmean/d_cost: device
- * arrays or NULL. */
+ * arrays or NULL.  LLAMPC_E_STATE while an llampc_plan_async tick is outstanding (both
+ * would share the bank's completion state and window). */
 int llampc_plan_device(llampc_bank* bank, const llampc_plan_in* in, void* d_out,
                        double* d_err, double* d_wmean, double* d_cost, void* stream);
 
