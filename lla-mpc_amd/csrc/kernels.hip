@@ -713,11 +713,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     // h lf/Iz cos d, delta) — dyn.hpp fused_in, with the shared constants of make_fused.
     const fm::FmK K = fm::FmK::load();
     const FusedK fq0 = make_fused(a.veh, make_stage<1>(a.veh, Tire{}, 0), a.Ts, LPM == 4);
-#ifdef LLAMPC_ABL_NOSTAGE                   // diagnostic ablation only (wrong inputs)
-    for (int e = threadIdx.x; e < 0; e += kBlock) {
-#else
     for (int e = threadIdx.x; e < C * H; e += kBlock) {
-#endif
       const int c = e / H, k = e - c * H;
       const double dl = a.U[2 * e + 1];
       double sd, cd;

@@ -665,6 +665,38 @@ def test_lookahead_out_of_domain_fallback(nat):
     close(r["costs"].ravel(), O.mpc_cost(traj, U, xref, np.zeros(2), Q, R, P), RTOL_ROLL)
 
 
+def test_plan_device_refused_while_async_outstanding(nat):
+    """llampc_plan_device returns LLAMPC_E_STATE while an llampc_plan_async tick is
+    outstanding on the bank (both would share its completion state and window), and runs
+    once llampc_plan_wait has returned."""
+    import ctypes
+    import torch
+    from llampc import _native
+    from llampc.mpc import generate_bank
+    from llampc.mpc.sharded import ShardedBank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    H = 20
+    U = np.tile(u[:, 1], (H, 1))[None]
+    xref = s[:2, 1:H + 2]
+    sb = ShardedBank(generate_bank(500, seed=2), 0, 1, 0, W=3)
+    try:
+        staged = sb.stage(s[:, 0], u[:, 0], s[:, 1], U, xref, u[:, 0])
+        pin = sb.make_plan_in(staged["pack"], 1, H, K=5)
+        lib = _native.load()
+        sb.bank.plan_async(s[:, 0], u[:, 0], s[:, 1], U, xref, u[:, 0], K=5)
+        rc = lib.llampc_plan_device(sb.bank.handle, ctypes.byref(pin), sb.d_local.data_ptr(), None, None, None,
+                                    sb.stream.cuda_stream)
+        assert rc == _native.E_STATE, rc
+        out = sb.bank.plan_wait()
+        assert out.status == 0
+        sb.launch(pin)
+        torch.cuda.synchronize()
+        assert sb.fetch().best_cand == 0
+    finally:
+        sb.close()
+
+
 def test_plan_async_two_banks(nat):
     """llampc_plan_async / llampc_plan_wait: two banks (two tracks) in flight together give
     the same records as the blocking llampc_plan; a second async tick on a busy bank and a
