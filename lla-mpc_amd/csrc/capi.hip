@@ -153,6 +153,7 @@ struct llampc_bank {
   bool async_pending = false;      // llampc_plan_async issued, llampc_plan_wait not yet
   double* d_rl = nullptr;          // raceline table: knots | xy | speed | mus
   int32_t rl_n = 0, rl_M = 0;
+  double rl_hmin = 1.0, rl_vmax = 0.0;   // the walkers' speed-window bounds (raceline.hpp)
   double* d_xref_pm = nullptr;     // per-model references [n][H][2] (RACELINE ticks)
   size_t xref_pm_cap = 0;
   int64_t timing_seen[3] = {0, 0, 0};
@@ -355,6 +356,9 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
       lal.rl.mus = lal.rl.speed + 4 * m * b->rl_M;
       lal.rl.n = b->rl_n;
       lal.rl.M = b->rl_M;
+      lal.rl.hmin = b->rl_hmin;
+      lal.rl.vmax = b->rl_vmax;
+      lal.rl.wcap = 0;                    // set by launch_plan from the LDS it leaves
       lal.xref_pm = b->d_xref_pm;       // sized by ensure_xref_pm before the launch
     }
   }
@@ -746,7 +750,7 @@ int llampc_bank_set_raceline(llampc_bank* b, const double* knots, int32_t n, con
                              const double* speed, const double* mus, int32_t M) {
   if (!b || !knots || !xy || !speed || !mus) return fail(LLAMPC_E_ARG, "NULL argument");
   if (n < 2 || M < 1 || M > 64) return fail(LLAMPC_E_ARG, "n=%d (>= 2) M=%d (1..64)", n, M);
-  if (raceline_lds_bytes(n) > 60 * 1024)
+  if (raceline_lds_bytes(n, M) > 60 * 1024)
     return fail(LLAMPC_E_ARG, "raceline of %d knots exceeds the 60 KB LDS stage", n);
   for (int32_t i = 1; i < n; ++i)
     if (!(knots[i] > knots[i - 1])) return fail(LLAMPC_E_ARG, "knots must increase (at %d)", i);
@@ -769,6 +773,10 @@ int llampc_bank_set_raceline(llampc_bank* b, const double* knots, int32_t n, con
   HIP_TRY(hipMemcpy(d + n + 8 * m + 4 * m * M, mus, M * sizeof(double), hipMemcpyHostToDevice));
   b->rl_n = n;
   b->rl_M = M;
+  double hmin = knots[1] - knots[0];
+  for (int32_t i = 2; i < n; ++i) hmin = std::min(hmin, knots[i] - knots[i - 1]);
+  b->rl_hmin = hmin;
+  b->rl_vmax = speed_bound(knots, speed, n, M);
   return LLAMPC_OK;
 }
 

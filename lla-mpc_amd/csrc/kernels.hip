@@ -42,6 +42,12 @@ __device__ unsigned long long g_lb_stamps[8][8][2];   // first 8 look-back block
   } while (0)
 __device__ unsigned long long g_la_all[1024][4][2];    // every look-ahead block, last launch
 __device__ unsigned long long g_la_wave[1024][4];      // rollout end of every look-ahead wave
+__device__ double g_rl_dbg[8];                          // raceline window decision (block 0)
+__device__ unsigned long long g_rl_ph[1024][4];         // raceline prologue phases per block
+#define RL_STAMP(blk, slot)                                                              \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && (blk) < 1024) g_rl_ph[blk][slot] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define LA_STAMP(blk, slot)                                                              \
   do {                                                                                   \
     if (threadIdx.x == 0) {                                                              \
@@ -70,6 +76,9 @@ __device__ unsigned long long g_la_wave[1024][4];      // rollout end of every l
   do {              \
   } while (0)
 #define LA_STAMP(blk, slot) \
+  do {                      \
+  } while (0)
+#define RL_STAMP(blk, slot) \
   do {                      \
   } while (0)
 #define LB_STAMP(blk, slot) \
@@ -652,6 +661,28 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   return J;
 }
 
+// Global -> LDS copy of `count` doubles with B loads in flight per thread: a plain strided
+// loop waits one memory round trip per element — ~25 per thread for the ETHZ spline table
+// (50 KB per block), which made the raceline prologue ~25 us.  src(e) gives element e; it
+// is called for e = threadIdx.x + j kBlock in order, j < B per batch, past count too (with
+// e clamped to count - 1: unguarded loads, no branch per element; those are not stored).
+template <int B = 16, typename Src>
+__device__ __forceinline__ void copy_lds(double* dst, int count, Src src) {
+  for (int base = threadIdx.x; base < count; base += B * kBlock) {
+    double v[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int e = base + j * kBlock;
+      v[j] = src(e < count ? e : count - 1);
+    }
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int e = base + j * kBlock;
+      if (e < count) dst[e] = v[j];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Look-ahead body.  Lane layout inside a block: sub = lane % LPM (LPM = 2: the lane pair
 // of one rollout, front/rear chain), cl = lane / LPM; G candidate-lanes per model (power of two); a model's
@@ -674,6 +705,10 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   const int g = cl & (G - 1);
   const int64_t n = (int64_t)blk * (kBlock / (G * LPM)) + cl / G;
   const bool live = n < a.n;
+  // XM: threads [0, mpb) walk the raceline; the U staging below runs on the threads after
+  // them, so the two overlap (the walk is one lane's serial chain, latency-bound)
+  const int mpb = kBlock / (G * LPM);
+  const int soff = (XM && mpb < kBlock) ? mpb : 0;
   Tire t{};
   if (live) t = load_tire(a.params, a.n, n);
   double x0[6];
@@ -682,23 +717,103 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   // XM = 1 (per-model raceline reference): knots [n] and the x/y spline rows [2][4][n-1]
   // after the (optional) U staging; a.xref holds the shared start {s0, v0, scale}
   double* rl_knots = su + (STAGE ? kStageW * C * H : 0);
-  double* rl_xy = rl_knots + a.rl.n;
+  double* rl_xy = rl_knots + a.rl.n + kKnotPad;
   if (XM) {
-    const int nk = a.rl.n, nxy = 8 * (a.rl.n - 1);
-    for (int e = threadIdx.x; e < nk; e += kBlock) rl_knots[e] = a.rl.knots[e];
-    for (int e = threadIdx.x; e < nxy; e += kBlock) rl_xy[e] = a.rl.xy[e];
+    const int nk = a.rl.n, nseg = a.rl.n - 1, nxy = 8 * nseg;
+    const double* gk = a.rl.knots;                          // knots | xy contiguous
+    const double* gmu = a.rl.mus;
+    double* rl_mus = rl_xy + nxy;                           // [M], then the speed window
+    // knots, the +inf pad (RaceRef::step), xy and mus in one batch (one memory round trip
+    // per thread at the ETHZ size)
+    copy_lds<4>(rl_knots, nk, [&](int e) { return gk[e]; });
+    copy_lds<24>(rl_xy, nxy + a.rl.M, [&](int e) {
+      const double* p = e < nxy ? gk + nk + e : gmu + (e - nxy);
+      return *p;
+    });
+    if ((int)threadIdx.x < kKnotPad) rl_knots[nk + threadIdx.x] = __builtin_inf();
+    // the window end: s0 plus the largest advance of H walker steps (one lap at most)
+    const double s0 = a.xref[0];
+    const double L = gk[nseg];
+    const double adv = window_adv(a.xref[1], a.xref[2], a.Ts, H, a.rl.vmax);
+    const bool bounded = adv < L && s0 >= 0.0 && s0 < L;
+    double te = s0 + adv;
+    if (te >= L) te -= L;
     __syncthreads();
+    RL_STAMP(blk, 0);
+    // bisect-right of s0 and te on the knots (RaceRef::init's: the largest i in [1, n-2]
+    // with knots[i] <= s, else 0) as one parallel pass: with the knots ascending, exactly
+    // one segment i has (i == 0 or knots[i] <= s) and (i == n-2 or not knots[i+1] <= s),
+    // and it writes i.  XM leaves sx (the shared xref stage) unused: two ints there.
+    int* rl_sel = reinterpret_cast<int*>(sx);
+    for (int i = threadIdx.x; i < nseg; i += kBlock) {
+      const double ki = rl_knots[i], kn = rl_knots[i + 1];
+      const bool last = i == nseg - 1;
+      if ((i == 0 || ki <= s0) && (last || !(kn <= s0))) rl_sel[0] = i;
+      if ((i == 0 || ki <= te) && (last || !(kn <= te))) rl_sel[1] = i;
+    }
+    __syncthreads();
+    // the speed profiles' window (raceline.hpp SpeedWin): from the start segment to the
+    // window end; block-uniform
+    SpeedWin sw{nullptr, 0, 0};
+    const int seg0 = rl_sel[0];
+    {
+      const int lo = seg0, l2 = rl_sel[1];
+      const double need = bounded ? (double)(l2 >= lo ? l2 - lo : l2 + nseg - lo) + 2.0 : 1e300;
+#ifdef LLAMPC_STAMPS
+      if (blk == 0 && threadIdx.x == 0) {
+        g_rl_dbg[0] = need;
+        g_rl_dbg[1] = a.rl.wcap;
+        g_rl_dbg[2] = adv;
+        g_rl_dbg[3] = a.xref[0];
+        g_rl_dbg[4] = L;
+        g_rl_dbg[5] = a.rl.vmax;
+      }
+#endif
+      if (need <= (double)a.rl.wcap) {
+        double* wl = rl_mus + ((a.rl.M + 1) & ~1);          // 16-B aligned
+        sw.w = wl;
+        sw.seg0 = lo;
+        sw.W = (int)need;
+        const int W = sw.W, tot = a.rl.M * 4 * W;
+        const double* gsp = a.rl.speed;
+        // element e = row W + j; copy_lds asks for e = threadIdx.x + i kBlock in order, so
+        // (row, j) steps by kBlock without a division per element
+        int row = (int)threadIdx.x / W, j = (int)threadIdx.x - row * W;
+        const int drow = kBlock / W, dj = kBlock - drow * W, rows = a.rl.M * 4;
+        copy_lds<24>(wl, tot, [&](int) {          // (row, j) past the end: clamped rows
+          int sg = lo + j;
+          if (sg >= nseg) sg -= nseg;
+          const double v = gsp[(size_t)(row < rows ? row : rows - 1) * nseg + sg];
+          row += drow;
+          j += dj;
+          if (j >= W) {
+            j -= W;
+            ++row;
+          }
+          return v;
+        });
+        __syncthreads();
+      }
+    }
+    RL_STAMP(blk, 1);
     // one thread per model of this block walks ConstantSpeed into xref_pm[m][H][2]
-    const int mpb = kBlock / (G * LPM);
     const int64_t m = (int64_t)blk * mpb + threadIdx.x;
     if ((int)threadIdx.x < mpb && m < a.n) {
       const double mu = (a.params[2 * a.n + m] + a.params[5 * a.n + m]) / (9.81 * a.veh.mass);
+      // the table descriptor in registers: the walk's global stores cannot alias it
+      const RacelineK rl = a.rl;
       RaceRef rr;
-      rr.init(a.rl, rl_knots, mu, a.xref[0], a.xref[1], a.xref[2], a.Ts);
-      double* out = a.xref_pm + m * 2 * H;
-      for (int k = 0; k < H; ++k) rr.step(a.rl, rl_knots, rl_xy, out[2 * k], out[2 * k + 1]);
+      rr.init(rl, rl_knots, rl_mus, mu, a.xref[0], a.xref[1], a.xref[2], a.Ts, seg0);
+      double2* out = reinterpret_cast<double2*>(a.xref_pm + m * 2 * H);
+      for (int k = 0; k < H; ++k) {
+        double xr, yr;
+        rr.step(rl, rl_knots, rl_xy, sw, xr, yr);
+        out[k] = make_double2(xr, yr);
+      }
     }
+    RL_STAMP(blk, 2);
     __threadfence_block();
+    RL_STAMP(blk, 3);
   } else {
     for (int e = threadIdx.x; e <= H; e += kBlock) {
       sx[2 * e] = a.xref[e];
@@ -713,7 +828,8 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     // h lf/Iz cos d, delta) — dyn.hpp fused_in, with the shared constants of make_fused.
     const fm::FmK K = fm::FmK::load();
     const FusedK fq0 = make_fused(a.veh, make_stage<1>(a.veh, Tire{}, 0), a.Ts, LPM == 4);
-    for (int e = threadIdx.x; e < C * H; e += kBlock) {
+    for (int e = (int)threadIdx.x - soff; e < C * H; e += kBlock - soff) {
+      if (e < 0) break;
       const int c = e / H, k = e - c * H;
       const double dl = a.U[2 * e + 1];
       double sd, cd;
@@ -1613,7 +1729,11 @@ int lookahead_blocks(int64_t n, int32_t C, int lpm) {
 // request), so the staging may use most of the CU's 160 KiB.
 constexpr size_t kStageLimit = 128 * 1024;
 
-size_t raceline_lds_bytes(int32_t n) { return 8 * (size_t)n + 64 * (size_t)(n - 1); }
+// knots [n] + the +inf pad [kKnotPad] + xy [8(n-1)] + mus [M] (padded to 16 B) (the speed
+// window on top: launch_plan)
+size_t raceline_lds_bytes(int32_t n, int32_t M) {
+  return 8 * (size_t)(n + kKnotPad) + 64 * (size_t)(n - 1) + 8 * (size_t)((M + 1) & ~1);
+}
 
 size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u) {
   const size_t base = kScratchBytes + 16 * (size_t)(H + 1);
@@ -1718,9 +1838,20 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
     integ = la->integrator;
     lpm = lookahead_lpm(la->n, la->C, integ);
     f.nb_la = lookahead_blocks(la->n, la->C, lpm);
-    if (la->xref_mode == LLAMPC_XREF_RACELINE) {  // knots + x/y rows in LDS; U from global
-      stage = false;
-      lds = std::max(lds, kScratchBytes + 16 * (size_t)(la->H + 1) + raceline_lds_bytes(la->rl.n));
+    if (la->xref_mode == LLAMPC_XREF_RACELINE) {
+      // knots + x/y rows in LDS, the staged inputs when they fit beside them, and the rest
+      // of the CU's LDS (up to the whole track) for the speed-profile window
+      constexpr size_t kLdsMax = 160 * 1024 - 1024;
+      const size_t rl = raceline_lds_bytes(la->rl.n, la->rl.M);
+      size_t base = lookahead_lds_bytes(la->C, la->H, &stage);
+      if (base + rl > kLdsMax) {
+        stage = false;
+        base = kScratchBytes + 16 * (size_t)(la->H + 1);
+      }
+      const size_t per_seg = 32 * (size_t)std::max(1, la->rl.M);
+      const size_t room = base + rl < kLdsMax ? kLdsMax - base - rl : 0;
+      lav.rl.wcap = (int32_t)std::min<size_t>(room / per_seg, (size_t)(la->rl.n - 1));
+      lds = std::max(lds, base + rl + per_seg * (size_t)lav.rl.wcap);
     } else {
       lds = std::max(lds, lookahead_lds_bytes(la->C, la->H, &stage));
     }
@@ -1757,6 +1888,12 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
 #ifdef LLAMPC_STAMPS
 extern "C" int llampc_debug_lb_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lb_stamps), sizeof(g_lb_stamps)) == hipSuccess ? 0 : -2;
+}
+extern "C" int llampc_debug_rl_ph(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rl_ph), sizeof(g_rl_ph)) == hipSuccess ? 0 : -2;
+}
+extern "C" int llampc_debug_rl(double* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rl_dbg), sizeof(g_rl_dbg)) == hipSuccess ? 0 : -2;
 }
 extern "C" int llampc_debug_la_wave(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_wave), sizeof(g_la_wave)) == hipSuccess ? 0 : -2;

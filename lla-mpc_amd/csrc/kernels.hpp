@@ -98,7 +98,7 @@ int lookahead_group(int32_t C);
 int lookahead_lpm(int64_t n, int32_t C, int32_t integrator);
 int lookahead_blocks(int64_t n, int32_t C, int lpm);
 size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u);
-size_t raceline_lds_bytes(int32_t n);
+size_t raceline_lds_bytes(int32_t n, int32_t M);
 
 // The whole tick in ONE launch: look-back blocks (if lb), look-ahead blocks (if la), and
 // the completion stages run by ticket winners; writes f.out.  f.nb_* / f.do_* are set here.

@@ -28,8 +28,11 @@ def harness(tmp_path_factory):
     return out
 
 
+@pytest.mark.parametrize("mode", ["global", "win"])
 @pytest.mark.parametrize("name", ["ETHZ", "ETHZMobil"])
-def test_raceline_walker_host_asan(harness, tmp_path, name):
+def test_raceline_walker_host_asan(harness, tmp_path, name, mode):
+    """mode 'win': the speed profiles read through the launch's window (raceline.hpp
+    SpeedWin, as the kernel prologue builds it) — the same references."""
     import sys
     sys.path.insert(0, os.path.join(REPO, "lla-mpc_amd"))
     from llampc.tracks import ETHZ, ETHZMobil
@@ -45,7 +48,7 @@ def test_raceline_walker_host_asan(harness, tmp_path, name):
             cases.append((mu, s0, v0, scale, Ts))
     np.concatenate([[H], np.ravel(cases)]).astype(np.float64).tofile(tmp_path / "c.bin")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
-    r = subprocess.run([harness, str(tmp_path / "t.bin"), str(tmp_path / "c.bin")], capture_output=True,
+    r = subprocess.run([harness, str(tmp_path / "t.bin"), str(tmp_path / "c.bin"), mode], capture_output=True,
                        text=True, env=env, check=True)
     got = np.array([list(map(float, ln.split())) for ln in r.stdout.strip().splitlines()]).reshape(len(cases), H, 2)
     td = np.load(os.path.join(REPO, "lla-mpc_amd", "llampc", "tracks", "data", "tracks.npz"))

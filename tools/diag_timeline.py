@@ -16,8 +16,15 @@ LB_ONLY = len(sys.argv) > 2 and sys.argv[2] == "lb"
 b = ModelBank(generate_bank(N, 0), W=10, device=0)
 xref = s[:2, :H + 1]
 U = np.tile(u[:, 0], (H, 1))[None]
+kw = {}
+if os.environ.get("RACELINE"):                # xref_mode RACELINE (per-model ConstantSpeed)
+    from llampc.mpc.planner import raceline_start
+    from llampc.tracks import ETHZ
+    tr = ETHZ()
+    b.set_raceline(tr)
+    kw = dict(raceline_start=(raceline_start(s[:, 1], tr, 0)[0], float(s[3, 1]), 0.9))
 for t in range(1, 30):
-    b.plan_raw(s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1], do_lookahead=not LB_ONLY)
+    b.plan_raw(s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1], do_lookahead=not LB_ONLY, **kw)
 la = (ctypes.c_ulonglong * (8 * 8 * 2))()
 lib.llampc_debug_la_stamps.argtypes = [ctypes.c_void_p]
 lib.llampc_debug_la_stamps(la)
@@ -67,3 +74,19 @@ if hasattr(lib, "llampc_debug_la_wave"):
     w0 = (V - V.min(axis=1, keepdims=True)) / 100.0
     print(f"wave rollout-end skew per block (us): {q(sk)}; mean offset of waves 0..3 from the block's first: "
           + ", ".join(f"{x:.2f}" for x in w0.mean(axis=0)))
+
+if os.environ.get("RACELINE") and hasattr(lib, "llampc_debug_rl"):
+    RD = (ctypes.c_double * 8)()
+    lib.llampc_debug_rl.argtypes = [ctypes.c_void_p]
+    lib.llampc_debug_rl(RD)
+    print("raceline window: need %.1f cap %.0f adv %.3f s0 %.3f L %.3f vmax %.3f" % tuple(RD[:6]))
+
+if os.environ.get("RACELINE") and hasattr(lib, "llampc_debug_rl_ph"):
+    PH = (ctypes.c_ulonglong * (1024 * 4))()
+    lib.llampc_debug_rl_ph.argtypes = [ctypes.c_void_p]
+    lib.llampc_debug_rl_ph(PH)
+    P = np.frombuffer(PH, dtype=np.uint64).reshape(1024, 4).astype(np.int64)[:nla]
+    st = Z[:, 0, 1]
+    print("raceline prologue (us after block start, min/median/max): tables " + q((P[:, 0] - st) / 100.0)
+          + ", window " + q((P[:, 1] - st) / 100.0) + ", walkers " + q((P[:, 2] - st) / 100.0)
+          + ", fence " + q((P[:, 3] - st) / 100.0))
