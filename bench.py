@@ -6,7 +6,9 @@ look-back (score every model on the newest transition, slide the W-window, argmi
 top-K) + look-ahead (H-step RK4 rollout + MPC cost of every (model, candidate)) +
 selection, i.e. ``llampc_plan_device`` (ONE kernel launch).  With --gpus N > 1 each rank owns a
 contiguous shard of N_per_gpu models (weak scaling; config 4 = 8 x 10^4) and every tick
-adds ONE RCCL all-gather of the 1.5 KB shard record plus the on-device merge.
+adds ONE exchange of the 1.5 KB shard records plus the on-device merge: by default one
+kernel that pushes the record into every peer's IPC-mapped mailbox over xGMI and merges
+(llampc_exchange_peer), else an RCCL all-gather + merge_kernel (LLAMPC_EXCHANGE).
 
 Workload (BASELINE.json configs[1]): ETHZ track, N_models = 10^4 per GPU, H = 20, C = 1
 candidate, W = 10, K = 10, Ts = 0.02, gradual friction change.  Tick inputs are
@@ -41,6 +43,14 @@ FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation
 # capacity: 1,024 SIMDs x 16 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md max clock).
 ISSUE_INSTR_PER_STEP = {4: 507, 2: 620, 1: 936}
 ISSUE_PEAK_LANE_INSTR = 1024 * 16 * 2.4e9
+
+
+EXCHANGE_DESC = {
+    "peer": "peer mailboxes over xGMI (HIP IPC): one push/poll/merge kernel per tick (llampc_exchange_peer)",
+    "rccl": "native RCCL all-gather on the tick stream (llampc_exchange_device) + merge_kernel",
+    "c10d": "c10d all_gather_into_tensor (nccl) + merge_kernel",
+    "host": "gloo all-gather on the host + merge_kernel",
+}
 
 
 def parse():
@@ -271,7 +281,7 @@ def main():
                                    f"C={C}, {args.scenario or ('sudden' if args.track == 'ETHZMobil' else 'gradual')} friction",
                        "N_models_total": N_total,
                        "N_models_per_gpu": N_local, "H": H, "C": C, "W": W, "K": K, "Ts": 0.02,
-                       "track": args.track, "parallelism": f"bank-shard x{world}" + (" + 1 RCCL all-gather/tick" if sb.exchange else "")},
+                       "track": args.track, "parallelism": f"bank-shard x{world}" + (f" + 1 exchange/tick ({sb.transport})" if sb.exchange else "")},
             "roofline": roof,
             "valu": {"bound": "fp64-valu", "achieved_gflops": valu_gf, "peak_tflops": FP64_VALU_PEAK_TFLOPS,
                      "frac": valu_gf / (FP64_VALU_PEAK_TFLOPS * 1e3) if valu_gf else None,
@@ -281,8 +291,7 @@ def main():
             "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0]),
                           "bracket": f"one plan launch in every {TIMING_SAMPLE} per event pair" if sb.exchange else
                                      f"groups of {TIMING_STRIDE} consecutive plan launches"},
-            "exchange": (("native RCCL all-gather on the tick stream (llampc_exchange_device)" if sb._comm is not None
-                          else f"c10d all_gather_into_tensor ({sb.backend})") + " + merge_kernel") if sb.exchange else None,
+            "exchange": EXCHANGE_DESC[sb.transport] if sb.exchange else None,
             "host_issue_us_per_step": t_issue / args.steps * 1e6,
             "lpm": lpm_of(N_local, C),
             "result_check": {"sel_model": merged.best_model, "window_full": merged.window_full,

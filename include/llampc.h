@@ -20,6 +20,8 @@
  *  llampc_plan / llampc_plan_device one LLA-MPC tick: rt.py:300-366 (look-back on the
  *                                  newest transition, selection, look-ahead from x_t)
  *  llampc_merge / _device          (new) cross-shard merge of per-GPU plan results
+ *  llampc_exchange_device / _peer  (new) the per-tick gather + merge of the sharded bank
+ *                                  (SURVEY.md §8e): RCCL all-gather, or xGMI mailboxes
  *  llampc_dynamics_batch           Dynamic.calc_forces_batch (llampc/models/dynamic.py:
  *                                  117-154), Dynamic._diffequation_batch (:98-115)
  *  llampc_integrate_batch          Model._integrate_batch (model.py:32-40, RK4),
@@ -129,7 +131,8 @@ typedef struct llampc_plan_out {
   int64_t la_best_model;  /* argmin over all (model, candidate) costs              */
   int32_t la_best_cand;
   int32_t status;         /* 0 ok; LLAMPC_STATUS_POLL_TIMEOUT (1): the in-launch
-                             completion gave up waiting (a device fault, never expected) */
+                             completion (or the peer exchange) gave up waiting (a device
+                             fault or a missing rank, never expected) */
   double  la_best_cost;
   int64_t topk[LLAMPC_KMAX];      /* argsort(window mean)[:K] (rt.py:360), -1 pad  */
   double  topk_val[LLAMPC_KMAX];
@@ -240,6 +243,29 @@ int llampc_merge_device(const void* d_parts, int32_t G, int32_t nan_policy, void
 int llampc_exchange_device(const void* d_local, void* d_all, int32_t world, void* d_merged,
                            int32_t nan_policy, void* comm, void* allgather_fn, int32_t device,
                            void* stream);
+
+/* Peer exchange: the same per-tick gather + merge with no collective library.  Each rank
+ * owns a mailbox (uncached device memory, [2][world] record slots of tagged words) that every
+ * peer process maps through HIP IPC; per tick ONE kernel pushes this rank's record into slot
+ * [rank] of every mailbox over xGMI (system-scope stores), polls its own mailbox until all
+ * `world` records of this tick have arrived and runs merge_kernel's merge — the output equals
+ * llampc_exchange_device's.  Setup: create, export the IPC handle (64 bytes), share the
+ * handles out of band (e.g. a torch.distributed all_gather_object), open every peer's.  All
+ * ranks must call llampc_exchange_peer the same number of times (the tick number is the tag).
+ * A rank that waits more than the poll bound (default 2 s; set_bound) gets status
+ * LLAMPC_STATUS_POLL_TIMEOUT in d_merged.  Replaces the same reference-side gather as
+ * llampc_exchange_device. */
+typedef struct llampc_mailbox llampc_mailbox;
+int llampc_mailbox_create(int32_t world, int32_t rank, int32_t device, llampc_mailbox** out);
+int llampc_mailbox_ipc_handle(llampc_mailbox* mb, void* handle /* 64 bytes out */);
+int llampc_mailbox_open_peer(llampc_mailbox* mb, int32_t peer, const void* handle /* 64 bytes */);
+/* Use `other`, a mailbox of rank `peer` created in THIS process on the same device, as that
+ * peer's (several ranks driven from one process; tests). */
+int llampc_mailbox_link(llampc_mailbox* mb, int32_t peer, const llampc_mailbox* other);
+int llampc_mailbox_set_bound(llampc_mailbox* mb, double seconds);
+int llampc_exchange_peer(llampc_mailbox* mb, const void* d_local, void* d_merged, int32_t nan_policy,
+                         void* stream);
+int llampc_mailbox_destroy(llampc_mailbox* mb);
 
 /* ---- raw batched dynamics (Dynamic API parity) ---------------------------------- */
 /* x [n][6], u [n][2]; params [6][P] with P == 1 (one model broadcast) or P == n.

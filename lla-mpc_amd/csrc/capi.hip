@@ -934,6 +934,112 @@ int llampc_exchange_device(const void* d_local, void* d_all, int32_t world, void
 
 }  // extern "C"
 
+// ---- peer exchange (xGMI mailboxes) -------------------------------------------------
+struct llampc_mailbox {
+  int32_t world = 0, rank = 0, device = 0;
+  uint64_t* own = nullptr;               // [2][world][kRecWords], uncached device memory
+  uint64_t* box[kPeerMax] = {};          // every rank's mailbox as mapped in this process
+  bool opened[kPeerMax] = {};            // box[g] came from hipIpcOpenMemHandle
+  uint32_t seq = 0;
+  uint64_t bound = 200000000ull;         // 2 s of s_memrealtime (100 MHz)
+};
+
+extern "C" {
+
+int llampc_mailbox_create(int32_t world, int32_t rank, int32_t device, llampc_mailbox** out) {
+  if (!out || world < 1 || world > kPeerMax || rank < 0 || rank >= world)
+    return fail(LLAMPC_E_ARG, "bad mailbox arguments (world=%d rank=%d, world 1..%d)", world, rank, kPeerMax);
+  DeviceGuard g(device);
+  if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", device);
+  auto* mb = new llampc_mailbox();
+  mb->world = world;
+  mb->rank = rank;
+  mb->device = device;
+  const size_t bytes = (size_t)2 * world * kRecWords * sizeof(uint64_t);
+  hipError_t e = hipExtMallocWithFlags((void**)&mb->own, bytes, hipDeviceMallocUncached);
+  if (e == hipSuccess) e = hipMemset(mb->own, 0, bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    if (mb->own) (void)hipFree(mb->own);
+    delete mb;
+    return fail(LLAMPC_E_HIP, "mailbox allocation: %s", hipGetErrorString(e));
+  }
+  mb->box[rank] = mb->own;
+  *out = mb;
+  return LLAMPC_OK;
+}
+
+int llampc_mailbox_ipc_handle(llampc_mailbox* mb, void* handle) {
+  if (!mb || !handle) return fail(LLAMPC_E_ARG, "null mailbox/handle");
+  DeviceGuard g(mb->device);
+  hipIpcMemHandle_t h;
+  HIP_TRY(hipIpcGetMemHandle(&h, mb->own));
+  memcpy(handle, &h, sizeof(h));
+  return LLAMPC_OK;
+}
+
+int llampc_mailbox_open_peer(llampc_mailbox* mb, int32_t peer, const void* handle) {
+  if (!mb || !handle || peer < 0 || peer >= mb->world || peer == mb->rank || mb->box[peer])
+    return fail(LLAMPC_E_ARG, "bad peer %d (world %d, rank %d, or already open)", mb ? peer : -1,
+                mb ? mb->world : 0, mb ? mb->rank : 0);
+  DeviceGuard g(mb->device);
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  void* p = nullptr;
+  HIP_TRY(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  mb->box[peer] = (uint64_t*)p;
+  mb->opened[peer] = true;
+  return LLAMPC_OK;
+}
+
+int llampc_mailbox_link(llampc_mailbox* mb, int32_t peer, const llampc_mailbox* other) {
+  if (!mb || !other || peer < 0 || peer >= mb->world || peer == mb->rank || mb->box[peer] ||
+      other->world != mb->world || other->rank != peer || other->device != mb->device)
+    return fail(LLAMPC_E_ARG, "bad mailbox link (peer %d)", peer);
+  mb->box[peer] = other->own;
+  return LLAMPC_OK;
+}
+
+int llampc_mailbox_set_bound(llampc_mailbox* mb, double seconds) {
+  if (!mb || !(seconds > 0) || seconds > 1e6) return fail(LLAMPC_E_ARG, "bad poll bound");
+  mb->bound = (uint64_t)(seconds * 1e8);
+  return LLAMPC_OK;
+}
+
+int llampc_exchange_peer(llampc_mailbox* mb, const void* d_local, void* d_merged, int32_t nan_policy,
+                         void* stream) {
+  if (!mb || !d_local || !d_merged) return fail(LLAMPC_E_ARG, "bad exchange arguments");
+  for (int g = 0; g < mb->world; ++g)
+    if (!mb->box[g]) return fail(LLAMPC_E_STATE, "mailbox of peer %d not open", g);
+  DeviceGuard g(mb->device);
+  if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", mb->device);
+  if (++mb->seq == 0) mb->seq = 1;       // 0 is the zeroed mailbox's tag
+  PeerLaunch a{};
+  a.local = (const llampc_plan_out*)d_local;
+  for (int r = 0; r < mb->world; ++r) a.box[r] = mb->box[r];
+  a.merged = (llampc_plan_out*)d_merged;
+  a.bound = mb->bound;
+  a.G = mb->world;
+  a.rank = mb->rank;
+  a.nan_first = nan_policy == LLAMPC_NAN_FIRST;
+  a.seq = mb->seq;
+  HIP_TRY(launch_peer_exchange(a, (hipStream_t)stream));
+  return LLAMPC_OK;
+}
+
+int llampc_mailbox_destroy(llampc_mailbox* mb) {
+  if (!mb) return LLAMPC_OK;
+  DeviceGuard g(mb->device);
+  (void)hipDeviceSynchronize();
+  for (int r = 0; r < mb->world; ++r)
+    if (mb->opened[r]) (void)hipIpcCloseMemHandle(mb->box[r]);
+  if (mb->own) (void)hipFree(mb->own);
+  delete mb;
+  return LLAMPC_OK;
+}
+
+}  // extern "C"
+
 // ------------------------------------------------------------------------------------
 // Raw batched dynamics: per-device cached workspace + stream
 // ------------------------------------------------------------------------------------

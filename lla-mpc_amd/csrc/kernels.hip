@@ -1501,21 +1501,15 @@ struct EntS {
   int32_t pad;
 };
 
-__global__ __launch_bounds__(kBlock) void merge_kernel(const llampc_plan_out* parts, int32_t G,
-                                                       int32_t nan_first, llampc_plan_out* m) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// The merge proper over G records already staged in LDS at `rec` (their sorted top-K lists
+// are ranked in `lists`, 2 G KMAX EntS); thread 0 writes the scalars, threads < KMAX the
+// top-K.  `late` (the peer exchange gave up waiting) is or-ed into the status.
+__device__ __forceinline__ void merge_staged(const llampc_plan_out* rec, int32_t G, int32_t nan_first,
+                                             llampc_plan_out* m, EntS* lists, int32_t late) {
   const int tid = threadIdx.x;
-  // the G gathered records -> LDS in ONE round trip of 16-B loads (every later read is LDS)
-  llampc_plan_out* rec = reinterpret_cast<llampc_plan_out*>(smem);
-  constexpr int kWords = sizeof(llampc_plan_out) / 16;
-  static_assert(sizeof(llampc_plan_out) % 16 == 0, "records staged as 16-B words");
-  const uint4* srcw = reinterpret_cast<const uint4*>(parts);
-  uint4* dstw = reinterpret_cast<uint4*>(rec);
-  for (int e = tid; e < G * kWords; e += kBlock) dstw[e] = srcw[e];
-  __syncthreads();
   const int K = rec[0].K;
   const int M = G * K;
-  EntS* buf0 = reinterpret_cast<EntS*>(smem + (size_t)G * sizeof(llampc_plan_out));
+  EntS* buf0 = lists;
   EntS* buf1 = buf0 + M;
   for (int e = tid; e < M; e += kBlock) {
     const int g = e / K, j = e - g * K;
@@ -1584,7 +1578,7 @@ __global__ __launch_bounds__(kBlock) void merge_kernel(const llampc_plan_out* pa
   m->window_count = p0.window_count;
   m->window_full = p0.window_full;
   m->K = K;
-  int32_t st = 0;
+  int32_t st = late ? kPollTimeoutStatus : 0;
   for (int g = 0; g < G; ++g) st |= rec[g].status;
   m->status = st;
   m->lb_best = bi == kNoIndex ? -1 : bi;
@@ -1604,6 +1598,71 @@ __global__ __launch_bounds__(kBlock) void merge_kernel(const llampc_plan_out* pa
   m->la_best_cand = am == kNoIndex ? -1 : ac;
   m->la_best_cost = av;
   m->n_nonfinite = nf;
+}
+
+__global__ __launch_bounds__(kBlock) void merge_kernel(const llampc_plan_out* parts, int32_t G,
+                                                       int32_t nan_first, llampc_plan_out* m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  // the G gathered records -> LDS in ONE round trip of 16-B loads (every later read is LDS)
+  llampc_plan_out* rec = reinterpret_cast<llampc_plan_out*>(smem);
+  constexpr int kWords = sizeof(llampc_plan_out) / 16;
+  static_assert(sizeof(llampc_plan_out) % 16 == 0, "records staged as 16-B words");
+  const uint4* srcw = reinterpret_cast<const uint4*>(parts);
+  uint4* dstw = reinterpret_cast<uint4*>(rec);
+  for (int e = tid; e < G * kWords; e += kBlock) dstw[e] = srcw[e];
+  __syncthreads();
+  merge_staged(rec, G, nan_first, m, reinterpret_cast<EntS*>(smem + (size_t)G * sizeof(llampc_plan_out)), 0);
+}
+
+// Peer exchange (xGMI, no collective library): every rank's mailbox is uncached device
+// memory mapped into every peer process (IPC).  One block per rank per tick:
+//  1. push — this rank's record as tagged 64-bit words (tick seq << 32 | 32 payload bits)
+//     into slot [seq & 1][rank] of every mailbox (its own included), system-scope stores
+//     that go straight over xGMI into the peer's HBM;
+//  2. poll — every thread spins on its share of the G slots of its own mailbox until each
+//     word carries this tick's seq (every word validates itself: no fence pairing across
+//     devices), unpacking the payloads into the LDS records;
+//  3. merge_staged — the same merge as merge_kernel.
+// Two slots by tick parity: a peer can only push tick t+2 after its own exchange of t+1,
+// which needs this rank's push of t+1, issued after this rank's exchange of t has finished
+// reading slot (t & 1) — so a slot is never overwritten while it is read.  A poll that
+// waits longer than `bound` (s_memrealtime ticks) gives status LLAMPC_STATUS_POLL_TIMEOUT.
+__global__ __launch_bounds__(kBlock) void peer_exchange_kernel(PeerLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int kW = kRecWords;
+  const int tid = threadIdx.x;
+  const int G = a.G;
+  const size_t slot0 = (size_t)(a.seq & 1) * G * kW;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(a.local);
+  for (int w = tid; w < kW; w += kBlock) {
+    const uint64_t v = tag_word(a.seq, src[w]);
+    const size_t off = slot0 + (size_t)a.rank * kW + w;
+    for (int g = 0; g < G; ++g)
+      __hip_atomic_store(a.box[g] + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  uint32_t* rec32 = reinterpret_cast<uint32_t*>(smem);
+  const uint64_t* own = a.box[a.rank] + slot0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  int late = 0;
+  for (int e = tid; e < G * kW; e += kBlock) {
+    uint64_t v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    while (!tag_ok(v, a.seq)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.bound) { late = 1; break; }
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    rec32[e] = (uint32_t)v;
+  }
+  // one flag per wave after the lists (no static LDS: the launch asks for all 160 KB)
+  EntS* lists = reinterpret_cast<EntS*>(smem + (size_t)G * sizeof(llampc_plan_out));
+  int* wave_late = reinterpret_cast<int*>(lists + 2 * (size_t)G * LLAMPC_KMAX);
+  const int wl = __any(late);
+  if ((tid & 63) == 0) wave_late[tid >> 6] = wl;
+  __syncthreads();
+  late = 0;
+  for (int w = 0; w < kBlock / 64; ++w) late |= wave_late[w];
+  merge_staged(reinterpret_cast<const llampc_plan_out*>(smem), G, a.nan_first, a.merged, lists, late);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1917,6 +1976,15 @@ hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_fir
   const size_t lds = (size_t)G * sizeof(llampc_plan_out) + 2 * M * sizeof(EntS);
   allow_lds(merge_kernel);
   hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(kBlock), lds, s, parts, G, nan_first, merged);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_exchange(const PeerLaunch& a, hipStream_t s) {
+  if (a.G < 1 || a.G > kPeerMax || a.rank < 0 || a.rank >= a.G || a.seq == 0) return hipErrorInvalidValue;
+  const size_t lds = (size_t)a.G * sizeof(llampc_plan_out) + 2 * (size_t)a.G * LLAMPC_KMAX * sizeof(EntS) +
+                     (kBlock / 64) * sizeof(int);
+  allow_lds(peer_exchange_kernel);
+  hipLaunchKernelGGL(peer_exchange_kernel, dim3(1), dim3(kBlock), lds, s, a);
   return hipGetLastError();
 }
 

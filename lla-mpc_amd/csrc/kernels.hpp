@@ -109,6 +109,19 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
 bool plan_inline_ok(int32_t C, int32_t H, int32_t integrator, int32_t xref_mode);
 hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
                         llampc_plan_out* merged, hipStream_t s);
+// Peer exchange of the sharded tick (peer_exchange_kernel): mailbox g is [2][G][kRecWords]
+// tagged 64-bit words in rank g's device memory, mapped into this process.
+constexpr int kPeerMax = 32;
+constexpr int kRecWords = (int)(sizeof(llampc_plan_out) / 4);
+struct PeerLaunch {
+  const llampc_plan_out* local;          // this rank's record (written by its plan launch)
+  uint64_t* box[kPeerMax];               // every rank's mailbox as mapped here (box[rank]: own)
+  llampc_plan_out* merged;
+  uint64_t bound;                        // poll bound, s_memrealtime ticks (100 MHz)
+  int32_t G, rank, nan_first;
+  uint32_t seq;                          // tick number, never 0 (the mailbox starts zeroed)
+};
+hipError_t launch_peer_exchange(const PeerLaunch& a, hipStream_t s);
 hipError_t launch_dynamics(int32_t op, const double* x, const double* u, const double* params,
                            int64_t P, VehK veh, int64_t n, double* out, hipStream_t s);
 hipError_t launch_math(int32_t fn, const double* a, const double* b, int64_t n, double* out,

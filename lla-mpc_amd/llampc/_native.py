@@ -103,6 +103,13 @@ _SIGNATURES = {
                                       C.c_void_p]),
     "llampc_exchange_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
                                          C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "llampc_mailbox_create": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "llampc_mailbox_ipc_handle": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "llampc_mailbox_open_peer": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
+    "llampc_mailbox_link": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
+    "llampc_mailbox_set_bound": (C.c_int, [C.c_void_p, C.c_double]),
+    "llampc_exchange_peer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "llampc_mailbox_destroy": (C.c_int, [C.c_void_p]),
     "llampc_dynamics_batch": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                         C.POINTER(Vehicle), C.c_int64, C.c_void_p, C.c_int32,
                                         C.c_int32, C.c_void_p]),

@@ -9,6 +9,17 @@ every rank runs the same deterministic merge (csrc/merge.hpp) on the device — 
 hold the identical result of the unsharded computation.  There is no other data-path
 collective.  With the "gloo" backend (CPU tests) the records travel as CPU tensors and the
 same merge code runs on the host (llampc_merge).
+
+Transports of the exchange (LLAMPC_EXCHANGE; the merged record is the same for all):
+  peer  (default when it verifies) — no collective library: every rank's mailbox (uncached
+        device memory) is mapped into every peer through HIP IPC, and ONE kernel per tick
+        pushes this rank's record into all mailboxes over xGMI, polls its own until the tick's
+        records have arrived and merges (llampc_exchange_peer).  Set up with one
+        all_gather_object of the IPC handles on any backend (gloo included), then checked by a
+        probe exchange against the host merge; on any failure every rank falls back together.
+  rccl  — ncclAllGather of the process's RCCL on the tick stream + merge_kernel.
+  c10d  — torch.distributed.all_gather_into_tensor + merge_kernel.
+  host  — (gloo) records gathered on the host, merged by merge_kernel.
 """
 from __future__ import annotations
 
@@ -42,6 +53,52 @@ def _rccl_allgather_addr() -> int:
     if path is None:
         raise nat.NativeError("no RCCL library loaded in this process")
     return C.cast(C.CDLL(path).ncclAllGather, C.c_void_p).value
+
+
+def _all_gather_obj(obj, group=None) -> list:
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def exchange_mode() -> str:
+    """LLAMPC_EXCHANGE = auto (peer, else rccl/c10d/host) | peer (required) | rccl | c10d | host;
+    LLAMPC_C10D_EXCHANGE=1 is the older spelling of c10d."""
+    if os.environ.get("LLAMPC_C10D_EXCHANGE"):
+        return "c10d"
+    m = os.environ.get("LLAMPC_EXCHANGE", "auto")
+    if m not in ("auto", "peer", "rccl", "c10d", "host"):
+        raise ValueError(f"LLAMPC_EXCHANGE={m!r}: auto | peer | rccl | c10d | host")
+    return m
+
+
+def probe_record(rank: int, world: int, K: int = 10) -> nat.PlanOut:
+    """A synthetic shard record for checking a transport: distinct global indices per rank,
+    sorted top-K values, one NaN-free look-ahead best (deterministic in rank)."""
+    rng = np.random.RandomState(7919 + rank)
+    o = nat.PlanOut()
+    o.window_count, o.window_full, o.K, o.sel_owned = 10, 1, K, int(rank == 0)
+    vals = np.sort(rng.uniform(0.0, 1.0, K))
+    for j in range(nat.KMAX):
+        o.topk[j] = rank * 1000 + j if j < K else -1
+        o.topk_val[j] = vals[j] if j < K else 0.0
+        o.topk_Df[j] = o.topk_Dr[j] = o.topk_cost[j] = float(rank + j) if j < K else 0.0
+        o.topk_cand[j] = j if j < K else -1
+    o.lb_best, o.lb_best_val = rank * 1000, vals[0]
+    o.sel_model, o.sel_cand, o.sel_cost = 0, 1, 0.5
+    o.la_best_model, o.la_best_cand, o.la_best_cost = rank * 1000 + 3, rank, float(rng.uniform())
+    o.n_nonfinite, o.status = rank, 0
+    return o
+
+
+def records_equal(a: nat.PlanOut, b: nat.PlanOut) -> bool:
+    A, B = nat.plan_out_to_dict(a), nat.plan_out_to_dict(b)
+    for k in B:
+        x, y = np.asarray(A[k]), np.asarray(B[k])
+        if x.shape != y.shape or not np.array_equal(x, y, equal_nan=x.dtype.kind == "f"):
+            return False
+    return True
 
 
 def gather_merge_host(local: nat.PlanOut, group=None, nan_policy=nat.NAN_FIRST) -> nat.PlanOut:
@@ -91,8 +148,66 @@ class ShardedBank:
         # on the tick's stream, over the communicator of a group of its own — no c10d stream
         # hand-off, ~1 us of host time per tick.  LLAMPC_C10D_EXCHANGE=1 keeps the c10d call.
         self._comm = None
-        if self.exchange and self.backend == "nccl" and not os.environ.get("LLAMPC_C10D_EXCHANGE"):
-            self._setup_native_exchange(dev)
+        self._mailbox = None
+        self.transport = None
+        if self.exchange:
+            mode = exchange_mode()
+            if mode in ("auto", "peer"):
+                self._setup_peer_exchange(dev, required=mode == "peer")
+            if self._mailbox is None and self.backend == "nccl" and mode in ("auto", "rccl"):
+                self._setup_native_exchange(dev)
+            self.transport = ("peer" if self._mailbox is not None else "rccl" if self._comm is not None
+                              else "c10d" if self.backend == "nccl" else "host")
+
+    def _setup_peer_exchange(self, dev, required=False):
+        """Map every rank's mailbox (collective: all ranks take the same decision)."""
+        import sys
+        import torch
+        lib = nat.load()
+        mb = C.c_void_p()
+        err, handle = None, b""
+        try:
+            nat.check(lib.llampc_mailbox_create(self.world, self.rank, self.device, C.byref(mb)))
+            h = (C.c_ubyte * 64)()
+            nat.check(lib.llampc_mailbox_ipc_handle(mb, h))
+            handle = bytes(h)
+        except Exception as e:                     # noqa: BLE001 — decided collectively below
+            err = e
+        handles = _all_gather_obj(handle, self.group)
+        if err is None and all(handles):
+            try:
+                for g, hg in enumerate(handles):
+                    if g != self.rank:
+                        nat.check(lib.llampc_mailbox_open_peer(mb, g, (C.c_ubyte * 64).from_buffer_copy(hg)))
+            except Exception as e:                 # noqa: BLE001
+                err = e
+        ok = all(_all_gather_obj(err is None, self.group))
+        if ok:                                     # probe exchange vs the host merge
+            rec = probe_record(self.rank, self.world)
+            parts = [_out_of(np.frombuffer(b, dtype=np.uint8))
+                     for b in _all_gather_obj(_bytes_of(rec).tobytes(), self.group)]
+            want = nat.merge(parts, nat.NAN_FIRST)
+            d_in = torch.from_numpy(_bytes_of(rec)).to(dev)
+            d_out = torch.zeros_like(d_in)
+            try:
+                nat.check(lib.llampc_exchange_peer(mb, d_in.data_ptr(), d_out.data_ptr(), nat.NAN_FIRST,
+                                                   self.stream.cuda_stream))
+                self.stream.synchronize()
+                got = _out_of(d_out.cpu().numpy())
+                if got.status != 0 or not records_equal(got, want):
+                    err = nat.NativeError(f"probe exchange differs from the host merge (status {got.status})")
+            except Exception as e:                 # noqa: BLE001
+                err = e
+            ok = all(_all_gather_obj(err is None, self.group))
+        if not ok:
+            if mb.value:
+                lib.llampc_mailbox_destroy(mb)
+            msg = f"llampc: peer exchange unavailable ({err or 'failed on another rank'})"
+            if required:
+                raise nat.NativeError(msg)
+            print(msg + "; falling back", file=sys.stderr)
+            return
+        self._mailbox = mb
 
     def _setup_native_exchange(self, dev):
         import sys
@@ -164,7 +279,10 @@ class ShardedBank:
         lib = nat.load()
         nat.check(lib.llampc_plan_device(self.bank.handle, C.byref(pin), self.d_local.data_ptr(),
                                          None, None, None, s.cuda_stream))
-        if self._comm is not None:           # native: all-gather + merge on stream s
+        if self._mailbox is not None:        # peer: push + poll + merge, one kernel on stream s
+            nat.check(lib.llampc_exchange_peer(self._mailbox, self.d_local.data_ptr(), self.d_merged.data_ptr(),
+                                               pin.nan_policy, s.cuda_stream))
+        elif self._comm is not None:           # native: all-gather + merge on stream s
             nat.check(lib.llampc_exchange_device(self.d_local.data_ptr(), self.d_all.data_ptr(), self.world,
                                                  self.d_merged.data_ptr(), pin.nan_policy, self._comm,
                                                  self._allgather, self.device, s.cuda_stream))
@@ -188,6 +306,9 @@ class ShardedBank:
         return self.launch(pin, stream)
 
     def close(self):
+        if self._mailbox is not None:        # after this rank's last exchange (it synchronises)
+            nat.load().llampc_mailbox_destroy(self._mailbox)
+            self._mailbox = None
         self.bank.close()
 
     def fetch(self, stream=None, U=None) -> PlanResult:

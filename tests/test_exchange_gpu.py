@@ -1,8 +1,9 @@
 """GPU test of the N > 1 tick path on one device: a 1-rank RCCL group with the exchange
 forced on (LLAMPC_FORCE_EXCHANGE=1), so each tick runs plan -> all-gather -> merge_kernel
 exactly as a rank of the 8-GPU job does.  Every tick's merged record must equal the plain
-single-bank tick on the same inputs, with the exchange issued natively
-(llampc_exchange_device on the tick's stream) and through c10d (LLAMPC_C10D_EXCHANGE=1).
+single-bank tick on the same inputs, for each transport: the peer mailbox (llampc_exchange_peer:
+push over IPC-mapped memory, poll, merge — one kernel), RCCL issued natively
+(llampc_exchange_device on the tick's stream) and c10d.
 No per-tick synchronisation: the stream order alone must make the records right."""
 import os
 import socket
@@ -36,7 +37,7 @@ def nccl_world1():
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("transport", ["native", "c10d"])
+@pytest.mark.parametrize("transport", ["peer", "rccl", "c10d"])
 def test_exchange_tick_equals_plain_tick(nccl_world1, transport):
     import torch
     from llampc import _native as nat
@@ -47,9 +48,7 @@ def test_exchange_tick_equals_plain_tick(nccl_world1, transport):
     N, H, C, W, K, T = 4000, 20, 2, 4, 6, 12
     rng = np.random.RandomState(5)
     bank = generate_bank(N, seed=6)
-    env = {"LLAMPC_FORCE_EXCHANGE": "1"}
-    if transport == "c10d":
-        env["LLAMPC_C10D_EXCHANGE"] = "1"
+    env = {"LLAMPC_FORCE_EXCHANGE": "1", "LLAMPC_EXCHANGE": transport}
     os.environ.update(env)
     try:
         sx = ShardedBank(bank, 0, 1, 0, W=W)
@@ -59,7 +58,7 @@ def test_exchange_tick_equals_plain_tick(nccl_world1, transport):
     sp = ShardedBank(bank, 0, 1, 0, W=W)
     try:
         assert sx.exchange and not sp.exchange
-        assert (sx._comm is not None) == (transport == "native")
+        assert sx.transport == transport
         staged = []
         for t in range(1, T + 1):
             U = np.repeat(u[:, t:t + H].T[None], C, axis=0)
@@ -94,3 +93,43 @@ def test_exchange_tick_equals_plain_tick(nccl_world1, transport):
     finally:
         sx.close()
         sp.close()
+
+
+def _mailboxes(G, bound=None):
+    import ctypes as C
+    from llampc import _native as nat
+    lib = nat.load()
+    mbs = []
+    for r in range(G):
+        mb = C.c_void_p()
+        nat.check(lib.llampc_mailbox_create(G, r, 0, C.byref(mb)))
+        if bound is not None:
+            nat.check(lib.llampc_mailbox_set_bound(mb, bound))
+        mbs.append(mb)
+    for r in range(G):
+        for g in range(G):
+            if g != r:
+                nat.check(lib.llampc_mailbox_link(mbs[r], g, mbs[g]))
+    return lib, mbs
+
+
+def test_peer_exchange_missing_rank_times_out():
+    """A rank whose peer never pushes gives up after the poll bound with status
+    LLAMPC_STATUS_POLL_TIMEOUT (the host path raises on it) instead of hanging."""
+    import time
+    import torch
+    from llampc import _native as nat
+    from llampc.mpc.sharded import _bytes_of, _out_of, probe_record
+    lib, mbs = _mailboxes(2, bound=0.05)
+    try:
+        d_in = torch.from_numpy(_bytes_of(probe_record(0, 2))).cuda()
+        d_out = torch.zeros_like(d_in)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        nat.check(lib.llampc_exchange_peer(mbs[0], d_in.data_ptr(), d_out.data_ptr(), nat.NAN_FIRST, None))
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 < 5.0
+        assert _out_of(d_out.cpu().numpy()).status == 1
+    finally:
+        for mb in mbs:
+            lib.llampc_mailbox_destroy(mb)

@@ -287,3 +287,24 @@ def test_raceline_npz_reader_reference_format(tmp_path):
     np.savez(f2, x=ref.x_raceline, y=ref.y_raceline, speed=ref.v_raceline[3], time=np.arange(n) * 0.02)
     one = Raceline.from_raceline_npz(f2)
     assert one.v_raceline.shape == (1, n) and list(one.mus) == [1.0]
+
+
+def test_exchange_probe_record_merge_and_mode(monkeypatch):
+    """The peer transport's setup probe: the host merge of probe records is the global
+    top-K by value; LLAMPC_EXCHANGE selects the transport (bad values refused)."""
+    from llampc import _native as nat
+    from llampc.mpc.sharded import exchange_mode, probe_record, records_equal
+    parts = [probe_record(r, 4) for r in range(4)]
+    m = nat.merge(parts)
+    want = sorted((parts[r].topk_val[j], parts[r].topk[j]) for r in range(4) for j in range(10))[:10]
+    assert [m.topk[j] for j in range(10)] == [i for _, i in want]
+    assert m.n_nonfinite == 0 + 1 + 2 + 3 and m.status == 0
+    assert records_equal(m, nat.merge(parts)) and not records_equal(m, parts[0])
+    monkeypatch.delenv("LLAMPC_C10D_EXCHANGE", raising=False)
+    monkeypatch.setenv("LLAMPC_EXCHANGE", "bogus")
+    with pytest.raises(ValueError):
+        exchange_mode()
+    monkeypatch.setenv("LLAMPC_EXCHANGE", "rccl")
+    assert exchange_mode() == "rccl"
+    monkeypatch.setenv("LLAMPC_C10D_EXCHANGE", "1")
+    assert exchange_mode() == "c10d"

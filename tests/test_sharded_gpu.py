@@ -1,8 +1,11 @@
-"""The N > 1 flow of the product (ShardedBank: per-shard plan kernel, all-gather of the
-records, merge_kernel) with world_size 2 and 3 on ONE GPU: the ranks share cuda:0 and gather
-over gloo (RCCL refuses two ranks on one device; test_exchange_gpu.py covers the RCCL
-transport on a 1-rank group).  Every rank's merged record, tick after tick, must equal the
-unsharded tick of the whole bank on the same inputs."""
+"""The N > 1 flow of the product (ShardedBank: per-shard plan kernel, exchange of the
+records, merge) with world_size 2 and 3 on ONE GPU: the ranks share cuda:0 (RCCL refuses two
+ranks on one device; test_exchange_gpu.py covers the RCCL transport on a 1-rank group).
+Transports: "peer" (each rank's mailbox mapped into the other processes through HIP IPC, one
+push/poll/merge kernel per tick — the ticks are enqueued back to back with no
+synchronisation, so the mailbox's two slots are reused under load) and "host" (gloo gather,
+merge_kernel).  Every rank's merged record, tick after tick, must equal the unsharded tick of
+the whole bank on the same inputs."""
 import os
 import socket
 import sys
@@ -35,8 +38,9 @@ def _ticks():
     return out
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, transport):
     try:
+        os.environ["LLAMPC_EXCHANGE"] = transport
         for pth in (REPO, PKG_ROOT):
             if pth not in sys.path:
                 sys.path.insert(0, pth)
@@ -48,10 +52,18 @@ def _worker(rank, world, port, q):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         sb = ShardedBank(generate_bank(N, seed=12), rank, world, 0, W=W)
-        recs = []
-        for a in _ticks():
-            r = sb.plan(*a, K=K, current_model=5)
-            recs.append(_bytes_of(r.raw))
+        assert sb.transport == transport, (sb.transport, transport)
+        pins = [sb.make_plan_in(sb.stage(*a)["pack"], C, H, K=K, current_model=5) for a in _ticks()]
+        torch.cuda.synchronize()
+        outs = []
+        for pin in pins:                        # back to back: no synchronisation between ticks
+            s_ = sb.launch(pin)
+            o = torch.empty_like(sb.d_merged)
+            with torch.cuda.stream(s_):
+                o.copy_(sb.d_merged)
+            outs.append(o)
+        torch.cuda.synchronize()
+        recs = [o.cpu().numpy() for o in outs]
         sb.close()
         dist.destroy_process_group()
         q.put((rank, np.stack(recs), None))
@@ -60,8 +72,9 @@ def _worker(rank, world, port, q):
         q.put((rank, None, traceback.format_exc()))
 
 
+@pytest.mark.parametrize("transport", ["peer", "host"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_tick_equals_unsharded_on_gpu(world):
+def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
     import torch.multiprocessing as mp
     from llampc import _native as nat
     from llampc.mpc import ModelBank, generate_bank
@@ -72,7 +85,7 @@ def test_sharded_tick_equals_unsharded_on_gpu(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, transport)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
