@@ -265,6 +265,15 @@ int llampc_mailbox_link(llampc_mailbox* mb, int32_t peer, const llampc_mailbox* 
 int llampc_mailbox_set_bound(llampc_mailbox* mb, double seconds);
 int llampc_exchange_peer(llampc_mailbox* mb, const void* d_local, void* d_merged, int32_t nan_policy,
                          void* stream);
+/* The sharded tick in ONE launch per rank: llampc_plan_device's tick on this rank's shard
+ * (record -> d_local) whose completing block then runs the peer exchange itself (push, poll,
+ * merge -> d_merged), so no second kernel follows the plan (RK4 look-ahead with the given
+ * xref; otherwise, for world > 16 (the merge's LDS) or with LLAMPC_PEER_SPLIT=1: the plan
+ * launch followed by llampc_exchange_peer).  Same rules as
+ * llampc_plan_device (stream, LLAMPC_E_STATE while an async tick is outstanding) and as
+ * llampc_exchange_peer (every rank makes the same sequence of exchange calls). */
+int llampc_plan_exchange(llampc_bank* bank, const llampc_plan_in* in, void* d_local, void* d_merged,
+                         llampc_mailbox* mb, void* stream);
 int llampc_mailbox_destroy(llampc_mailbox* mb);
 
 /* ---- raw batched dynamics (Dynamic API parity) ---------------------------------- */

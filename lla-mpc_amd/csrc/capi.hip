@@ -115,6 +115,18 @@ int dev_alloc(T** p, size_t count) {
 
 }  // namespace
 
+// ---- peer exchange (xGMI mailboxes) -------------------------------------------------
+struct llampc_mailbox {
+  int32_t world = 0, rank = 0, device = 0;
+  uint64_t* own = nullptr;               // [2][world][kRecWords], uncached device memory
+  uint64_t* box[kPeerMax] = {};          // every rank's mailbox as mapped in this process
+  bool opened[kPeerMax] = {};            // box[g] came from hipIpcOpenMemHandle
+  uint32_t seq = 0;
+  uint64_t bound = 200000000ull;         // 2 s of s_memrealtime (100 MHz)
+  uint64_t** d_box = nullptr;            // device copy of box[] (the fused exchange reads it)
+  bool box_synced = false;
+};
+
 struct llampc_bank {
   int device = 0;
   int64_t n = 0, goff = 0;
@@ -293,7 +305,8 @@ uint64_t poll_bound_ticks(int64_t n, int32_t C, int32_t H) {
 // Advances the window bookkeeping when a look-back runs.
 int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out, double* d_err,
                 double* d_wmean, double* d_cost, hipStream_t s, uint64_t* host_tag = nullptr,
-                uint64_t host_seq = 0, const InlinePack* pk = nullptr) {
+                uint64_t host_seq = 0, const InlinePack* pk = nullptr,
+                llampc_mailbox* px = nullptr, llampc_plan_out* px_merged = nullptr) {
   if (int rc = ensure_xref_pm(b, &in)) return rc;
   const bool lb = in.do_lookback != 0;
   const bool la = in.do_lookahead != 0;
@@ -399,6 +412,15 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   }
   f.host_tag = host_tag;
   f.host_seq = host_seq;
+  if (px) {                             // fused peer exchange (llampc_plan_exchange)
+    if (++px->seq == 0) px->seq = 1;
+    f.px_box = px->d_box;
+    f.px_merged = px_merged;
+    f.px_G = px->world;
+    f.px_rank = px->rank;
+    f.px_seq = px->seq;
+    f.px_bound = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((px->bound + 0xFFFF) >> 16, 1), UINT32_MAX);
+  }
   if (la) {
     lal.la_tag = b->d_la_tag;
     lal.blk_tag = b->d_blk_tag;
@@ -934,16 +956,6 @@ int llampc_exchange_device(const void* d_local, void* d_all, int32_t world, void
 
 }  // extern "C"
 
-// ---- peer exchange (xGMI mailboxes) -------------------------------------------------
-struct llampc_mailbox {
-  int32_t world = 0, rank = 0, device = 0;
-  uint64_t* own = nullptr;               // [2][world][kRecWords], uncached device memory
-  uint64_t* box[kPeerMax] = {};          // every rank's mailbox as mapped in this process
-  bool opened[kPeerMax] = {};            // box[g] came from hipIpcOpenMemHandle
-  uint32_t seq = 0;
-  uint64_t bound = 200000000ull;         // 2 s of s_memrealtime (100 MHz)
-};
-
 extern "C" {
 
 int llampc_mailbox_create(int32_t world, int32_t rank, int32_t device, llampc_mailbox** out) {
@@ -963,6 +975,12 @@ int llampc_mailbox_create(int32_t world, int32_t rank, int32_t device, llampc_ma
     if (mb->own) (void)hipFree(mb->own);
     delete mb;
     return fail(LLAMPC_E_HIP, "mailbox allocation: %s", hipGetErrorString(e));
+  }
+  e = hipMalloc((void**)&mb->d_box, kPeerMax * sizeof(uint64_t*));
+  if (e != hipSuccess) {
+    (void)hipFree(mb->own);
+    delete mb;
+    return fail(LLAMPC_E_HIP, "mailbox table allocation: %s", hipGetErrorString(e));
   }
   mb->box[rank] = mb->own;
   *out = mb;
@@ -989,6 +1007,7 @@ int llampc_mailbox_open_peer(llampc_mailbox* mb, int32_t peer, const void* handl
   HIP_TRY(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
   mb->box[peer] = (uint64_t*)p;
   mb->opened[peer] = true;
+  mb->box_synced = false;
   return LLAMPC_OK;
 }
 
@@ -997,6 +1016,7 @@ int llampc_mailbox_link(llampc_mailbox* mb, int32_t peer, const llampc_mailbox* 
       other->world != mb->world || other->rank != peer || other->device != mb->device)
     return fail(LLAMPC_E_ARG, "bad mailbox link (peer %d)", peer);
   mb->box[peer] = other->own;
+  mb->box_synced = false;
   return LLAMPC_OK;
 }
 
@@ -1027,6 +1047,32 @@ int llampc_exchange_peer(llampc_mailbox* mb, const void* d_local, void* d_merged
   return LLAMPC_OK;
 }
 
+int llampc_plan_exchange(llampc_bank* b, const llampc_plan_in* in, void* d_local, void* d_merged,
+                         llampc_mailbox* mb, void* stream) {
+  if (!b || !d_local || !d_merged || !mb) return fail(LLAMPC_E_ARG, "bank/d_local/d_merged/mailbox is NULL");
+  if (mb->device != b->device) return fail(LLAMPC_E_ARG, "mailbox on device %d, bank on %d", mb->device, b->device);
+  for (int g = 0; g < mb->world; ++g)
+    if (!mb->box[g]) return fail(LLAMPC_E_STATE, "mailbox of peer %d not open", g);
+  int rc = check_plan_in(b, in);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
+  DeviceGuard g(b->device);
+  hipStream_t s = pick_stream(b, stream);
+  if (!mb->box_synced) {                 // the peers are open: publish the table once
+    HIP_TRY(hipMemcpy(mb->d_box, mb->box, kPeerMax * sizeof(uint64_t*), hipMemcpyHostToDevice));
+    mb->box_synced = true;
+  }
+  const bool split = getenv("LLAMPC_PEER_SPLIT") != nullptr;   // A/B: separate kernel
+  const bool fusable = !in->do_lookahead || (in->integrator == LLAMPC_RK4 && in->xref_mode == LLAMPC_XREF_GIVEN);
+  if (!split && fusable && mb->world <= kPeerFuseMax)
+    return plan_launch(b, *in, (llampc_plan_out*)d_local, nullptr, nullptr, nullptr, s, nullptr, 0, nullptr,
+                       mb, (llampc_plan_out*)d_merged);
+  rc = plan_launch(b, *in, (llampc_plan_out*)d_local, nullptr, nullptr, nullptr, s);
+  if (rc) return rc;
+  return llampc_exchange_peer(mb, d_local, d_merged, in->nan_policy, s);
+}
+
 int llampc_mailbox_destroy(llampc_mailbox* mb) {
   if (!mb) return LLAMPC_OK;
   DeviceGuard g(mb->device);
@@ -1034,6 +1080,7 @@ int llampc_mailbox_destroy(llampc_mailbox* mb) {
   for (int r = 0; r < mb->world; ++r)
     if (mb->opened[r]) (void)hipIpcCloseMemHandle(mb->box[r]);
   if (mb->own) (void)hipFree(mb->own);
+  if (mb->d_box) (void)hipFree(mb->d_box);
   delete mb;
   return LLAMPC_OK;
 }

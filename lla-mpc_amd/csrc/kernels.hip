@@ -1431,65 +1431,6 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
   final_write(f, lb, sel, owned, kcand, kcost, scand, scost, lav, lai, nf, status);
 }
 
-// ------------------------------------------------------------------------------------
-// The tick: ONE launch.  Blocks [0, nb_lb) run the look-back, blocks [nb_lb, nb_lb+nb_la)
-// the look-ahead (the halves are independent: x_{t-1} -> x_t vs. rollouts from x_t).
-// Look-back blocks come first in dispatch order; the last of them merges the look-back
-// (lb_final) while look-ahead blocks still run; the last block overall completes the
-// llampc_plan_out record (final_select).
-// ------------------------------------------------------------------------------------
-template <int INTEG, bool STAGE, int LPM, int XM>
-__device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const LookaheadLaunch& la,
-                                          const FinalLaunch& fin, int G, int cpl) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const Scratch sc(smem);
-  int* flag = reinterpret_cast<int*>(smem + 144);
-  if ((int)blockIdx.x < fin.nb_lb) {
-    lookback_block(lb, blockIdx.x, sc);
-    if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
-    if (fin.full) {
-      lb_final(fin, smem);
-      // host completion: lb_final's record stores are performed before any later hand-off
-      // (the final block, possibly another one, publishes the host tag after them)
-      if (fin.host_tag) __threadfence_system();
-    }
-    if (fin.poll) {                   // the look-back winner completes the tick
-      __syncthreads();
-      final_poll(fin, sc);
-      return;
-    }
-  } else {
-    lookahead_block<INTEG, STAGE, LPM, XM>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
-    if (fin.poll) return;                // published tagged records; no ticket
-  }
-  const unsigned expected = (unsigned)fin.nb_la + (fin.nb_lb > 0 ? 1u : 0u);
-  if (!ticket_last(&fin.tickets[1], expected, flag)) return;
-  final_select(fin, sc);
-}
-
-template <int INTEG, bool STAGE, int LPM, int XM>
-__global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
-                                                      FinalLaunch fin, int G, int cpl) {
-  plan_body<INTEG, STAGE, LPM, XM>(lb, la, fin, G, cpl);
-}
-
-// The same tick with its inputs in the kernarg segment (InlinePack): the pointers are set to
-// the pack's fields, read by flat loads like any other input (no H2D copy on the host path).
-template <int LPM>
-__global__ __launch_bounds__(kBlock) void plan_kernel_inl(LookbackLaunch lb, LookaheadLaunch la,
-                                                          FinalLaunch fin, int G, int cpl,
-                                                          InlinePack pk) {
-  const double* v = pk.v;
-  lb.x_prev = v;
-  lb.u_prev = v + 6;
-  lb.x_now = v + 8;
-  la.x0 = v + 8;
-  la.uprev = v + 14;
-  la.xref = v + 16;
-  la.U = v + 16 + 2 * (la.H + 1);
-  plan_body<0, true, LPM, 0>(lb, la, fin, G, cpl);
-}
-
 // Cross-shard merge after the all-gather: one wave.  Scalars by lane-parallel reads and
 // shuffles; the shards' sorted top-K lists by the LDS tree merge.  merge.hpp holds the
 // same semantics as straight-line host code (llampc_merge); the tests check both agree.
@@ -1600,6 +1541,125 @@ __device__ __forceinline__ void merge_staged(const llampc_plan_out* rec, int32_t
   m->n_nonfinite = nf;
 }
 
+// Fused peer exchange, run by the block that completed this rank's record (after final_poll /
+// final_select): the record's words are read back, pushed as tagged words into slot [seq & 1][rank] of every mailbox, and the
+// px_G slots of this rank's mailbox are polled into LDS and merged (peer_exchange_kernel's
+// protocol and merge; its comment has the slot-reuse argument).
+__device__ __forceinline__ void peer_finish(const FinalLaunch& f, unsigned char* smem) {
+  const int tid = threadIdx.x;
+  const int G = f.px_G;
+  constexpr int kW2 = kRecWords / 2;            // the record as 64-bit loads
+  static_assert(kRecWords % 2 == 0, "record of whole 64-bit words");
+  // The record is read back with plain loads after the block barrier: this block wrote it
+  // (poll path: lb_final and final_poll run here), or the rest of it was released to this
+  // block by the completion tickets (ticket path).  No agent-scope fence: on MI355X that is
+  // an L2 writeback of the XCD (measured ~3 us per tick here).
+  __syncthreads();
+  const size_t slot0 = (size_t)(f.px_seq & 1) * G * kRecWords;
+  const size_t mine = slot0 + (size_t)f.px_rank * kRecWords;
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(f.out);
+  unsigned char* base = smem + 256;             // past the scratch the completion used
+  uint32_t* rec32 = reinterpret_cast<uint32_t*>(base);
+  uint64_t* rec_mine = reinterpret_cast<uint64_t*>(base + (size_t)f.px_rank * sizeof(llampc_plan_out));
+  for (int w = tid; w < kW2; w += kBlock) {
+    const uint64_t v = src[w];
+    rec_mine[w] = v;                            // this rank's record: straight to LDS
+    const uint64_t lo = tag_word(f.px_seq, (uint32_t)v), hi = tag_word(f.px_seq, (uint32_t)(v >> 32));
+    for (int g = 0; g < G; ++g) {
+      if (g == f.px_rank) continue;
+      uint64_t* d = f.px_box[g] + mine + 2 * w;
+      __hip_atomic_store(d, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(d + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  const uint64_t* own = f.px_box[f.px_rank] + slot0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t bound = (uint64_t)f.px_bound << 16;
+  const int skip0 = f.px_rank * kRecWords, skip1 = skip0 + kRecWords;
+  int late = 0;
+  for (int e = tid; e < G * kRecWords; e += kBlock) {
+    if (e >= skip0 && e < skip1) continue;       // this rank's slot is not read back
+    uint64_t v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    while (!tag_ok(v, f.px_seq)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > bound) { late = 1; break; }
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    rec32[e] = (uint32_t)v;
+  }
+  EntS* lists = reinterpret_cast<EntS*>(base + (size_t)G * sizeof(llampc_plan_out));
+  int* wave_late = reinterpret_cast<int*>(lists + 2 * (size_t)G * LLAMPC_KMAX);
+  const int wl = __any(late);
+  if ((tid & 63) == 0) wave_late[tid >> 6] = wl;
+  __syncthreads();
+  late = 0;
+  for (int w = 0; w < kWaves; ++w) late |= wave_late[w];
+  merge_staged(reinterpret_cast<const llampc_plan_out*>(base), G, f.nan_first, f.px_merged, lists, late);
+}
+
+// ------------------------------------------------------------------------------------
+// The tick: ONE launch.  Blocks [0, nb_lb) run the look-back, blocks [nb_lb, nb_lb+nb_la)
+// the look-ahead (the halves are independent: x_{t-1} -> x_t vs. rollouts from x_t).
+// Look-back blocks come first in dispatch order; the last of them merges the look-back
+// (lb_final) while look-ahead blocks still run; the last block overall completes the
+// llampc_plan_out record (final_select).
+// ------------------------------------------------------------------------------------
+template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false>
+__device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const LookaheadLaunch& la,
+                                          const FinalLaunch& fin, int G, int cpl) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Scratch sc(smem);
+  int* flag = reinterpret_cast<int*>(smem + 144);
+  if ((int)blockIdx.x < fin.nb_lb) {
+    lookback_block(lb, blockIdx.x, sc);
+    if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
+    if (fin.full) {
+      lb_final(fin, smem);
+      // host completion: lb_final's record stores are performed before any later hand-off
+      // (the final block, possibly another one, publishes the host tag after them)
+      if (fin.host_tag) __threadfence_system();
+    }
+    if (fin.poll) {                   // the look-back winner completes the tick
+      __syncthreads();
+      final_poll(fin, sc);
+      if constexpr (PX) peer_finish(fin, smem);
+      return;
+    }
+  } else {
+    lookahead_block<INTEG, STAGE, LPM, XM>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
+    if (fin.poll) return;                // published tagged records; no ticket
+  }
+  const unsigned expected = (unsigned)fin.nb_la + (fin.nb_lb > 0 ? 1u : 0u);
+  if (!ticket_last(&fin.tickets[1], expected, flag)) return;
+  final_select(fin, sc);
+  if constexpr (PX) peer_finish(fin, smem);
+}
+
+// PX: the sharded tick's fused peer exchange (a separate instantiation, so the plain tick's
+// code is unchanged: inlining it into every variant cost the headline tick 0.5 us)
+template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false>
+__global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
+                                                      FinalLaunch fin, int G, int cpl) {
+  plan_body<INTEG, STAGE, LPM, XM, PX>(lb, la, fin, G, cpl);
+}
+
+// The same tick with its inputs in the kernarg segment (InlinePack): the pointers are set to
+// the pack's fields, read by flat loads like any other input (no H2D copy on the host path).
+template <int LPM>
+__global__ __launch_bounds__(kBlock) void plan_kernel_inl(LookbackLaunch lb, LookaheadLaunch la,
+                                                          FinalLaunch fin, int G, int cpl,
+                                                          InlinePack pk) {
+  const double* v = pk.v;
+  lb.x_prev = v;
+  lb.u_prev = v + 6;
+  lb.x_now = v + 8;
+  la.x0 = v + 8;
+  la.uprev = v + 14;
+  la.xref = v + 16;
+  la.U = v + 16 + 2 * (la.H + 1);
+  plan_body<0, true, LPM, 0>(lb, la, fin, G, cpl);
+}
+
 __global__ __launch_bounds__(kBlock) void merge_kernel(const llampc_plan_out* parts, int32_t G,
                                                        int32_t nan_first, llampc_plan_out* m) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1618,8 +1678,8 @@ __global__ __launch_bounds__(kBlock) void merge_kernel(const llampc_plan_out* pa
 // Peer exchange (xGMI, no collective library): every rank's mailbox is uncached device
 // memory mapped into every peer process (IPC).  One block per rank per tick:
 //  1. push — this rank's record as tagged 64-bit words (tick seq << 32 | 32 payload bits)
-//     into slot [seq & 1][rank] of every mailbox (its own included), system-scope stores
-//     that go straight over xGMI into the peer's HBM;
+//     into slot [seq & 1][rank] of every peer's mailbox, system-scope stores that go straight
+//     over xGMI into the peer's HBM (its own copy goes straight to LDS);
 //  2. poll — every thread spins on its share of the G slots of its own mailbox until each
 //     word carries this tick's seq (every word validates itself: no fence pairing across
 //     devices), unpacking the payloads into the LDS records;
@@ -1635,17 +1695,21 @@ __global__ __launch_bounds__(kBlock) void peer_exchange_kernel(PeerLaunch a) {
   const int G = a.G;
   const size_t slot0 = (size_t)(a.seq & 1) * G * kW;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(a.local);
+  uint32_t* rec32 = reinterpret_cast<uint32_t*>(smem);
   for (int w = tid; w < kW; w += kBlock) {
-    const uint64_t v = tag_word(a.seq, src[w]);
+    const uint32_t x = src[w];
+    rec32[a.rank * kW + w] = x;                 // this rank's record: straight to LDS
+    const uint64_t v = tag_word(a.seq, x);
     const size_t off = slot0 + (size_t)a.rank * kW + w;
     for (int g = 0; g < G; ++g)
-      __hip_atomic_store(a.box[g] + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (g != a.rank) __hip_atomic_store(a.box[g] + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  uint32_t* rec32 = reinterpret_cast<uint32_t*>(smem);
   const uint64_t* own = a.box[a.rank] + slot0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int skip0 = a.rank * kW, skip1 = skip0 + kW;
   int late = 0;
   for (int e = tid; e < G * kW; e += kBlock) {
+    if (e >= skip0 && e < skip1) continue;       // this rank's slot is not read back
     uint64_t v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     while (!tag_ok(v, a.seq)) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > a.bound) { late = 1; break; }
@@ -1834,6 +1898,14 @@ template <int INTEG, bool STAGE, int LPM>
 static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
                           int G, int cpl, size_t lds, hipStream_t s) {
   lds = std::max(lds, kOneBlockPerCuLds);
+  if constexpr (INTEG == LLAMPC_RK4) {
+    if (f.px_G) {                        // given xref only (launch_plan checks)
+      allow_lds(plan_kernel<INTEG, STAGE, LPM, 0, true>);
+      hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, LPM, 0, true>), dim3(f.nb_lb + f.nb_la), dim3(kBlock), lds,
+                         s, lb, la, f, G, cpl);
+      return;
+    }
+  }
   if (la.xref_mode == LLAMPC_XREF_RACELINE) {
     allow_lds(plan_kernel<INTEG, STAGE, LPM, 1>);
     hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, LPM, 1>), dim3(f.nb_lb + f.nb_la), dim3(kBlock), lds, s,
@@ -1918,6 +1990,12 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
   f.do_lb = lb != nullptr;
   f.do_la = la != nullptr;
   if (f.nb_lb + f.nb_la == 0) return hipErrorInvalidValue;
+  if (f.px_G) {                          // fused peer exchange: RK4, given xref, device inputs
+    if (pk || integ != LLAMPC_RK4 || (la && la->xref_mode == LLAMPC_XREF_RACELINE) || f.px_G > kPeerFuseMax)
+      return hipErrorInvalidValue;
+    lds = std::max(lds, 256 + (size_t)f.px_G * (sizeof(llampc_plan_out) + 2 * LLAMPC_KMAX * sizeof(EntS)) +
+                            kWaves * sizeof(int));
+  }
 
   if (pk) {
     if (!la || !plan_inline_ok(la->C, la->H, integ, la->xref_mode) || !stage) return hipErrorInvalidValue;

@@ -83,6 +83,15 @@ struct FinalLaunch {
   // copy + stream synchronisation.  Null for device-resident ticks.
   uint64_t* host_tag;
   uint64_t host_seq;
+  // fused peer exchange (llampc_plan_exchange; px_G = 0: none): after the record is complete,
+  // the block that completed it pushes it into every rank's mailbox (px_box: device array of
+  // the px_G mailboxes as mapped here), polls this rank's, and merges into px_merged — the
+  // sharded tick in one launch per rank (peer_exchange_kernel's protocol)
+  uint64_t* const* px_box;
+  llampc_plan_out* px_merged;
+  int32_t px_G, px_rank;
+  uint32_t px_seq;
+  uint32_t px_bound;                      // poll bound, units of 2^16 s_memrealtime ticks
 };
 
 // Tick inputs in the kernarg segment (host-pointer ticks whose pack fits): x_prev[6],
@@ -122,6 +131,8 @@ struct PeerLaunch {
   uint32_t seq;                          // tick number, never 0 (the mailbox starts zeroed)
 };
 hipError_t launch_peer_exchange(const PeerLaunch& a, hipStream_t s);
+// Largest world the plan launch can merge in its own LDS (records + lists, see launch_plan).
+constexpr int kPeerFuseMax = 16;
 hipError_t launch_dynamics(int32_t op, const double* x, const double* u, const double* params,
                            int64_t P, VehK veh, int64_t n, double* out, hipStream_t s);
 hipError_t launch_math(int32_t fn, const double* a, const double* b, int64_t n, double* out,

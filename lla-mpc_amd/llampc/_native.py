@@ -109,6 +109,8 @@ _SIGNATURES = {
     "llampc_mailbox_link": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
     "llampc_mailbox_set_bound": (C.c_int, [C.c_void_p, C.c_double]),
     "llampc_exchange_peer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "llampc_plan_exchange": (C.c_int, [C.c_void_p, C.POINTER(PlanIn), C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]),
     "llampc_mailbox_destroy": (C.c_int, [C.c_void_p]),
     "llampc_dynamics_batch": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                         C.POINTER(Vehicle), C.c_int64, C.c_void_p, C.c_int32,
@@ -148,6 +150,9 @@ def load():
                               "`make -C lla-mpc_amd/csrc` (there is no CPU fallback)")
         lib = C.CDLL(path)
         for name, (res, args) in _SIGNATURES.items():
+            # an A/B build named by LLAMPC_HIP_LIB may predate newer entry points
+            if path != _LIB_PATH and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

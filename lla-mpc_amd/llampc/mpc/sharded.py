@@ -12,9 +12,10 @@ same merge code runs on the host (llampc_merge).
 
 Transports of the exchange (LLAMPC_EXCHANGE; the merged record is the same for all):
   peer  (default when it verifies) — no collective library: every rank's mailbox (uncached
-        device memory) is mapped into every peer through HIP IPC, and ONE kernel per tick
-        pushes this rank's record into all mailboxes over xGMI, polls its own until the tick's
-        records have arrived and merges (llampc_exchange_peer).  Set up with one
+        device memory) is mapped into every peer through HIP IPC, and the tick's own plan
+        launch, once its record is complete, pushes it into all mailboxes over xGMI, polls its
+        own until the tick's records have arrived and merges (llampc_plan_exchange: one launch
+        per rank per tick; LLAMPC_PEER_SPLIT=1 runs the exchange as a second kernel).  Set up with one
         all_gather_object of the IPC handles on any backend (gloo included), then checked by a
         probe exchange against the host merge; on any failure every rank falls back together.
   rccl  — ncclAllGather of the process's RCCL on the tick stream + merge_kernel.
@@ -277,12 +278,13 @@ class ShardedBank:
         torch = self._torch
         s = self.tick_stream(stream)
         lib = nat.load()
+        if self._mailbox is not None:        # peer: the plan launch pushes, polls and merges
+            nat.check(lib.llampc_plan_exchange(self.bank.handle, C.byref(pin), self.d_local.data_ptr(),
+                                               self.d_merged.data_ptr(), self._mailbox, s.cuda_stream))
+            return s
         nat.check(lib.llampc_plan_device(self.bank.handle, C.byref(pin), self.d_local.data_ptr(),
                                          None, None, None, s.cuda_stream))
-        if self._mailbox is not None:        # peer: push + poll + merge, one kernel on stream s
-            nat.check(lib.llampc_exchange_peer(self._mailbox, self.d_local.data_ptr(), self.d_merged.data_ptr(),
-                                               pin.nan_policy, s.cuda_stream))
-        elif self._comm is not None:           # native: all-gather + merge on stream s
+        if self._comm is not None:           # native: all-gather + merge on stream s
             nat.check(lib.llampc_exchange_device(self.d_local.data_ptr(), self.d_all.data_ptr(), self.world,
                                                  self.d_merged.data_ptr(), pin.nan_policy, self._comm,
                                                  self._allgather, self.device, s.cuda_stream))

@@ -37,8 +37,8 @@ def nccl_world1():
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("transport", ["peer", "rccl", "c10d"])
-def test_exchange_tick_equals_plain_tick(nccl_world1, transport):
+@pytest.mark.parametrize("transport", ["peer", "peer-ticket", "peer-split", "rccl", "c10d"])
+def test_exchange_tick_equals_plain_tick(nccl_world1, transport, monkeypatch):
     import torch
     from llampc import _native as nat
     from llampc.mpc import generate_bank
@@ -48,6 +48,12 @@ def test_exchange_tick_equals_plain_tick(nccl_world1, transport):
     N, H, C, W, K, T = 4000, 20, 2, 4, 6, 12
     rng = np.random.RandomState(5)
     bank = generate_bank(N, seed=6)
+    if transport == "peer-split":            # the plan launch, then peer_exchange_kernel
+        monkeypatch.setenv("LLAMPC_PEER_SPLIT", "1")
+        transport = "peer"
+    if transport == "peer-ticket":           # fused exchange after the ticket completion
+        monkeypatch.setenv("LLAMPC_NO_POLL", "1")
+        transport = "peer"
     env = {"LLAMPC_FORCE_EXCHANGE": "1", "LLAMPC_EXCHANGE": transport}
     os.environ.update(env)
     try:

@@ -1,9 +1,10 @@
 """The N > 1 flow of the product (ShardedBank: per-shard plan kernel, exchange of the
 records, merge) with world_size 2 and 3 on ONE GPU: the ranks share cuda:0 (RCCL refuses two
 ranks on one device; test_exchange_gpu.py covers the RCCL transport on a 1-rank group).
-Transports: "peer" (each rank's mailbox mapped into the other processes through HIP IPC, one
-push/poll/merge kernel per tick — the ticks are enqueued back to back with no
-synchronisation, so the mailbox's two slots are reused under load) and "host" (gloo gather,
+Transports: "peer" (each rank's mailbox mapped into the other processes through HIP IPC; the
+plan launch itself pushes, polls and merges — "peer-split": a second kernel does — with the
+ticks enqueued back to back with no synchronisation, so the mailbox's two slots are reused
+under load) and "host" (gloo gather,
 merge_kernel).  Every rank's merged record, tick after tick, must equal the unsharded tick of
 the whole bank on the same inputs."""
 import os
@@ -40,6 +41,9 @@ def _ticks():
 
 def _worker(rank, world, port, q, transport):
     try:
+        if transport == "peer-split":
+            os.environ["LLAMPC_PEER_SPLIT"] = "1"
+            transport = "peer"
         os.environ["LLAMPC_EXCHANGE"] = transport
         for pth in (REPO, PKG_ROOT):
             if pth not in sys.path:
@@ -72,7 +76,7 @@ def _worker(rank, world, port, q, transport):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("transport", ["peer", "host"])
+@pytest.mark.parametrize("transport", ["peer", "peer-split", "host"])
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
     import torch.multiprocessing as mp
