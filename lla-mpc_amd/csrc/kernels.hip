@@ -1392,13 +1392,10 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
       lai = t ? pi : lai;
     }
   }
-  // (no __syncthreads_or: its static LDS would break the launches' full-LDS requests)
-  int* any_late = reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(sc.sv) + 152);
-  if (tid == 0) *any_late = 0;
-  __syncthreads();
-  if (late) *any_late = 1;
-  __syncthreads();
-  if (*any_late) status = kPollTimeoutStatus;
+  // the waves' late flags travel with the block reduction's LDS exchange below (one barrier;
+  // no __syncthreads_or: its static LDS would break the launches' full-LDS requests)
+  unsigned char* late_w = reinterpret_cast<unsigned char*>(sc.sv) + 152;
+  const int wlate = __any((int)late);
   int32_t kcand = -1, scand = -1;
   double kcost = __builtin_nan(""), scost = __builtin_nan("");
   if (mk >= 0 && f.do_la) {
@@ -1415,18 +1412,22 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
     sc.sv[4 + (tid >> 6)] = lav;
     sc.si[4 + (tid >> 6)] = lai;
     sc.sn[tid >> 6] = nf;
+    late_w[tid >> 6] = (unsigned char)wlate;
   }
   __syncthreads();
   lav = sc.sv[4];
   lai = sc.si[4];
   nf = sc.sn[0];
+  int anyl = late_w[0];
 #pragma unroll
   for (int w = 1; w < kWaves; ++w) {
     const bool t = (int)(sc.si[4 + w] != kNoIndex) & (int)less_bf<0>(sc.sv[4 + w], sc.si[4 + w], lav, lai);
     lav = t ? sc.sv[4 + w] : lav;
     lai = t ? sc.si[4 + w] : lai;
     nf += sc.sn[w];
+    anyl |= late_w[w];
   }
+  if (anyl) status = kPollTimeoutStatus;
   STAMP(4);
   final_write(f, lb, sel, owned, kcand, kcost, scand, scost, lav, lai, nf, status);
 }
