@@ -46,7 +46,7 @@ ISSUE_PEAK_LANE_INSTR = 1024 * 16 * 2.4e9
 
 
 EXCHANGE_DESC = {
-    "peer": "peer mailboxes over xGMI (HIP IPC): one push/poll/merge kernel per tick (llampc_exchange_peer)",
+    "peer": "peer mailboxes over xGMI (HIP IPC): the plan launch pushes its record, polls and merges (llampc_plan_exchange)",
     "rccl": "native RCCL all-gather on the tick stream (llampc_exchange_device) + merge_kernel",
     "c10d": "c10d all_gather_into_tensor (nccl) + merge_kernel",
     "host": "gloo all-gather on the host + merge_kernel",
@@ -212,6 +212,8 @@ def main():
     def step(i):
         sb.launch(pins[i % T], stream)
 
+    if world > 1:                       # every rank's exchange waits for the others' records
+        dist.barrier()
     for i in range(args.warmup):
         step(i)
     if not args.no_timing:
@@ -321,6 +323,9 @@ def extras(args, sb, stream, world, rank=0):
     p64 = torch.from_numpy(t64).to(torch.device("cuda", sb.device))
     torch.cuda.synchronize()
     pins = [sb.make_plan_in(p64[i], 64, H, K=args.K) for i in range(8)]
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
     for i in range(5):
         sb.launch(pins[i % 8], stream)
     torch.cuda.synchronize()

@@ -252,7 +252,7 @@ int llampc_exchange_device(const void* d_local, void* d_all, int32_t world, void
  * llampc_exchange_device's.  Setup: create, export the IPC handle (64 bytes), share the
  * handles out of band (e.g. a torch.distributed all_gather_object), open every peer's.  All
  * ranks must call llampc_exchange_peer the same number of times (the tick number is the tag).
- * A rank that waits more than the poll bound (default 2 s; set_bound) gets status
+ * A rank that waits more than the poll bound (default 10 s; set_bound) gets status
  * LLAMPC_STATUS_POLL_TIMEOUT in d_merged.  Replaces the same reference-side gather as
  * llampc_exchange_device. */
 typedef struct llampc_mailbox llampc_mailbox;

@@ -122,7 +122,8 @@ struct llampc_mailbox {
   uint64_t* box[kPeerMax] = {};          // every rank's mailbox as mapped in this process
   bool opened[kPeerMax] = {};            // box[g] came from hipIpcOpenMemHandle
   uint32_t seq = 0;
-  uint64_t bound = 200000000ull;         // 2 s of s_memrealtime (100 MHz)
+  uint64_t bound = 1000000000ull;        // 10 s of s_memrealtime (100 MHz): ranks may drift apart
+                                         // by host-side pauses; only a missing rank should time out
   uint64_t** d_box = nullptr;            // device copy of box[] (the fused exchange reads it)
   bool box_synced = false;
 };

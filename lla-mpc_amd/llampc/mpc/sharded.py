@@ -190,6 +190,7 @@ class ShardedBank:
             want = nat.merge(parts, nat.NAN_FIRST)
             d_in = torch.from_numpy(_bytes_of(rec)).to(dev)
             d_out = torch.zeros_like(d_in)
+            torch.cuda.current_stream(dev).synchronize()   # the fill above ran on torch's stream
             try:
                 nat.check(lib.llampc_exchange_peer(mb, d_in.data_ptr(), d_out.data_ptr(), nat.NAN_FIRST,
                                                    self.stream.cuda_stream))
