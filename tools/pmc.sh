@@ -14,12 +14,12 @@ for group in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_AN
              "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $group --output-format csv -d gpurun_out/pmc/p$i -o run -- \
-     python3 bench.py $ARGS --no-cpu-baseline --no-extra --no-timing > gpurun_out/pmc/p$i.log 2>&1 || { echo "pass $i failed: $group"; tail -5 gpurun_out/pmc/p$i.log; }
+     python3 bench.py $ARGS --no-cpu-baseline --no-extra --no-timing > gpurun_out/pmc/p$i.log 2>&1 || { echo "pass $i failed: $group"; tail -5 gpurun_out/pmc/p$i.log; exit 1; }
 done
 # calibration dispatch for the 8-B/lane FETCH/WRITE counters (tools/pmc_calib.py)
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 240 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc/cal_$c -o run -- \
-     python3 tools/pmc_calib.py > gpurun_out/pmc/cal_$c.log 2>&1 || { echo "calibration $c failed"; tail -5 gpurun_out/pmc/cal_$c.log; }
+     python3 tools/pmc_calib.py > gpurun_out/pmc/cal_$c.log 2>&1 || { echo "calibration $c failed"; tail -5 gpurun_out/pmc/cal_$c.log; exit 1; }
 done
 python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.txt 2>&1; cat gpurun_out/pmc/summary.txt
 if [ -n "$PMC_KEY" ]; then python3 tools/pmc_traffic.py gpurun_out/pmc "$PMC_KEY"; fi

@@ -48,3 +48,4 @@ except (OSError, ValueError):
 d[key] = out
 json.dump(d, open(path, "w"), indent=1)
 print(json.dumps({key: out}, indent=1))
+json.dump({key: out}, open(os.path.join(sys.argv[1], "pmc_lookahead_entry.json"), "w"), indent=1)
