@@ -43,6 +43,26 @@ def shard_range(n_global: int, rank: int, world: int) -> tuple[int, int]:
     return lo, hi
 
 
+_Z6, _Z2 = np.zeros(6), np.zeros(2)
+
+
+def _pin_template() -> "nat.PlanIn":
+    """The PlanIn fields _plan_in leaves at their defaults unless asked (rk4, look-back and
+    look-ahead, NAN_FIRST, current model 0, Ts 0.02, the rt.py cost, shared xref)."""
+    pin = nat.PlanIn()
+    pin.integrator = nat.RK4
+    pin.do_lookback = pin.do_lookahead = 1
+    pin.nan_policy = nat.NAN_FIRST
+    pin.current_model = 0
+    pin.Ts = 0.02
+    pin.cost = nat.default_cost()
+    pin.xref_mode = nat.XREF_GIVEN
+    return pin
+
+
+_PIN_TEMPLATE = _pin_template()
+
+
 class ModelBank:
     """A shard of the model bank resident on one HIP device."""
 
@@ -181,27 +201,38 @@ class ModelBank:
         U = nat.f64(U)
         if U.ndim == 2:
             U = U.reshape(1, *U.shape)
-        # one packed array, one address lookup (~1 us each in NumPy): pointers = base + offsets
-        parts = [np.zeros(6) if x_prev is None else x_prev, np.zeros(2) if u_prev is None else u_prev,
-                 x_now, uprev, xref, U]
-        flat = [np.asarray(a, dtype=np.float64).ravel() for a in parts]
+        # one packed array, one address lookup (~1 us each in NumPy): pointers = base + offsets;
+        # the constant fields come from a per-bank template (a struct copy, not ~15 setattrs)
+        flat = (np.ravel(_Z6 if x_prev is None else x_prev), np.ravel(_Z2 if u_prev is None else u_prev),
+                np.ravel(x_now), np.ravel(uprev), np.ravel(xref), U.reshape(-1))
         pack = np.concatenate(flat)
+        if pack.dtype != np.float64:
+            pack = pack.astype(np.float64)
         keep = [pack]
-        base, off = pack.ctypes.data, 0
-        ptrs = []
-        for a in flat:
-            ptrs.append(base + 8 * off)
-            off += a.size
-        pin = nat.PlanIn()
-        pin.x_prev, pin.u_prev, pin.x_now, pin.uprev, pin.xref, pin.U = ptrs
+        base = pack.ctypes.data
+        o1 = flat[0].size
+        o2 = o1 + flat[1].size
+        o3 = o2 + flat[2].size
+        o4 = o3 + flat[3].size
+        o5 = o4 + flat[4].size
+        pin = nat.PlanIn.from_buffer_copy(_PIN_TEMPLATE)
+        pin.x_prev, pin.u_prev, pin.x_now = base, base + 8 * o1, base + 8 * o2
+        pin.uprev, pin.xref, pin.U = base + 8 * o3, base + 8 * o4, base + 8 * o5
         pin.C, pin.H, pin.K = U.shape[0], U.shape[1], int(K)
-        pin.integrator = nat.INTEGRATORS[integrator]
-        pin.do_lookback, pin.do_lookahead = int(bool(do_lookback)), int(bool(do_lookahead))
-        pin.nan_policy = int(nan_policy)
-        pin.current_model = int(current_model)
-        pin.Ts = float(Ts)
-        pin.cost = cost if cost is not None else nat.default_cost()
-        pin.xref_mode = nat.XREF_RACELINE if raceline_start is not None else nat.XREF_GIVEN
+        if integrator != "rk4":
+            pin.integrator = nat.INTEGRATORS[integrator]
+        if not (do_lookback and do_lookahead):
+            pin.do_lookback, pin.do_lookahead = int(bool(do_lookback)), int(bool(do_lookahead))
+        if nan_policy:
+            pin.nan_policy = int(nan_policy)
+        if current_model:
+            pin.current_model = int(current_model)
+        if Ts != 0.02:
+            pin.Ts = float(Ts)
+        if cost is not None:
+            pin.cost = cost
+        if raceline_start is not None:
+            pin.xref_mode = nat.XREF_RACELINE
         return pin, keep
 
     def plan_raw(self, x_prev, u_prev, x_now, U, xref, uprev, Ts=0.02, K=10, integrator="rk4",
