@@ -308,3 +308,37 @@ def test_exchange_probe_record_merge_and_mode(monkeypatch):
     assert exchange_mode() == "rccl"
     monkeypatch.setenv("LLAMPC_C10D_EXCHANGE", "1")
     assert exchange_mode() == "c10d"
+
+
+def test_plan_in_builder_pointers_and_fields():
+    """The host tick's PlanIn (ModelBank._plan_in, no device needed): every input pointer
+    addresses its own values in the packed array, defaults come from the template, and each
+    non-default argument lands in its field."""
+    import ctypes as C
+    from llampc import _native as nat
+    from llampc.mpc.bank import ModelBank
+    rng = np.random.RandomState(3)
+    x_prev, u_prev, x_now, uprev = rng.randn(6), rng.randn(2), rng.randn(6), rng.randn(2)
+    U, xref = rng.randn(3, 7, 2), rng.randn(2, 8)
+
+    def read(addr, n):
+        return np.ctypeslib.as_array((C.c_double * n).from_address(addr)).copy()
+
+    pin, keep = ModelBank._plan_in(None, x_prev, u_prev, x_now, U, xref, uprev, 0.02, 10, "rk4",
+                                   True, True, 0, nat.NAN_FIRST, None)
+    for addr, want in ((pin.x_prev, x_prev), (pin.u_prev, u_prev), (pin.x_now, x_now),
+                       (pin.uprev, uprev), (pin.xref, xref.ravel()), (pin.U, U.ravel())):
+        np.testing.assert_array_equal(read(addr, want.size), want)
+    assert (pin.C, pin.H, pin.K, pin.integrator, pin.do_lookback, pin.do_lookahead) == (3, 7, 10, nat.RK4, 1, 1)
+    assert (pin.nan_policy, pin.current_model, pin.Ts, pin.xref_mode) == (nat.NAN_FIRST, 0, 0.02, nat.XREF_GIVEN)
+    assert bytes(pin.cost) == bytes(nat.default_cost())
+    cost = nat.cost_struct(enforce_bounds=True)
+    pin, keep = ModelBank._plan_in(None, None, None, list(x_now), U[0], None, uprev, 0.01, 4, "euler_nlp",
+                                   False, True, 17, nat.NAN_IGNORE, cost, (1.5, 2.0, 0.9))
+    np.testing.assert_array_equal(read(pin.x_prev, 6), np.zeros(6))
+    np.testing.assert_array_equal(read(pin.x_now, 6), x_now)
+    np.testing.assert_array_equal(read(pin.xref, 4), [1.5, 2.0, 0.9, 0.0])
+    np.testing.assert_array_equal(read(pin.U, 14), U[0].ravel())
+    assert (pin.C, pin.H, pin.K, pin.integrator, pin.do_lookback) == (1, 7, 4, nat.EULER_NLP, 0)
+    assert (pin.nan_policy, pin.current_model, pin.Ts, pin.xref_mode) == (nat.NAN_IGNORE, 17, 0.01, nat.XREF_RACELINE)
+    assert bytes(pin.cost) == bytes(cost)
