@@ -1,5 +1,5 @@
 """The N > 1 flow of the product (ShardedBank: per-shard plan kernel, exchange of the
-records, merge) with world_size 2 and 3 on ONE GPU: the ranks share cuda:0 (RCCL refuses two
+records, merge) with world_size 2, 3 and 4 on ONE GPU: the ranks share cuda:0 (RCCL refuses two
 ranks on one device; test_exchange_gpu.py covers the RCCL transport on a 1-rank group).
 Transports: "peer" (each rank's mailbox mapped into the other processes through HIP IPC; the
 plan launch itself pushes, polls and merges — "peer-split": a second kernel does — with the
@@ -77,7 +77,7 @@ def _worker(rank, world, port, q, transport):
 
 
 @pytest.mark.parametrize("transport", ["peer", "peer-split", "host"])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
     import torch.multiprocessing as mp
     from llampc import _native as nat
