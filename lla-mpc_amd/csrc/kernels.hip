@@ -1955,6 +1955,9 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
   if (lb) {
     lbv = *lb;
     lbv.R = lookback_r(lb->n, std::max(1, lb->K));
+    // A/B knob: at least LLAMPC_LB_R models per look-back lane (fewer look-back blocks)
+    static const int r_min = getenv("LLAMPC_LB_R") ? std::max(1, atoi(getenv("LLAMPC_LB_R"))) : 1;
+    lbv.R = std::max(lbv.R, r_min);
     f.nb_lb = lookback_blocks_r(lb->n, lbv.R);
     if (lb->full) {
       const size_t M = (size_t)f.nb_lb * lb->K, L = f.nb_lb;   // lb_final (layout there)
