@@ -126,6 +126,7 @@ struct llampc_mailbox {
                                          // by host-side pauses; only a missing rank should time out
   uint64_t** d_box = nullptr;            // device copy of box[] (the fused exchange reads it)
   bool box_synced = false;
+  std::mutex mu;                         // serialises the tick sequence (seq) and the table
 };
 
 struct llampc_bank {
@@ -1002,6 +1003,7 @@ int llampc_mailbox_open_peer(llampc_mailbox* mb, int32_t peer, const void* handl
     return fail(LLAMPC_E_ARG, "bad peer %d (world %d, rank %d, or already open)", mb ? peer : -1,
                 mb ? mb->world : 0, mb ? mb->rank : 0);
   DeviceGuard g(mb->device);
+  std::lock_guard<std::mutex> lm(mb->mu);
   hipIpcMemHandle_t h;
   memcpy(&h, handle, sizeof(h));
   void* p = nullptr;
@@ -1016,6 +1018,7 @@ int llampc_mailbox_link(llampc_mailbox* mb, int32_t peer, const llampc_mailbox* 
   if (!mb || !other || peer < 0 || peer >= mb->world || peer == mb->rank || mb->box[peer] ||
       other->world != mb->world || other->rank != peer || other->device != mb->device)
     return fail(LLAMPC_E_ARG, "bad mailbox link (peer %d)", peer);
+  std::lock_guard<std::mutex> lm(mb->mu);
   mb->box[peer] = other->own;
   mb->box_synced = false;
   return LLAMPC_OK;
@@ -1034,6 +1037,7 @@ int llampc_exchange_peer(llampc_mailbox* mb, const void* d_local, void* d_merged
     if (!mb->box[g]) return fail(LLAMPC_E_STATE, "mailbox of peer %d not open", g);
   DeviceGuard g(mb->device);
   if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", mb->device);
+  std::lock_guard<std::mutex> lm(mb->mu);
   if (++mb->seq == 0) mb->seq = 1;       // 0 is the zeroed mailbox's tag
   PeerLaunch a{};
   a.local = (const llampc_plan_out*)d_local;
@@ -1060,6 +1064,7 @@ int llampc_plan_exchange(llampc_bank* b, const llampc_plan_in* in, void* d_local
   if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
   DeviceGuard g(b->device);
   hipStream_t s = pick_stream(b, stream);
+  std::unique_lock<std::mutex> lm(mb->mu);
   if (!mb->box_synced) {                 // the peers are open: publish the table once
     HIP_TRY(hipMemcpy(mb->d_box, mb->box, kPeerMax * sizeof(uint64_t*), hipMemcpyHostToDevice));
     mb->box_synced = true;
@@ -1071,6 +1076,7 @@ int llampc_plan_exchange(llampc_bank* b, const llampc_plan_in* in, void* d_local
                        mb, (llampc_plan_out*)d_merged);
   rc = plan_launch(b, *in, (llampc_plan_out*)d_local, nullptr, nullptr, nullptr, s);
   if (rc) return rc;
+  lm.unlock();                           // llampc_exchange_peer takes it
   return llampc_exchange_peer(mb, d_local, d_merged, in->nan_policy, s);
 }
 
