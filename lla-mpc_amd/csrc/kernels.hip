@@ -1542,6 +1542,58 @@ __device__ __forceinline__ void merge_staged(const llampc_plan_out* rec, int32_t
   m->n_nonfinite = nf;
 }
 
+// Poll this rank's mailbox slots [G][kRecWords] (tick parity already applied) for the G-1 peer
+// records of tick `seq`, unpacking the payloads into rec32 (LDS).  Every round issues ALL of a
+// thread's loads before it checks any (unconditional loads — a load under a per-word
+// condition gets its own branch and vmcnt(0) wait, i.e. one memory round trip per word: ~11
+// sequential round trips per thread at G = 8); words already valid, past the end or in this
+// rank's own slot (never read back) reload a harmless address in that own slot.  Returns 1 if
+// `bound` s_memrealtime ticks pass first.
+// A peer exchange that gave up waiting (a missing rank): the merged record is this rank's own
+// record with status LLAMPC_STATUS_POLL_TIMEOUT (the missing slots hold no record to merge).
+__device__ __forceinline__ void peer_timeout_record(const uint32_t* rec32, int rank, llampc_plan_out* m) {
+  const uint32_t* mine = rec32 + (size_t)rank * kRecWords;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(m);
+  constexpr int kStatus = (int)(offsetof(llampc_plan_out, status) / 4);
+  for (int w = threadIdx.x; w < kRecWords; w += kBlock)
+    dst[w] = w == kStatus ? (uint32_t)LLAMPC_STATUS_POLL_TIMEOUT : mine[w];
+}
+
+template <int kPer>
+__device__ __forceinline__ int poll_mailbox(const uint64_t* own, int G, int rank, uint32_t seq,
+                                            uint64_t bound, uint32_t* rec32) {
+  static_assert(kPer <= 64, "one need bit per word");
+  const int tid = threadIdx.x;
+  const int total = G * kRecWords, skip0 = rank * kRecWords, skip1 = skip0 + kRecWords;
+  const int idle = skip0 + tid % kRecWords;      // this thread's harmless address
+  uint64_t need = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int e = tid + j * kBlock;
+    if (e < total && (e < skip0 || e >= skip1)) need |= 1ull << j;
+  }
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (need) {
+    uint64_t v[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int e = ((need >> j) & 1) ? tid + j * kBlock : idle;
+      v[j] = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (((need >> j) & 1) && tag_ok(v[j], seq)) {
+        rec32[tid + j * kBlock] = (uint32_t)v[j];
+        need &= ~(1ull << j);
+      }
+    }
+    if (!need) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > bound) return 1;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return 0;
+}
+
 // Fused peer exchange, run by the block that completed this rank's record (after final_poll /
 // final_select): the record's words are read back, pushed as tagged words into slot [seq & 1][rank] of every mailbox, and the
 // px_G slots of this rank's mailbox are polled into LDS and merged (peer_exchange_kernel's
@@ -1574,20 +1626,8 @@ __device__ __forceinline__ void peer_finish(const FinalLaunch& f, unsigned char*
     }
   }
   const uint64_t* own = f.px_box[f.px_rank] + slot0;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  const uint64_t bound = (uint64_t)f.px_bound << 16;
-  const int skip0 = f.px_rank * kRecWords, skip1 = skip0 + kRecWords;
-  int late = 0;
-  for (int e = tid; e < G * kRecWords; e += kBlock) {
-    if (e >= skip0 && e < skip1) continue;       // this rank's slot is not read back
-    uint64_t v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    while (!tag_ok(v, f.px_seq)) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > bound) { late = 1; break; }
-      __builtin_amdgcn_s_sleep(1);
-      v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    rec32[e] = (uint32_t)v;
-  }
+  constexpr int kPerF = (kPeerFuseMax * kRecWords + kBlock - 1) / kBlock;
+  int late = poll_mailbox<kPerF>(own, G, f.px_rank, f.px_seq, (uint64_t)f.px_bound << 16, rec32);
   EntS* lists = reinterpret_cast<EntS*>(base + (size_t)G * sizeof(llampc_plan_out));
   int* wave_late = reinterpret_cast<int*>(lists + 2 * (size_t)G * LLAMPC_KMAX);
   const int wl = __any(late);
@@ -1595,7 +1635,11 @@ __device__ __forceinline__ void peer_finish(const FinalLaunch& f, unsigned char*
   __syncthreads();
   late = 0;
   for (int w = 0; w < kWaves; ++w) late |= wave_late[w];
-  merge_staged(reinterpret_cast<const llampc_plan_out*>(base), G, f.nan_first, f.px_merged, lists, late);
+  if (late) {                                   // block-uniform
+    peer_timeout_record(rec32, f.px_rank, f.px_merged);
+    return;
+  }
+  merge_staged(reinterpret_cast<const llampc_plan_out*>(base), G, f.nan_first, f.px_merged, lists, 0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1706,19 +1750,8 @@ __global__ __launch_bounds__(kBlock) void peer_exchange_kernel(PeerLaunch a) {
       if (g != a.rank) __hip_atomic_store(a.box[g] + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const uint64_t* own = a.box[a.rank] + slot0;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  const int skip0 = a.rank * kW, skip1 = skip0 + kW;
-  int late = 0;
-  for (int e = tid; e < G * kW; e += kBlock) {
-    if (e >= skip0 && e < skip1) continue;       // this rank's slot is not read back
-    uint64_t v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    while (!tag_ok(v, a.seq)) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > a.bound) { late = 1; break; }
-      __builtin_amdgcn_s_sleep(1);
-      v = __hip_atomic_load(own + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    rec32[e] = (uint32_t)v;
-  }
+  constexpr int kPerK = (kPeerMax * kRecWords + kBlock - 1) / kBlock;
+  int late = poll_mailbox<kPerK>(own, G, a.rank, a.seq, a.bound, rec32);
   // one flag per wave after the lists (no static LDS: the launch asks for all 160 KB)
   EntS* lists = reinterpret_cast<EntS*>(smem + (size_t)G * sizeof(llampc_plan_out));
   int* wave_late = reinterpret_cast<int*>(lists + 2 * (size_t)G * LLAMPC_KMAX);
@@ -1727,7 +1760,11 @@ __global__ __launch_bounds__(kBlock) void peer_exchange_kernel(PeerLaunch a) {
   __syncthreads();
   late = 0;
   for (int w = 0; w < kBlock / 64; ++w) late |= wave_late[w];
-  merge_staged(reinterpret_cast<const llampc_plan_out*>(smem), G, a.nan_first, a.merged, lists, late);
+  if (late) {                                   // block-uniform
+    peer_timeout_record(rec32, a.rank, a.merged);
+    return;
+  }
+  merge_staged(reinterpret_cast<const llampc_plan_out*>(smem), G, a.nan_first, a.merged, lists, 0);
 }
 
 // ------------------------------------------------------------------------------------
