@@ -86,7 +86,7 @@ def make_ticks(args, T, seed=0):
     p = ORCA()
     plant = Dynamic(**p, device=torch_device_index())
     x = d["states"][:, 0].copy()
-    track = ETHZ() if args.track == "ETHZ" else ETHZMobil()
+    track = ETHZ('optimal', True) if args.track == "ETHZ" else ETHZMobil('optimal', True)
     gen = CandidateGenerator(args.C, args.H, seed=2)
     H, Ts = args.H, 0.02
     scenario = getattr(args, "scenario", None) or ("sudden" if args.track == "ETHZMobil" else "gradual")
@@ -133,14 +133,74 @@ def torch_device_index():
     return _DEV[0]
 
 
+def cpu_model_name() -> str:
+    """The host CPU's model name (what `lscpu` prints as "Model name"), from /proc/cpuinfo."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores() -> int:
+    """CPUs this process may run on (the box's CPU share, not the whole machine's count)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+_CPU_SHARD = {}
+
+
+def _cpu_shard_init(N, lo, hi, W, K, seed, ticks):
+    """Worker of the sharded NumPy baseline: its contiguous shard [lo, hi) of the seeded bank
+    and its own look-back window (the reference state per rank of SURVEY.md §8(e))."""
+    for p in (REPO, os.path.join(REPO, "lla-mpc_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from llampc.mpc import generate_bank
+    from oracle import llampc_oracle as O
+    p = O.orca_params()
+    _CPU_SHARD.update(
+        O=O, bank=generate_bank(N, seed=seed)[:, lo:hi], lo=lo, ticks=ticks,
+        win=O.LookbackWindow(hi - lo, W, K),
+        shared={k: p[k] for k in ("lf", "lr", "mass", "Iz", "Cm1", "Cm2", "Cr0", "Cr2")})
+
+
+def _cpu_shard_tick(i, C, H):
+    """One tick of the oracle plan_cpu on this worker's shard; returns the shard record the
+    merge needs: the window's top-K (values, global indices) and the look-ahead best."""
+    S = _CPU_SHARD
+    O, pk = S["O"], S["ticks"][i % len(S["ticks"])]
+    xref = pk[16:16 + 2 * (H + 1)].reshape(2, H + 1)
+    U = pk[16 + 2 * (H + 1):].reshape(C, H, 2)
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    _, best_k, cost = O.plan_cpu(S["shared"], S["bank"], S["win"], pk[0:6], pk[6:8], pk[8:14], U, xref,
+                                 pk[14:16], 0.02, Q, R, P)
+    flat = cost.ravel()
+    j = int(np.argmin(np.where(np.isnan(flat), np.inf, flat)))
+    if best_k is None:
+        return None, None, float(flat[j]), S["lo"] * C + j
+    return S["win"].avg[best_k], best_k + S["lo"], float(flat[j]), S["lo"] * C + j
+
+
 def cpu_baseline(args, seconds):
-    """The oracle (NumPy restatement of the reference path, one core) on the same
-    workload shape: look-back + window/argmin/argsort + H-step RK4 rollout + cost."""
+    """The oracle (NumPy restatement of the reference path) on the same workload shape:
+    look-back + window/argmin/argsort + H-step RK4 rollout + cost.  Two legs: one process
+    (the reference runs single-threaded) and the bank split over P worker
+    processes (SURVEY.md §8(d) "n-process sharded NumPy variant": contiguous shards, each with
+    its own window, merged per tick like the GPU shards)."""
     from llampc.mpc import generate_bank
     from oracle import llampc_oracle as O
     ticks = make_ticks(args, 4)
     N, H, C = args.n_per_gpu, args.H, args.C
-    bank = generate_bank(N, seed=0)
+    seed = 0 if args.track == "ETHZ" else 1
+    bank = generate_bank(N, seed=seed)
     p = O.orca_params()
     shared = {k: p[k] for k in ("lf", "lr", "mass", "Iz", "Cm1", "Cm2", "Cr0", "Cr2")}
     win = O.LookbackWindow(N, args.W, args.K)
@@ -152,25 +212,118 @@ def cpu_baseline(args, seconds):
         U = pk[16 + 2 * (H + 1):].reshape(C, H, 2)
         O.plan_cpu(shared, bank, win, pk[0:6], pk[6:8], pk[8:14], U, xref, pk[14:16], 0.02, Q, R, P)
 
-    one(0)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        one(reps + 1)
-        reps += 1
-        el = time.perf_counter() - t0
-        if (el >= seconds and reps >= 2) or reps >= 1000:
-            break
+    def timed(fn, budget):
+        fn(0)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn(reps + 1)
+            reps += 1
+            el = time.perf_counter() - t0
+            if (el >= budget and reps >= 2) or reps >= 1000:
+                return reps, el
+
+    reps, el = timed(one, seconds)
     per = el / reps
-    return {"value": (N * C * H + N) / per, "unit": "model-rollout-steps/s", "cores": 1, "kind": "port",
+    model = cpu_model_name()
+    out = {"value": (N * C * H + N) / per, "unit": "model-rollout-steps/s", "cores": 1, "kind": "port",
+           "ms_per_step": per * 1e3, "cpu_model": model, "host_cores_available": host_cores(),
+           "sample": f"{reps} plan() ticks of the oracle NumPy restatement (oracle/llampc_oracle.py "
+                     f"plan_cpu = reference evaluate_models_vectorized + rt.py window logic + H x "
+                     f"_integrate_batch + nmpc.py cost) at N={N}, H={H}, C={C} on 1 core of "
+                     f"{host_cores()} available ({model}), {el:.1f} s"}
+    nproc = min(16, host_cores())
+    if nproc > 1:
+        out["sharded"] = cpu_baseline_sharded(args, ticks, nproc, seconds, seed)
+    return out
+
+
+def cpu_baseline_sharded(args, ticks, nproc, seconds, seed):
+    """The sharded NumPy leg: nproc worker processes (spawned: fresh interpreters, no GPU
+    state), each ticking plan_cpu on its contiguous shard; per tick the parent gathers the
+    shard records and merges them (top-K by value, ties to the lower index; look-ahead best)."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    N, H, C, W, K = args.n_per_gpu, args.H, args.C, args.W, args.K
+    pools = []
+    try:
+        for r in range(nproc):
+            lo, hi = (r * N) // nproc, ((r + 1) * N) // nproc
+            pools.append(ProcessPoolExecutor(1, mp_context=mp.get_context("spawn"), initializer=_cpu_shard_init,
+                                             initargs=(N, lo, hi, W, K, seed, ticks)))
+
+        def one(i):
+            parts = [f.result() for f in [p.submit(_cpu_shard_tick, i, C, H) for p in pools]]
+            if parts[0][0] is not None:
+                vals = np.concatenate([q[0] for q in parts])
+                idx = np.concatenate([q[1] for q in parts])
+                order = np.lexsort((idx, vals))[:K]
+                _ = idx[order]
+            return min((q[2], q[3]) for q in parts)
+
+        one(0)                                  # start the workers (imports) outside the clock
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            one(reps + 1)
+            reps += 1
+            el = time.perf_counter() - t0
+            if (el >= seconds and reps >= 2) or reps >= 1000:
+                break
+    finally:
+        for p in pools:
+            p.shutdown(wait=True, cancel_futures=True)
+    per = el / reps
+    return {"value": (N * C * H + N) / per, "unit": "model-rollout-steps/s", "cores": nproc, "kind": "port",
             "ms_per_step": per * 1e3,
-            "sample": f"{reps} plan() ticks of the oracle NumPy restatement (oracle/llampc_oracle.py "
-                      f"plan_cpu = reference evaluate_models_vectorized + rt.py window logic + H x "
-                      f"_integrate_batch + nmpc.py cost) at N={N}, H={H}, C={C} on 1 host core "
-                      f"({os.cpu_count()} visible), {el:.1f} s"}
+            "sample": f"{reps} plan() ticks, bank split into {nproc} contiguous shards, one NumPy process "
+                      f"each (own window), records merged per tick; N={N}, H={H}, C={C}, {el:.1f} s"}
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) started WITHOUT a launcher (no RANK in the environment):
+    start N rank processes of this same command line, one per GPU, with the environment
+    torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE,
+    MASTER_ADDR=127.0.0.1, a free MASTER_PORT), and return their exit status.  This parent
+    never touches the GPU — no torch import, no HIP call, no exec — it starts, watches and, if
+    one rank fails, stops its own children by PID so the rest do not wait in a rendezvous."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc, live = 0, list(procs)
+    try:
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c          # killed by signal -c
+                    print(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for q in procs:                                   # only reached with live ranks on error
+            if q.poll() is None:
+                q.kill()
+                q.wait()
+    return rc
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -252,6 +405,10 @@ def main():
 
     merged = sb.fetch(stream)          # result of the last tick (all ranks identical)
 
+    # SURVEY §8(d)'s per-plan() wall time: the same tick with its inputs coming from host
+    # memory and its record going back (every rank; the exchange included when world > 1)
+    call = plan_call_latency(args, sb, stream, ticks, world)
+
     extra = {}
     if not args.no_extra:              # every rank: the C=64 extra ticks run the collective
         extra = extras(args, sb, stream, world, rank)
@@ -283,7 +440,13 @@ def main():
                                    f"C={C}, {args.scenario or ('sudden' if args.track == 'ETHZMobil' else 'gradual')} friction",
                        "N_models_total": N_total,
                        "N_models_per_gpu": N_local, "H": H, "C": C, "W": W, "K": K, "Ts": 0.02,
-                       "track": args.track, "parallelism": f"bank-shard x{world}" + (f" + 1 exchange/tick ({sb.transport})" if sb.exchange else "")},
+                       "track": args.track, "parallelism": f"bank-shard x{world}" + (f" + 1 exchange/tick ({sb.transport})" if sb.exchange else ""),
+                       "transport": sb.transport, "transport_fallback": sb.fallback_reason},
+            "value_basis": "resident inputs: ms_per_step = wall time per tick of llampc_plan_device (ONE launch"
+                           + (" + the exchange" if sb.exchange else "") + ") on tick inputs already in HBM, "
+                           "K ticks back to back; plan_call_us is the same tick with H2D of its inputs and "
+                           "D2H of its record, timed alone",
+            "plan_call_us": call,
             "roofline": roof,
             "valu": {"bound": "fp64-valu", "achieved_gflops": valu_gf, "peak_tflops": FP64_VALU_PEAK_TFLOPS,
                      "frac": valu_gf / (FP64_VALU_PEAK_TFLOPS * 1e3) if valu_gf else None,
@@ -308,6 +471,42 @@ def main():
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+
+
+def plan_call_latency(args, sb, stream, ticks, world, n=1000, warm=50):
+    """Per-plan() wall time as SURVEY.md §8(d) defines it: HIP events on the tick's stream
+    around [H2D of the tick's input pack from pinned host memory -> the tick (one launch; with
+    world > 1 the exchange too) -> D2H of the (merged) record into pinned host memory], one
+    tick at a time (each waited for), p50/p99 over n ticks after `warm`; max over ranks."""
+    import torch
+    from llampc import _native as nat
+    dev = torch.device("cuda", sb.device)
+    T = len(ticks)
+    h_in = [torch.from_numpy(np.ascontiguousarray(t)).pin_memory() for t in ticks]
+    d_in = torch.empty(ticks.shape[1], dtype=torch.float64, device=dev)
+    h_out = torch.empty(nat.PLAN_OUT_BYTES, dtype=torch.uint8).pin_memory()
+    torch.cuda.synchronize(dev)
+    pin = sb.make_plan_in(d_in, args.C, args.H, K=args.K)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    lat = []
+    for i in range(n + warm):
+        with torch.cuda.stream(stream):
+            e0.record(stream)
+            d_in.copy_(h_in[i % T], non_blocking=True)
+            sb.launch(pin, stream)
+            h_out.copy_(sb.d_merged, non_blocking=True)
+            e1.record(stream)
+        e1.synchronize()
+        if i >= warm:
+            lat.append(e0.elapsed_time(e1) * 1e3)
+    lat = np.array(lat)
+    p50, p99 = float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
+    if world > 1:
+        p50, p99 = max_over_ranks(p50), max_over_ranks(p99)
+    return {"p50": p50, "p99": p99, "ticks": int(lat.size),
+            "rollout_steps_per_s_at_p50": (args.n_per_gpu * world * (args.C * args.H + 1)) / (p50 * 1e-6),
+            "note": "hipEvent-timed on the tick stream: H2D input pack + plan launch"
+                    + (" + exchange" if world > 1 else "") + " + D2H record, one tick at a time"}
 
 
 def extras(args, sb, stream, world, rank=0):

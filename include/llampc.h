@@ -159,6 +159,9 @@ int llampc_bank_destroy(llampc_bank* bank);
 int llampc_bank_info(const llampc_bank* bank, int64_t* n, int64_t* global_offset,
                      int32_t* W, int32_t* window_count, int32_t* device);
 int llampc_bank_reset(llampc_bank* bank);                 /* empty the window       */
+/* plan-kernel launches enqueued on this bank so far (every tick entry point is ONE
+ * launch; the controller test counts them — replaces nothing in the reference) */
+int llampc_bank_launches(const llampc_bank* bank, int64_t* launches);
 /* ring: [n][W] oldest -> newest (the rt.py error_windows layout, zeros if unfilled) */
 int llampc_bank_window(llampc_bank* bank, double* ring, int32_t* window_count);
 /* stream the bank launches on (hipStream_t as void*); NULL = its own stream */

@@ -183,6 +183,7 @@ struct llampc_bank {
   uint64_t* d_tag = nullptr;
   uint64_t hseq = 0;
   uint64_t async_seq = 0;          // the outstanding llampc_plan_async tick's tag (0: copy path)
+  int64_t launches = 0;            // plan-kernel launches enqueued on this bank (llampc_bank_launches)
 };
 
 namespace {
@@ -303,6 +304,12 @@ uint64_t poll_bound_ticks(int64_t n, int32_t C, int32_t H) {
   return ticks >= 1.8e19 ? ~0ull : (uint64_t)ticks;
 }
 
+// Next tick number of a tag sequence: never 0 (the zeroed buffers' tag), and the parity
+// alternates across the 32-bit wrap (0xFFFFFFFF -> 2), so consecutive ticks of a peer
+// mailbox always use different slots (seq & 1).  Callers commit it only after the launch
+// that uses it was enqueued: a failed launch must not leave this rank a tick ahead.
+uint32_t next_seq(uint32_t s) { return s == 0xFFFFFFFFu ? 2u : s + 1u; }
+
 // The tick on device pointers: ONE launch (look-back + look-ahead + completion).
 // Advances the window bookkeeping when a look-back runs.
 int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out, double* d_err,
@@ -402,10 +409,10 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   // the ticket + last-block path, for A/B runs)
   const bool no_poll = getenv("LLAMPC_NO_POLL") != nullptr;
   const int32_t poll = (lb && la && !no_poll) ? 1 : 0;
-  if (poll && ++b->seq == 0) b->seq = 1;
+  const uint32_t seq = poll ? next_seq(b->seq) : b->seq;
   f.la_tag = b->d_la_tag;
   f.blk_tag = b->d_blk_tag;
-  f.seq = b->seq;
+  f.seq = seq;
   if (poll) {                           // the bound in 2^16-tick units, at least one
     const uint64_t units = (poll_bound_ticks(b->n, in.C, in.H) + 0xFFFF) >> 16;
     f.poll = (int32_t)std::min<uint64_t>(std::max<uint64_t>(units, 1), INT32_MAX);
@@ -414,25 +421,28 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   }
   f.host_tag = host_tag;
   f.host_seq = host_seq;
+  const uint32_t px_seq = px ? next_seq(px->seq) : 0;
   if (px) {                             // fused peer exchange (llampc_plan_exchange)
-    if (++px->seq == 0) px->seq = 1;
     f.px_box = px->d_box;
     f.px_merged = px_merged;
     f.px_G = px->world;
     f.px_rank = px->rank;
-    f.px_seq = px->seq;
+    f.px_seq = px_seq;
     f.px_bound = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((px->bound + 0xFFFF) >> 16, 1), UINT32_MAX);
   }
   if (la) {
     lal.la_tag = b->d_la_tag;
     lal.blk_tag = b->d_blk_tag;
-    lal.seq = b->seq;
+    lal.seq = seq;
     lal.poll = poll;
   }
   {
     TimedLaunch tl(b, 0, s);
     HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s, pk));
   }
+  b->seq = seq;
+  if (px) px->seq = px_seq;
+  b->launches++;
   if (lb) {
     b->slot = (slot + 1) % b->W;
     b->count = count;
@@ -632,6 +642,12 @@ int llampc_bank_info(const llampc_bank* b, int64_t* n, int64_t* goff, int32_t* W
   if (W) *W = b->W;
   if (window_count) *window_count = b->count;
   if (device) *device = b->device;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_launches(const llampc_bank* b, int64_t* launches) {
+  if (!b || !launches) return fail(LLAMPC_E_ARG, "bank/launches is NULL");
+  *launches = b->launches;
   return LLAMPC_OK;
 }
 
@@ -1038,7 +1054,7 @@ int llampc_exchange_peer(llampc_mailbox* mb, const void* d_local, void* d_merged
   DeviceGuard g(mb->device);
   if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", mb->device);
   std::lock_guard<std::mutex> lm(mb->mu);
-  if (++mb->seq == 0) mb->seq = 1;       // 0 is the zeroed mailbox's tag
+  const uint32_t seq = next_seq(mb->seq);
   PeerLaunch a{};
   a.local = (const llampc_plan_out*)d_local;
   for (int r = 0; r < mb->world; ++r) a.box[r] = mb->box[r];
@@ -1047,8 +1063,9 @@ int llampc_exchange_peer(llampc_mailbox* mb, const void* d_local, void* d_merged
   a.G = mb->world;
   a.rank = mb->rank;
   a.nan_first = nan_policy == LLAMPC_NAN_FIRST;
-  a.seq = mb->seq;
+  a.seq = seq;
   HIP_TRY(launch_peer_exchange(a, (hipStream_t)stream));
+  mb->seq = seq;
   return LLAMPC_OK;
 }
 

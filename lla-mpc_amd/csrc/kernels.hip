@@ -1194,22 +1194,28 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
     kv = val[e];
   }
   STAMP(2);
+  // Every record field is stored write-through (sc1): on the ticket path another block —
+  // possibly on another XCD — completes the record, and peer_finish reads all of it back
+  // with sc1 loads (MI355X_MICROARCH.md "Valid forms": sc1 stores AND sc1 loads).
   llampc_plan_out* o = f.out;
   if (lane < LLAMPC_KMAX) {
     const int k = lane;
     if (k < K && kl != kNoLocal) {
       st_wt(&o->topk[k], f.goff + (int64_t)kl);      // read by final_select
-      o->topk_val[k] = kv;
-      o->topk_Df[k] = f.params[2 * f.n + kl];
-      o->topk_Dr[k] = f.params[5 * f.n + kl];
+      st_wt(&o->topk_val[k], kv);
+      st_wt(&o->topk_Df[k], f.params[2 * f.n + kl]);
+      st_wt(&o->topk_Dr[k], f.params[5 * f.n + kl]);
     } else {
+      const double nan = __builtin_nan("");
       st_wt(&o->topk[k], (int64_t)-1);
-      o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = __builtin_nan("");
+      st_wt(&o->topk_val[k], nan);
+      st_wt(&o->topk_Df[k], nan);
+      st_wt(&o->topk_Dr[k], nan);
     }
   }
   if (lane == 0) {
     st_wt(&o->lb_best, li == kNoLocal ? (int64_t)-1 : f.goff + (int64_t)li);
-    o->lb_best_val = li == kNoLocal ? __builtin_nan("") : v;
+    st_wt(&o->lb_best_val, li == kNoLocal ? __builtin_nan("") : v);
   }
 }
 
@@ -1220,38 +1226,37 @@ __device__ __forceinline__ void final_write(const FinalLaunch& f, bool lb, int64
                                             int status = 0) {
   const int tid = threadIdx.x;
   llampc_plan_out* o = f.out;
+  const double nan = __builtin_nan("");
+  // sc1 stores like lb_final's: the fused peer exchange reads the whole record back sc1
   if (tid < LLAMPC_KMAX) {
     const int k = tid;
     if (!lb) {
-      o->topk[k] = -1;
-      o->topk_val[k] = o->topk_Df[k] = o->topk_Dr[k] = __builtin_nan("");
+      st_wt(&o->topk[k], (int64_t)-1);
+      st_wt(&o->topk_val[k], nan);
+      st_wt(&o->topk_Df[k], nan);
+      st_wt(&o->topk_Dr[k], nan);
     }
-    o->topk_cand[k] = kcand;
-    o->topk_cost[k] = kcost;
+    st_wt(&o->topk_cand[k], kcand);
+    st_wt(&o->topk_cost[k], kcost);
   }
   if (tid == 0) {
     if (!lb) {
-      o->lb_best = -1;
-      o->lb_best_val = __builtin_nan("");
+      st_wt(&o->lb_best, (int64_t)-1);
+      st_wt(&o->lb_best_val, nan);
     }
-    o->window_count = f.window_count;
-    o->window_full = f.full;
-    o->K = f.K;
-    o->n_nonfinite = nf;
-    o->status = status;
-    o->sel_model = sel;
-    o->sel_owned = owned;
-    o->sel_cand = scand;
-    o->sel_cost = scost;
-    if (f.do_la && lai != kNoIndex) {
-      o->la_best_model = lai / f.C;
-      o->la_best_cand = (int32_t)(lai % f.C);
-      o->la_best_cost = lav;
-    } else {
-      o->la_best_model = -1;
-      o->la_best_cand = -1;
-      o->la_best_cost = __builtin_nan("");
-    }
+    st_wt(&o->window_count, f.window_count);
+    st_wt(&o->window_full, f.full);
+    st_wt(&o->K, f.K);
+    st_wt(&o->n_nonfinite, nf);
+    st_wt(&o->status, status);
+    st_wt(&o->sel_model, sel);
+    st_wt(&o->sel_owned, (int32_t)owned);
+    st_wt(&o->sel_cand, scand);
+    st_wt(&o->sel_cost, scost);
+    const bool la_ok = f.do_la && lai != kNoIndex;
+    st_wt(&o->la_best_model, la_ok ? lai / f.C : (int64_t)-1);
+    st_wt(&o->la_best_cand, la_ok ? (int32_t)(lai % f.C) : (int32_t)-1);
+    st_wt(&o->la_best_cost, la_ok ? lav : nan);
     __hip_atomic_store(&f.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&f.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1603,10 +1608,13 @@ __device__ __forceinline__ void peer_finish(const FinalLaunch& f, unsigned char*
   const int G = f.px_G;
   constexpr int kW2 = kRecWords / 2;            // the record as 64-bit loads
   static_assert(kRecWords % 2 == 0, "record of whole 64-bit words");
-  // The record is read back with plain loads after the block barrier: this block wrote it
-  // (poll path: lb_final and final_poll run here), or the rest of it was released to this
-  // block by the completion tickets (ticket path).  No agent-scope fence: on MI355X that is
-  // an L2 writeback of the XCD (measured ~3 us per tick here).
+  // The record is read back with sc1 loads after the block barrier.  This block wrote part
+  // of it (final_write); on the ticket path lb_final wrote the rest in ANOTHER block, which
+  // can sit on another XCD: every lb_final field is stored sc1 and every load here is sc1,
+  // so the ticket hand-off is the "sc1 stores and loads both sides" form and no stale L2
+  // line of last tick's record can be merged.  No agent-scope fence: on MI355X that is an
+  // L2 writeback of the XCD (measured ~3 us per tick here).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const size_t slot0 = (size_t)(f.px_seq & 1) * G * kRecWords;
   const size_t mine = slot0 + (size_t)f.px_rank * kRecWords;
@@ -1615,7 +1623,7 @@ __device__ __forceinline__ void peer_finish(const FinalLaunch& f, unsigned char*
   uint32_t* rec32 = reinterpret_cast<uint32_t*>(base);
   uint64_t* rec_mine = reinterpret_cast<uint64_t*>(base + (size_t)f.px_rank * sizeof(llampc_plan_out));
   for (int w = tid; w < kW2; w += kBlock) {
-    const uint64_t v = src[w];
+    const uint64_t v = ld_wt(&src[w]);
     rec_mine[w] = v;                            // this rank's record: straight to LDS
     const uint64_t lo = tag_word(f.px_seq, (uint32_t)v), hi = tag_word(f.px_seq, (uint32_t)(v >> 32));
     for (int g = 0; g < G; ++g) {

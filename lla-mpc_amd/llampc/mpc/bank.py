@@ -133,6 +133,13 @@ class ModelBank:
         nat.check(nat.load().llampc_bank_info(self.handle, None, None, None, nat.C.byref(c), None))
         return c.value
 
+    @property
+    def launches(self) -> int:
+        """Plan-kernel launches enqueued on this bank so far (one per tick entry point)."""
+        c = nat.C.c_int64()
+        nat.check(nat.load().llampc_bank_launches(self.handle, nat.C.byref(c)))
+        return c.value
+
     def reset(self):
         nat.check(nat.load().llampc_bank_reset(self.handle))
 

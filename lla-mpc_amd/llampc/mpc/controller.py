@@ -164,18 +164,18 @@ class LLAMPC:
         self.last_topk = None
 
     def tick(self, x_t) -> PlanResult:
+        """One control tick.  After the warm-up (t > W) it is ONE fused launch on the bank:
+        look-back on the newest transition (rt.py:347-349), window + argmin + top-K
+        (rt.py:352-366), and the look-ahead of every (model, candidate), the selected
+        model's best candidate being the chosen control (rt.py:300-305).  While the window
+        fills (t <= W) the look-ahead plans with the nominal model (rt.py:300-301), so the
+        tick is the bank's look-back plus a one-model look-ahead (two launches).
+        Raises NativeError if the selected model is not on this bank (a shard of a larger
+        bank: use ShardedBank, whose merged record carries the owner's choice)."""
         x_t = np.asarray(x_t, dtype=np.float64)
         t = self.t
-        # 1. look-back on the newest transition (the reference scores transition
-        #    idt -> idt+1 for idt >= 1, so tick t >= 2 here; rt.py:347)
-        lb = None
-        if t >= 2:
-            lb = self.bank.lookback(self.x_prev, self.u_prev, x_t, Ts=self.Ts, K=self.K,
-                                    nan_policy=self.nan_policy)
-            if lb["full"]:
-                self.current_model = int(lb["best"])
-                self.last_topk = lb["topk"]
-        # 2. reference (rt.py:278-282); it uses the mu-hat of the previous tick because
+        warm = t <= self.W
+        # 1. reference (rt.py:278-282); it uses the mu-hat of the previous tick because
         #    the reference updates mu-hat after its solve (rt.py:326-344)
         if t > self.W + 1:
             xref, self.projidx, _ = ConstantSpeed(x_t[:2], x_t[3], self.track, self.H, self.Ts,
@@ -186,35 +186,44 @@ class LLAMPC:
                                                   self.projidx)
         if self.projidx > self.track.lap_projidx:              # lap wrap (rt.py:287-296)
             self.projidx = 0
-        # 3. mu-hat update from this look-back's top-K (rt.py:326-344)
-        if t <= self.W:
-            self.mu.warmup()
-        else:
-            p = self.bank.params
-            loc = self.last_topk - self.bank.global_offset
-            loc = loc[self.last_topk >= 0]           # -1 pads a bank of fewer than K models
-            self.mu.update(p[5][loc], p[2][loc])
-        # 4. look-ahead of every (model, candidate) and the chosen control: the nominal
-        #    model while the window fills (rt.py:300-301), the selected bank model after
-        #    (rt.py:303)
         uprev = np.zeros(2) if self.u_prev is None else self.u_prev
         U = self.gen(self.u_seq, uprev)
-        warm = t <= self.W
-        planner = self.nominal_bank if warm else self.bank
-        o, _, _, _ = planner.plan_raw(np.zeros(6), np.zeros(2), x_t, U, xref, uprev, Ts=self.Ts,
-                                      K=self.K, integrator=self.integrator, do_lookback=False,
-                                      do_lookahead=True, current_model=0 if warm else self.current_model,
-                                      cost=self.cost)
-        res = result_from_out(o, U, mu_hat=self.mu.mu_pred)
-        res.nominal = warm
         if warm:
+            # 2w. look-back on the bank (the reference scores transition idt -> idt+1 for
+            #     idt >= 1, so tick t >= 2 here; rt.py:347), look-ahead with the nominal model
+            lb = None
+            if t >= 2:
+                lb = self.bank.lookback(self.x_prev, self.u_prev, x_t, Ts=self.Ts, K=self.K,
+                                        nan_policy=self.nan_policy)
+            o, _, _, _ = self.nominal_bank.plan_raw(np.zeros(6), np.zeros(2), x_t, U, xref, uprev,
+                                                    Ts=self.Ts, K=self.K, integrator=self.integrator,
+                                                    do_lookback=False, do_lookahead=True, current_model=0,
+                                                    cost=self.cost)
+            res = result_from_out(o, U)
             res.best_model = self.current_model
-        if lb is not None and lb["full"]:
-            kk = lb["topk"] >= 0                     # argsort()[:K] has min(n, K) entries
-            res.window_full, res.topk, res.topk_err = True, lb["topk"][kk], lb["topk_val"][kk]
-        res.window_count = self.bank.window_count
-        if res.u_seq is None:                       # selected model lives on another shard
-            res.u_seq = np.ascontiguousarray(U[0].T)
+            res.window_count = lb["window_count"] if lb is not None else self.bank.window_count
+            self.mu.warmup()                                   # rt.py:326-330
+        else:
+            # 2. ONE launch: look-back + selection + look-ahead of every (model, candidate);
+            #    the record carries the selected model's best candidate (rt.py:303-305)
+            o, _, _, _ = self.bank.plan_raw(self.x_prev, self.u_prev, x_t, U, xref, uprev, Ts=self.Ts,
+                                            K=self.K, integrator=self.integrator, do_lookback=True,
+                                            do_lookahead=True, current_model=self.current_model,
+                                            nan_policy=self.nan_policy, cost=self.cost)
+            res = result_from_out(o, U)
+            if res.u_seq is None:
+                raise nat.NativeError(
+                    f"tick {t}: the selected model {res.best_model} is not on this bank "
+                    f"(models [{self.bank.global_offset}, {self.bank.global_offset + self.bank.n})); "
+                    "a shard's controller needs the merged record (ShardedBank)")
+            self.current_model = res.best_model
+            if res.window_full:
+                self.last_topk = res.topk
+                # 3. mu-hat from this look-back's top-K Df/Dr (rt.py:331-344); the record
+                #    carries them, -1 padding (a bank of fewer than K models) already cut
+                self.mu.update(res.topk_Dr, res.topk_Df)
+        res.nominal = warm
+        res.mu_hat = self.mu.mu_pred
         self.u_seq = res.u_seq.T
         self.x_prev = x_t
         self.u_prev = res.u_seq[:, 0].copy()

@@ -151,6 +151,7 @@ class ShardedBank:
         self._comm = None
         self._mailbox = None
         self.transport = None
+        self.fallback_reason = None        # why a preferred transport was not taken (reported)
         if self.exchange:
             mode = exchange_mode()
             if mode in ("auto", "peer"):
@@ -208,6 +209,7 @@ class ShardedBank:
             if required:
                 raise nat.NativeError(msg)
             print(msg + "; falling back", file=sys.stderr)
+            self.fallback_reason = f"peer: {err or 'failed on another rank'}"
             return
         self._mailbox = mb
 
@@ -225,6 +227,7 @@ class ShardedBank:
         except Exception as e:                     # transport only: results are the same
             print(f"llampc: native exchange unavailable ({e}); using the c10d all-gather",
                   file=sys.stderr)
+            self.fallback_reason = ((self.fallback_reason + "; ") if self.fallback_reason else "") + f"rccl: {e}"
             return
         if comm:
             self._xgroup, self._comm, self._allgather = xg, comm, fn

@@ -83,6 +83,13 @@ def main():
         tracks[f"{name}_init"] = np.array([t.x_init, t.y_init, t.psi_init, t.vx_init])
         tracks[f"{name}_s"] = np.asarray(t.spline.s, dtype=np.float64)
         tracks[f"{name}_track_width"] = np.array(t.track_width)
+        # the boundary / centre lines (ethz.py:20-42), read the reference's way
+        for line in ("inner", "center", "outer"):
+            tracks[f"{name}_{line}"] = np.asarray(getattr(t, line), dtype=np.float64)
+    # the short optimal ETHZ raceline (ethz.py:62-65 with longer=False; no Mobil counterpart)
+    raw = np.load(os.path.join(REF, "llampc/tracks/src", "ethz_raceline_.npz"))
+    for k in ("x", "y", "speeds", "mus"):
+        tracks[f"ETHZ_short_{k}"] = np.asarray(raw[k], dtype=np.float64)
     dpath = os.path.join(REPO, "lla-mpc_amd", "llampc", "tracks", "data")
     os.makedirs(dpath, exist_ok=True)
     np.savez_compressed(os.path.join(dpath, "tracks.npz"), **tracks)
@@ -225,6 +232,53 @@ def main():
         out[f"{name}_cases"] = np.array(cases)
         out[f"{name}_xref"] = np.array(xrefs)
     save("planner.npz", **out)
+
+    # ---------------- track loaders (ethz.py:15-138, track.py:12-160) ----------------
+    tr = {}
+    rng_t = np.random.RandomState(17)
+    for name, cls in (("ETHZ", ETHZ), ("ETHZMobil", ETHZMobil)):
+        t = cls()                                   # the reference's defaults: reference='center'
+        tr[f"{name}_center_s"] = np.asarray(t.spline.s, dtype=np.float64)
+        tr[f"{name}_center_raceline"] = np.asarray(t.raceline, dtype=np.float64)
+        tr[f"{name}_center_init"] = np.array([t.x_init, t.y_init, t.psi_init, t.vx_init])
+        tr[f"{name}_track_length"] = np.array(t.track_length)
+        tr[f"{name}_theta_track"] = np.asarray(t.theta_track, dtype=np.float64)
+        thetas = np.concatenate([[0.0, 1e-3], rng_t.uniform(0, t.track_length, 30), [t.theta_track[-1] - 1e-6]])
+        tr[f"{name}_thetas"] = thetas
+        tr[f"{name}_param_to_xy"] = np.array([t.param_to_xy(th) for th in thetas])
+        idx = rng_t.randint(0, t.center.shape[1], 30)
+        pts = t.center[:, idx].T + rng_t.uniform(-0.1, 0.1, (30, 2))
+        mid_close = 0.5 * (t.center[:, -1] + t.center[:, 0])          # on the closing segment
+        pts = np.vstack([pts, mid_close + [0.001, -0.001]])
+        tr[f"{name}_xy_points"] = pts
+        tr[f"{name}_xy_to_param"] = np.array([t.xy_to_param(px, py) for px, py in pts])
+        proj = [t.project(px, py, t.center_line) for px, py in pts]
+        tr[f"{name}_project_xy"] = np.array([p[0] for p in proj])
+        tr[f"{name}_project_idx"] = np.array([p[1] for p in proj])
+        try:                                        # no speed profiles on the centre line
+            ConstantSpeed(x0=t.raceline[:, 5], v0=1.0, track=t, N=5, Ts=TS, projidx=0)
+            tr[f"{name}_center_constantspeed_error"] = np.array("")
+        except Exception as e:                      # noqa: BLE001
+            tr[f"{name}_center_constantspeed_error"] = np.array(type(e).__name__)
+    ts = ETHZ(reference='optimal', longer=False)
+    tr["ETHZ_short_s"] = np.asarray(ts.spline.s, dtype=np.float64)
+    tr["ETHZ_short_mus"] = np.asarray(ts.mus, dtype=np.float64)
+    cases, xrefs = [], []
+    for j, (pi, mu, scale, H_) in enumerate([(0, 1.0, 1.0, 20), (120, 0.55, 0.9, 40), (300, 0.8, 0.9, 20),
+                                             (480, 0.95, 0.9, 40)]):
+        px = ts.raceline[:, pi + 3] + np.array([0.01, -0.02])
+        xr, pidx, vr = ConstantSpeed(x0=px, v0=1.0 + 0.2 * j, track=ts, N=H_, Ts=TS, projidx=pi, scale=scale,
+                                     curr_mu=mu)
+        cases.append([px[0], px[1], 1.0 + 0.2 * j, pi, mu, scale, H_, pidx, vr])
+        xrefs.append(np.pad(xr, ((0, 0), (0, 41 - xr.shape[1])), constant_values=np.nan))
+    tr["ETHZ_short_cases"] = np.array(cases)
+    tr["ETHZ_short_xref"] = np.array(xrefs)
+    try:
+        ETHZMobil(reference='optimal', longer=False)
+        tr["ETHZMobil_short_error"] = np.array("")
+    except Exception as e:                          # noqa: BLE001
+        tr["ETHZMobil_short_error"] = np.array(type(e).__name__)
+    save("tracks_center.npz", **tr)
 
     # ---------------- closed-loop look-back + mu-hat emulation (rt.py:269-366) ----------------
     # Plant: reference RK6 with a gradual friction drop; controls: recorded DYN inputs

@@ -499,12 +499,16 @@ def test_llampc_controller_closed_loop_vs_oracle(nat, monkeypatch, N):
     win = O.LookbackWindow(N, W, K)
     x = d["states"][:, 0].copy()
     cur = 0
-    with ModelBank(bank_p, W=W, device=0) as b, LLAMPC(b, ETHZ(), H=H, C=C, K=K) as ctl:
+    with ModelBank(bank_p, W=W, device=0) as b, LLAMPC(b, ETHZ('optimal', True), H=H, C=C, K=K) as ctl:
         gen = ctl.gen
         ctl.gen = lambda prev, up: (lambda U: (Us.append(U), U)[1])(gen(prev, up))
         x_prev = u_prev = None
         for t in range(W + 6):
+            l0 = b.launches + ctl.nominal_bank.launches
             res = ctl.tick(x)
+            # after the warm-up one fused launch per tick (rt.py:300-366 in one plan kernel);
+            # while the window fills, the bank's look-back plus the nominal look-ahead
+            assert b.launches + ctl.nominal_bank.launches - l0 == (1 if (t > W or t < 2) else 2), t
             if t >= 2:                                   # oracle look-back on (x_{t-1}, u_{t-1}) -> x_t
                 pred = O.evaluate_models_vectorized(shared(), tuple(bank_p), x_prev, u_prev, TS)
                 win.push(O.lookback_errors(pred, x))
@@ -541,7 +545,7 @@ def test_baseline_sizes_properties(nat, N, H, track):
     from llampc.tracks import ETHZ, ETHZMobil
     d = golden("dyn_slice.npz")
     s, u = d["states"], d["inputs"]
-    tr = ETHZ() if track == "ETHZ" else ETHZMobil()
+    tr = ETHZ('optimal', True) if track == "ETHZ" else ETHZMobil('optimal', True)
     p = generate_bank(N, seed=0 if track == "ETHZ" else 1)
     W, K = 10, 10
     with ModelBank(p, W=W, device=0) as b:
@@ -733,6 +737,86 @@ def test_plan_async_two_banks(nat):
             b.close()
 
 
+def _mobil_states(T, u):
+    """A physical ETHZMobil trajectory (no recorded one exists): the oracle's RK6 plant from
+    the track's start pose at 1 m/s, driven by the recorded controls, friction dropping by
+    x21/22 for 9 ticks after tick 2 (the sudden scenario of config 3, rt.py:132-141)."""
+    from llampc.tracks import ETHZMobil
+    tr = ETHZMobil('optimal', True)
+    p = O.orca_params()
+    v = O.Vehicle.from_params(p)
+    xs = [np.array([tr.x_init, tr.y_init, tr.psi_init, 1.0, 0.0, 0.0])]
+    for k in range(T):
+        if 2 <= k < 11:
+            v.Df -= v.Df / 22.
+            v.Dr -= v.Dr / 22.
+        xn, _ = O.sim_continuous(v, xs[-1], u[:, k].reshape(2, 1), [0, TS])
+        xs.append(xn[:, -1])
+    return np.array(xs).T
+
+
+def test_config5_concurrent_tracks_vs_oracle(nat):
+    """BASELINE config 5's workload on one GPU: an ETHZ bank (seed 0) and an ETHZMobil bank
+    (seed 1) of 10^4 models each, H = 40, ticked CONCURRENTLY every control step through
+    llampc_plan_async / llampc_plan_wait (two streams in flight), over W + 2 ticks, against
+    the oracle (rt.py:347-366 look-back + H x _integrate_batch + nmpc.py cost per track):
+    selection, top-K and the look-ahead argmin exact; every cost in the record (selected
+    model's, top-K models', global best) within 1e-7; top-K Df/Dr bitwise."""
+    from llampc import _native
+    from llampc.mpc import ConstantSpeed, ModelBank, generate_bank
+    from llampc.tracks import ETHZ, ETHZMobil
+    d = golden("dyn_slice.npz")
+    u = d["inputs"]
+    N, H, W, K = 10000, 40, 10, 10
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    T = W + 2
+    tracks = {"ETHZ": (ETHZ('optimal', True), d["states"], 0), "ETHZMobil": (ETHZMobil('optimal', True),
+                                                                              _mobil_states(T + 1, u), 1)}
+    banks, wins, params, proj = {}, {}, {}, {}
+    try:
+        for name, (tr, s, seed) in tracks.items():
+            params[name] = generate_bank(N, seed=seed)
+            banks[name] = ModelBank(params[name], W=W, device=0)
+            wins[name] = O.LookbackWindow(N, W, K)
+            proj[name] = 0
+        for t in range(1, T + 1):
+            args = {}
+            for name, (tr, s, _) in tracks.items():
+                xref, proj[name], _ = ConstantSpeed(s[:2, t], s[3, t], tr, H, TS, proj[name], scale=0.9)
+                U = u[:, t:t + H].T[None].copy()
+                args[name] = (s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1])
+            for name, b in banks.items():                 # both in flight before either wait
+                b.plan_async(*args[name], K=K, current_model=3)
+            outs = {name: _native.plan_out_to_dict(b.plan_wait()) for name, b in banks.items()}
+            for name, (tr, s, _) in tracks.items():
+                p, win, o = params[name], wins[name], outs[name]
+                x_prev, u_prev, x_now, U, xref, uprev = args[name]
+                win.push(O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), x_prev, u_prev, TS), x_now))
+                cref = O.mpc_cost(O.rollout_rk4(shared(), tuple(p), x_now, U, TS), U, xref, uprev, Q, R, P)
+                cinf = np.where(np.isnan(cref), np.inf, cref)
+                assert o["status"] == 0
+                assert o["window_full"] == (win.count >= W)
+                sel = win.current if win.count >= W else 3
+                assert o["sel_model"] == sel, (name, t)
+                if np.isfinite(cref[sel]):
+                    assert o["sel_cand"] == 0
+                np.testing.assert_allclose(o["sel_cost"], cref[sel], rtol=RTOL_ROLL)
+                j = int(np.argmin(cinf))
+                assert (o["la_best_model"], o["la_best_cand"]) == (j, 0), (name, t)
+                np.testing.assert_allclose(o["la_best_cost"], cref[j], rtol=RTOL_ROLL)
+                if win.count >= W:
+                    assert o["lb_best"] == win.current
+                    np.testing.assert_array_equal(o["topk"][:K], win.best_k)
+                    np.testing.assert_array_equal(o["topk_Df"][:K], p[2][win.best_k])
+                    np.testing.assert_array_equal(o["topk_Dr"][:K], p[5][win.best_k])
+                    np.testing.assert_allclose(o["topk_val"][:K], win.avg[win.best_k], rtol=RTOL_STEP)
+                    np.testing.assert_allclose(o["topk_cost"][:K], cref[win.best_k], rtol=RTOL_ROLL)
+                assert o["n_nonfinite"] == int(np.count_nonzero(~np.isfinite(cref)))
+    finally:
+        for b in banks.values():
+            b.close()
+
+
 def test_polled_completion_equals_ticket_completion(nat):
     """The polled in-launch completion (look-ahead blocks publish tagged records, the
     look-back winner polls them) gives records identical to the ticket + last-block path
@@ -875,8 +959,8 @@ def test_setupnlp_solve_sampling(nat):
     H, Ts = 20, TS
     Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
     model = Dynamic(**p)
-    nlp = setupNLP(H, Ts, Q, P, R, p, model, ETHZ())
-    track = ETHZ()
+    nlp = setupNLP(H, Ts, Q, P, R, p, model, ETHZ('optimal', True))
+    track = ETHZ('optimal', True)
     x0, uprev, projidx = s[:, 10].copy(), u[:, 9].copy(), 0
     bank6 = tuple(np.array([p[k]]) for k in O.BANK_ORDER)
     for tick in range(3):
@@ -908,7 +992,7 @@ def test_lookahead_raceline_per_model_xref(nat, track_name, start):
     from llampc.mpc import ModelBank, generate_bank, plan
     from llampc.mpc.planner import raceline_start
     from llampc.tracks import ETHZ, ETHZMobil
-    tr = ETHZ() if track_name == "ETHZ" else ETHZMobil()
+    tr = ETHZ('optimal', True) if track_name == "ETHZ" else ETHZMobil('optimal', True)
     td = np.load(os.path.join(os.path.dirname(__file__), "..", "lla-mpc_amd", "llampc", "tracks", "data", "tracks.npz"))
     ref = O.RacelineRef(td[f"{track_name}_x"], td[f"{track_name}_y"], td[f"{track_name}_speeds"], td[f"{track_name}_mus"])
     N, C, H, scale = 192, 2, 20, 0.9

@@ -152,7 +152,7 @@ def test_generate_bank_matches_reference_loop_and_shards():
 def test_product_planner_matches_reference_constant_speed(name):
     from llampc.mpc.planner import ConstantSpeed
     from llampc.tracks import ETHZ, ETHZMobil
-    tr = ETHZ() if name == "ETHZ" else ETHZMobil()
+    tr = ETHZ('optimal', True) if name == "ETHZ" else ETHZMobil('optimal', True)
     g = golden("planner.npz")
     for case, xr in zip(g[f"{name}_cases"], g[f"{name}_xref"]):
         px, py, v0, pi, mu, scale, H, pidx, vr = case
@@ -161,6 +161,72 @@ def test_product_planner_matches_reference_constant_speed(name):
         np.testing.assert_allclose(out, xr[:, :H + 1], rtol=1e-10, atol=1e-12)
         assert oidx == pidx
         np.testing.assert_allclose(ovr, vr, rtol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["ETHZ", "ETHZMobil"])
+def test_track_center_loader_matches_reference(name):
+    """ETHZ/ETHZMobil(reference='center') — the reference's default — pinned to the
+    reference's own objects (tracks_center.npz, gen_golden.py): the centre-line raceline and
+    its spline knots, track length, theta_track, param_to_xy, xy_to_param and project on the
+    closed centre line (closing segment = index -1), the init pose; ConstantSpeed on the
+    centre line fails as the reference's does (no speed profiles: TypeError)."""
+    from llampc.mpc.planner import ConstantSpeed
+    from llampc.tracks import ETHZ, ETHZMobil
+    g = golden("tracks_center.npz")
+    t = ETHZ() if name == "ETHZ" else ETHZMobil()
+    assert t.reference == 'center' and t.mus is None
+    np.testing.assert_array_equal(t.raceline, g[f"{name}_center_raceline"])
+    np.testing.assert_allclose(t.spline.s, g[f"{name}_center_s"], rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose([t.x_init, t.y_init, t.psi_init, t.vx_init], g[f"{name}_center_init"], rtol=0)
+    np.testing.assert_allclose(t.track_length, g[f"{name}_track_length"], rtol=1e-13)
+    np.testing.assert_allclose(t.theta_track, g[f"{name}_theta_track"], rtol=1e-13, atol=1e-13)
+    got = np.array([t.param_to_xy(th) for th in g[f"{name}_thetas"]])
+    np.testing.assert_allclose(got, g[f"{name}_param_to_xy"], rtol=1e-12, atol=1e-13)
+    for (px, py), th, pxy, pidx in zip(g[f"{name}_xy_points"], g[f"{name}_xy_to_param"],
+                                       g[f"{name}_project_xy"], g[f"{name}_project_idx"]):
+        xy, idx = t.project(px, py, t.center_line)
+        assert idx == pidx
+        np.testing.assert_allclose(xy, pxy, rtol=1e-12, atol=1e-13)
+        np.testing.assert_allclose(t.xy_to_param(px, py), th, rtol=1e-12, atol=1e-12)
+    assert str(g[f"{name}_center_constantspeed_error"]) == "TypeError"
+    with pytest.raises(TypeError):
+        ConstantSpeed(t.raceline[:, 5], 1.0, t, 5, 0.02, 0)
+
+
+def test_track_txt_format_and_short_raceline():
+    """The packaged lines equal what ETHZTrack.load_txt reads from a file in the reference's
+    txt format (comma-separated x row / y row); ETHZ(reference='optimal', longer=False)
+    loads the short raceline (6 friction profiles) and ConstantSpeed on it matches the
+    reference; ETHZMobil has no short raceline (FileNotFoundError, as the reference)."""
+    import tempfile
+    from llampc.mpc.planner import ConstantSpeed
+    from llampc.tracks import ETHZ, ETHZMobil, ETHZTrack
+    g = golden("tracks_center.npz")
+    t = ETHZ()
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
+        f.write("# x row, y row\n")
+        for row in t.center:
+            f.write(",".join(repr(float(v)) for v in row) + "\n")
+    try:
+        np.testing.assert_array_equal(ETHZTrack.load_txt(f.name), t.center)
+    finally:
+        os.unlink(f.name)
+    assert t.inner.shape == t.outer.shape == t.center.shape and t.center.shape[0] == 2
+    ts = ETHZ(reference='optimal', longer=False)
+    np.testing.assert_allclose(ts.spline.s, g["ETHZ_short_s"], rtol=1e-13, atol=1e-13)
+    np.testing.assert_array_equal(ts.mus, g["ETHZ_short_mus"])
+    for case, xr in zip(g["ETHZ_short_cases"], g["ETHZ_short_xref"]):
+        px, py, v0, pi, mu, scale, H, pidx, vr = case
+        H = int(H)
+        out, oidx, ovr = ConstantSpeed(np.array([px, py]), v0, ts, H, 0.02, int(pi), scale=scale, curr_mu=mu)
+        np.testing.assert_allclose(out, xr[:, :H + 1], rtol=1e-10, atol=1e-12)
+        assert oidx == pidx
+        np.testing.assert_allclose(ovr, vr, rtol=1e-10)
+    assert str(g["ETHZMobil_short_error"]) == "FileNotFoundError"
+    with pytest.raises(FileNotFoundError):
+        ETHZMobil(reference='optimal', longer=False)
+    with pytest.raises(NotImplementedError):
+        ETHZ(reference='inner')
 
 
 def test_spline_coefficients_match_reference_dense_solve():
@@ -274,7 +340,7 @@ def test_raceline_npz_reader_reference_format(tmp_path):
     (ethz.py:59-96 keys x, y, speed, time, speeds, mus) into the same splines and device
     tables as the packaged library; a file without ``speeds`` gets one profile."""
     from llampc.tracks import ETHZ, Raceline
-    ref = ETHZ()
+    ref = ETHZ('optimal', True)
     n = ref.raceline.shape[1]
     f = tmp_path / "ethz_raceline_long_.npz"
     np.savez(f, x=ref.x_raceline, y=ref.y_raceline, speed=ref.v_raceline[0], time=np.arange(n) * 0.02,

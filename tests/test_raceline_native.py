@@ -36,7 +36,7 @@ def test_raceline_walker_host_asan(harness, tmp_path, name, mode):
     import sys
     sys.path.insert(0, os.path.join(REPO, "lla-mpc_amd"))
     from llampc.tracks import ETHZ, ETHZMobil
-    tr = ETHZ() if name == "ETHZ" else ETHZMobil()
+    tr = ETHZ('optimal', True) if name == "ETHZ" else ETHZMobil('optimal', True)
     knots, xy, speed, mus = tr.device_table()
     n, M = len(knots), len(mus)
     np.concatenate([[n, M], knots, xy.ravel(), speed.ravel(), mus]).astype(np.float64).tofile(tmp_path / "t.bin")

@@ -1,5 +1,5 @@
 """The N > 1 flow of the product (ShardedBank: per-shard plan kernel, exchange of the
-records, merge) with world_size 2, 3 and 4 on ONE GPU: the ranks share cuda:0 (RCCL refuses two
+records, merge) with world_size 2, 3, 4 and 8 on ONE GPU: the ranks share cuda:0 (RCCL refuses two
 ranks on one device; test_exchange_gpu.py covers the RCCL transport on a 1-rank group).
 Transports: "peer" (each rank's mailbox mapped into the other processes through HIP IPC; the
 plan launch itself pushes, polls and merges — "peer-split": a second kernel does — with the
@@ -18,7 +18,12 @@ from conftest import REPO, PKG_ROOT, golden
 
 pytestmark = pytest.mark.gpu
 
-N, H, C, W, K, T = 3001, 20, 3, 3, 7, 6
+H, C, W, K, T = 20, 3, 3, 7, 6
+
+
+def n_models(world):
+    """3001 models (ragged shards) up to world 4; BASELINE config 4's 8 x 10^4 at world 8."""
+    return 80000 if world == 8 else 3001
 
 
 def _free_port():
@@ -44,6 +49,9 @@ def _worker(rank, world, port, q, transport):
         if transport == "peer-split":
             os.environ["LLAMPC_PEER_SPLIT"] = "1"
             transport = "peer"
+        elif transport == "peer-ticket":       # ticket completion: lb_final in another block
+            os.environ["LLAMPC_NO_POLL"] = "1"
+            transport = "peer"
         os.environ["LLAMPC_EXCHANGE"] = transport
         for pth in (REPO, PKG_ROOT):
             if pth not in sys.path:
@@ -55,7 +63,7 @@ def _worker(rank, world, port, q, transport):
         from llampc.mpc.sharded import ShardedBank, _bytes_of
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        sb = ShardedBank(generate_bank(N, seed=12), rank, world, 0, W=W)
+        sb = ShardedBank(generate_bank(n_models(world), seed=12), rank, world, 0, W=W)
         assert sb.transport == transport, (sb.transport, transport)
         pins = [sb.make_plan_in(sb.stage(*a)["pack"], C, H, K=K, current_model=5) for a in _ticks()]
         torch.cuda.synchronize()
@@ -76,9 +84,14 @@ def _worker(rank, world, port, q, transport):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("transport", ["peer", "peer-split", "host"])
-@pytest.mark.parametrize("world", [2, 3, 4])
+CASES = ([(w, "peer") for w in (2, 3, 4, 8)] + [(w, "host") for w in (2, 3, 8)] +
+         [(w, "peer-split") for w in (2, 4)] + [(w, "peer-ticket") for w in (2, 3, 8)])
+
+
+@pytest.mark.parametrize("world,transport", CASES)
 def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
+    """peer-ticket: LLAMPC_NO_POLL=1, so the record's look-back half is written by lb_final in
+    another block than the one that pushes it to the peers (the sc1 hand-off of peer_finish)."""
     import torch.multiprocessing as mp
     from llampc import _native as nat
     from llampc.mpc import ModelBank, generate_bank
@@ -94,13 +107,13 @@ def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
         p.start()
     got = {}
     for _ in range(world):
-        rank, recs, err = q.get(timeout=100)
+        rank, recs, err = q.get(timeout=150)
         assert err is None, f"rank {rank}:\n{err}"
         got[rank] = recs
     for p in procs:
         p.join(timeout=30)
     ref = []
-    with ModelBank(generate_bank(N, seed=12), W=W, device=0) as b:
+    with ModelBank(generate_bank(n_models(world), seed=12), W=W, device=0) as b:
         for a in _ticks():
             ref.append(nat.plan_out_to_dict(b.plan_raw(*a, K=K, current_model=5)[0]))
     for rank in range(world):
@@ -113,3 +126,25 @@ def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
                     np.testing.assert_array_equal(A[k], B[k], err_msg=f"rank {rank} tick {t} {k}")
                 else:
                     assert A[k] == B[k] or (A[k] != A[k] and B[k] != B[k]), (rank, t, k, A[k], B[k])
+
+
+def test_bench_spawns_its_own_ranks():
+    """`python bench.py --gpus 2` with no launcher (no RANK in the environment) starts its two
+    rank processes itself (the parent never touches the GPU) and rank 0 prints ONE JSON line
+    for the whole job — rehearsed on one GPU (LLAMPC_SAME_DEVICE=1, gloo for the host-side
+    collectives; the records travel through the peer mailboxes)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
+                                                              "MASTER_ADDR", "MASTER_PORT")}
+    env.update(LLAMPC_DIST_BACKEND="gloo", LLAMPC_SAME_DEVICE="1")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "40",
+                        "--warmup", "5", "--ticks", "4", "--n-per-gpu", "2000", "--no-extra",
+                        "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["N_models_total"] == 4000
+    assert rec["config"]["transport"] == "peer" and rec["config"]["transport_fallback"] is None
+    assert rec["value"] > 0 and rec["plan_call_us"]["p50"] > 0

@@ -5,7 +5,7 @@ from llampc.mpc import ModelBank, generate_bank, plan
 from llampc.mpc.planner import raceline_start
 from llampc.tracks import ETHZ
 mode, N, C, sig = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), float(sys.argv[4])
-tr = ETHZ()
+tr = ETHZ('optimal', True)
 H = 20
 p = generate_bank(N, seed=21, sigma=sig)
 d = np.load("/root/repo/tests/golden/dyn_slice.npz")

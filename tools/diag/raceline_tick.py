@@ -13,7 +13,7 @@ from llampc.tracks import ETHZ
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-tr = ETHZ()
+tr = ETHZ('optimal', True)
 d = np.load(os.path.join(REPO, "tests/golden/dyn_slice.npz"))
 s, u = d["states"], d["inputs"]
 x0 = s[:, 30]

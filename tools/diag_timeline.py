@@ -20,7 +20,7 @@ kw = {}
 if os.environ.get("RACELINE"):                # xref_mode RACELINE (per-model ConstantSpeed)
     from llampc.mpc.planner import raceline_start
     from llampc.tracks import ETHZ
-    tr = ETHZ()
+    tr = ETHZ('optimal', True)
     b.set_raceline(tr)
     kw = dict(raceline_start=(raceline_start(s[:, 1], tr, 0)[0], float(s[3, 1]), 0.9))
 for t in range(1, 30):
