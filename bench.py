@@ -72,6 +72,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C=64 and latency extras")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--no-call-latency", action="store_true", help="skip the per-plan() H2D+tick+D2H latency")
     return ap.parse_args()
 
 
@@ -226,11 +227,11 @@ def cpu_baseline(args, seconds):
     per = el / reps
     model = cpu_model_name()
     out = {"value": (N * C * H + N) / per, "unit": "model-rollout-steps/s", "cores": 1, "kind": "port",
-           "ms_per_step": per * 1e3, "cpu_model": model, "host_cores_available": host_cores(),
+           "ms_per_step": per * 1e3, "cpu_model": model, "host_cores_visible": host_cores(),
            "sample": f"{reps} plan() ticks of the oracle NumPy restatement (oracle/llampc_oracle.py "
                      f"plan_cpu = reference evaluate_models_vectorized + rt.py window logic + H x "
                      f"_integrate_batch + nmpc.py cost) at N={N}, H={H}, C={C} on 1 core of "
-                     f"{host_cores()} available ({model}), {el:.1f} s"}
+                     f"{host_cores()} visible ({model}; the sharded leg uses the box share of 16), {el:.1f} s"}
     nproc = min(16, host_cores())
     if nproc > 1:
         out["sharded"] = cpu_baseline_sharded(args, ticks, nproc, seconds, seed)
@@ -407,7 +408,7 @@ def main():
 
     # SURVEY §8(d)'s per-plan() wall time: the same tick with its inputs coming from host
     # memory and its record going back (every rank; the exchange included when world > 1)
-    call = plan_call_latency(args, sb, stream, ticks, world)
+    call = None if args.no_call_latency else plan_call_latency(args, sb, stream, ticks, world)
 
     extra = {}
     if not args.no_extra:              # every rank: the C=64 extra ticks run the collective

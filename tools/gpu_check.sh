@@ -26,7 +26,7 @@ step "bench 2 ranks, self-spawned, one device"
 LLAMPC_DIST_BACKEND=gloo LLAMPC_SAME_DEVICE=1 timeout -k 10 300 python -u bench.py --gpus 2 --no-cpu-baseline \
   > "$OUT/bench_g2.json" 2> "$OUT/bench_g2.err" || exit $?
 step "rocprof kernel trace of the bench"
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
   python3 "$GRAFT_REPO_ROOT/bench.py" --no-extra --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2>&1 || exit $?
 cd "$GRAFT_REPO_ROOT"
 step "done (pytest rc=$rc)"

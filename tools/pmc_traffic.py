@@ -39,7 +39,7 @@ out = {"kernel": "plan_kernel", "fetch_kb": mean(f_plan), "write_kb": mean(w_pla
        "hbm_bytes_per_launch_uncorrected": fetch + write,
        "dispatches": len(f_plan),
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/pmc.sh); "
-                 "KB units; corrected by the 8-B/lane calibration dispatch", "round": "r02"}
+                 "KB units; corrected by the 8-B/lane calibration dispatch", "round": os.environ.get("PMC_ROUND", "r03")}
 path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_lookahead.json")
 try:
     d = json.load(open(path))
