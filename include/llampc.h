@@ -306,7 +306,10 @@ int llampc_integrate_batch(const double* x0, const double* u, int64_t u_stride_l
 enum llampc_math_fn { LLAMPC_MATH_ATAN2_XPOS = 0, LLAMPC_MATH_ATAN = 1, LLAMPC_MATH_SIN = 2,
                       LLAMPC_MATH_COS = 3, LLAMPC_MATH_ATAN2_FAST = 4, LLAMPC_MATH_ATAN_FAST = 5,
                       LLAMPC_MATH_SIN_WIDE = 6, LLAMPC_MATH_SIN_FAST = 7, LLAMPC_MATH_COS_FAST = 8,
-                      LLAMPC_MATH_DIV6 = 9 };
+                      LLAMPC_MATH_DIV6 = 9,
+                      /* the look-ahead's lean cores (fastmath.hpp kAtanRL / kSinWQL) */
+                      LLAMPC_MATH_ATAN2_LEAN = 10, LLAMPC_MATH_ATAN_LEAN = 11,
+                      LLAMPC_MATH_SIN_WIDE_LEAN = 12 };
 int llampc_math_batch(int32_t fn, const double* a, const double* b, int64_t n, double* out,
                       int32_t device);
 

@@ -297,16 +297,17 @@ struct Dom {
 // F = D sin(C atan(B slip)) with slip = dsel - atan2(yy, den) for the front tire
 // (dsel = delta) and atan2(yy, den) for the rear (dsel = 0); yy = lf om + vy | lr om - vy
 // (dynamic.py:149-152 / :215-220).  The divisors go to the lane's Dom.
+template <bool LEAN = false>
 __device__ __forceinline__ double chain_fast(const Chain& c, double den, double vy, double om,
                                              double dsel, Dom& dm, const fm::FmK& K) {
   const double yy = fma(c.lw, om, c.sg * vy);
   double h2;
-  const double a2 = fm::atan2_fast(yy, den, K, h2);
+  const double a2 = fm::atan2_fast<LEAN>(yy, den, K, h2);
   const double z = c.B * fma(-c.sg, a2, dsel);
-  const double at = fm::atan_fast(z, K);
+  const double at = fm::atan_fast<LEAN>(z, K);
   dm.lo = fm::vmin(dm.lo, h2);
   dm.hi = fm::vmax(dm.hi, h2);
-  return c.D * fm::sin_wide(c.C * at, K);
+  return c.D * fm::sin_wide<LEAN>(c.C * at, K);
 }
 
 // LPM = 4: the quad's lanes run ONE instruction stream — lanes 0/1 the front/rear chain,
@@ -320,7 +321,7 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
 // SCALED: psi arrives as Psi = (2/pi) psi (the fused quad's state, step_fused): k2 = the
 // even integer nearest Psi, r = (Psi - k2) pi/2 — the subtraction is exact (|Psi| < 2^51),
 // so the fold is 4 instructions instead of the 3-part Cody-Waite's 5.
-template <bool SCALED = false>
+template <bool SCALED = false, bool LEAN = false>
 __device__ __forceinline__ double chain_fold(const Chain& c, double den, double vy, double om,
                                              double Bd, double psi, int ra, double pm,
                                              double po, Dom& dm, const fm::FmK& K) {
@@ -349,13 +350,13 @@ __device__ __forceinline__ double chain_fold(const Chain& c, double den, double 
 #endif
     const double yy = fma(c.lw, om, c.sg * vy);
     double h2;
-    const double a2 = fm::atan2_fast(yy, den, K, h2);
+    const double a2 = fm::atan2_fast<LEAN>(yy, den, K, h2);
     const double z = fma(c.nsB, a2, Bd);                  // B (dsel - sg a2)
-    at = fm::atan_fast(z, K);
+    at = fm::atan_fast<LEAN>(z, K);
     dm.lo = fm::vmin(dm.lo, h2);
     dm.hi = fm::vmax(dm.hi, h2);
   }
-  return c.D * fm::sin_wide(fma(c.C, at, arg_psi), K);
+  return c.D * fm::sin_wide<LEAN>(fma(c.C, at, arg_psi), K);
 }
 
 // Per-rollout constants of the fast stage.  ch[0] is this lane's chain (LPM = 2) or the
@@ -410,14 +411,14 @@ struct StageF {
 // Bd = B d fw, the chain's steering term (LPM = 4 only; formed once per step).
 // SPLIT (LPM = 4, position split): sp/cp carry the split's A/B operands instead (X lanes:
 // cos, sin; Y lanes: sin, cos — kQuadPosA/B).
-template <int LPM, bool SPLIT = false, bool SCALED = false>
+template <int LPM, bool SPLIT = false, bool SCALED = false, bool LEAN = false>
 __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, double vy, double om,
                                               double d, double psi, const fm::FmK& K, Dom& dm,
                                               double Bd = 0.0) {
   StageF f;
   dm.ps = fm::vmax_abs(psi, dm.ps);
   if (LPM == 4) {
-    const double r = chain_fold<SCALED>(sk.ch[0], den, vy, om, Bd, psi, sk.ra, sk.pm, sk.po, dm, K);
+    const double r = chain_fold<SCALED, LEAN>(sk.ch[0], den, vy, om, Bd, psi, sk.ra, sk.pm, sk.po, dm, K);
     f.Ffy = quad_bcast<kQuad0, 0>(r);
     f.Fry = quad_bcast<kQuad1, 1>(r);
     if constexpr (SPLIT) {
@@ -430,12 +431,12 @@ __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, doub
     return f;
   }
   if (LPM == 2) {
-    const double r = chain_fast(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
+    const double r = chain_fast<LEAN>(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
     f.Ffy = dpp_bcast<kPair0>(r);
     f.Fry = dpp_bcast<kPair1>(r);
   } else {
-    f.Ffy = chain_fast(sk.ch[0], den, vy, om, d, dm, K);
-    f.Fry = chain_fast(sk.ch[1], den, vy, om, 0.0, dm, K);
+    f.Ffy = chain_fast<LEAN>(sk.ch[0], den, vy, om, d, dm, K);
+    f.Fry = chain_fast<LEAN>(sk.ch[1], den, vy, om, 0.0, dm, K);
   }
   fm::sincos_fast(psi, &f.sp, &f.cp, K);
   return f;
@@ -487,6 +488,18 @@ __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::F
 // (~1 ulp per step, the transcendental cores' class; tests/test_gpu_parity.py bounds the
 // rollouts at 1e-7 relative).  42 fewer instructions per step than step_fast's reference
 // roundings, which the look-back keeps (its errors are ranked, rt.py:359-360).
+// The look-ahead's fused stages use the lean cores (fastmath.hpp kAtanRL / kSinWQL, the
+// division without its residual step; the FmK of those rollouts is loaded with
+// FmK::load<kLeanLA>()): ~1e-14 relative on the tire forces; 467 instructions per step at
+// LPM 4 (494 with the precise 10-term cores, 507 in round 2), A/B 28.8 -> 27.2 us per tick
+// (profiles/r03/ab_lean).  -DLLAMPC_PRECISE_LA
+// builds the precise (<= 4 ulp) cores into the look-ahead too, for A/B runs.
+#ifdef LLAMPC_PRECISE_LA
+constexpr bool kLeanLA = false;
+#else
+constexpr bool kLeanLA = true;
+#endif
+
 struct FusedK {
   double h, hm, hIlf, hIlr, m1, m0, m2, m3;   // hm = h/m; m1 = hm k1, m0 = hm k0,
 };                                            // m2 = hm k2, m3 = -hm k3 (StageK)
@@ -524,7 +537,7 @@ __device__ __forceinline__ void k_fused(const StageK& sk, const FusedK& q, doubl
                                         const double* y, double* k, const fm::FmK& K, Dom& dm) {
   const double vx = y[3], vy = y[4], om = y[5];
   constexpr bool kScaled = (LPM == 4);    // om = W = h omega, y[2] = Psi (make_fused)
-  const StageF f = forces_fast<LPM, SPLIT, kScaled>(sk, vx, vy, om, d, y[2], K, dm, Bd);
+  const StageF f = forces_fast<LPM, SPLIT, kScaled, kLeanLA>(sk, vx, vy, om, d, y[2], K, dm, Bd);
   // h sin(psi), h cos(psi): LPM = 4 lanes 2/3 scale their sine by h already (make_stage)
   const double hsp = (LPM == 4) ? f.sp : q.h * f.sp, hcp = (LPM == 4) ? f.cp : q.h * f.cp;
   const double hmFrx = fma(vx, fma(q.m3, vx, F1), F0);                     // hm Frx

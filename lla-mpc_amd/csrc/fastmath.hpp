@@ -165,23 +165,33 @@ __device__ __host__ __forceinline__ double sin_(double a) {
 // re-does the rare out-of-domain lanes with the general functions above, behind ONE
 // wave-uniform branch per stage that is normally not taken.
 // ------------------------------------------------------------------------------------
-constexpr double kSinWQ[11] = {
-    -0.16666666666666666,   0.008333333333333333,   -0.0001984126984126983,
-    2.755731922398403e-06,  -2.5052108385275923e-08, 1.6059043828214877e-10,
-    -7.647163453155476e-13, 2.8114514557344955e-15, -8.21985910722077e-18,
-    1.950826068108976e-20,  -3.56150612064771e-23};
-// atan(t) = t + t*s*QR(s) for |t| <= tan(pi/8) (11 terms): the fast cores reduce their
+constexpr double kSinWQ[10] = {
+    -0.16666666666666666,  0.008333333333333328,  -0.00019841269841267895,
+    2.7557319223709e-06,  -2.505210836542107e-08,  1.6059043004898195e-10,
+    -7.647142668717314e-13,  2.8111267068839815e-15,  -8.18919565437741e-18,
+    1.790528073907954e-20};
+// atan(t) = t + t*s*QR(s) for |t| <= tan(pi/8) (10 terms: fit error 1.5e-16 relative, <= 1 ulp): the fast cores reduce their
 // ratio r in [0, 1] by atan(r) = pi/4 + atan((r - 1)/(r + 1)) when r > tan(pi/8), so the
 // polynomial is half as long as QA's on [0, 1] for 6 more instructions
 // (tools/fit_fastmath.py; -DLLAMPC_ATAN_FULL keeps the 22-term core for A/B runs).
-constexpr double kAtanR[11] = {
-    -0.3333333333333333,    0.1999999999999552,     -0.14285714284666542,
-    0.11111111015256361,    -0.09090904578123903,   0.07692183190826087,
-    -0.06664511447381948,   0.0585814891280221,     -0.0508544973794026,
-    0.03923165829558719,    -0.01917688711906226};
+constexpr double kAtanR[10] = {
+    -0.3333333333333325,  0.19999999999898407,  -0.1428571426609662,
+    0.11111109636534361,  -0.09090852557176049,  0.0769105515839315,
+    -0.06649613695291669,  0.05736332165907643,  -0.04483334622272886,
+    0.02275052699336167};
 constexpr double kTanPi8 = 0.41421356237309503;
-constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s), |a| <= 3: <= 4 ulp up to
-                                       // |a| = 2, then <= 2^-49 absolute (cancellation)
+// Lean cores of the look-ahead rollouts (kLeanLA): 9-term atan (3.8e-15 relative on |t| <=
+// tan(pi/8)) and 9-term sin_wide (2.3e-15 absolute to |a| = 3, <= 4 ulp to 2), and the
+// division without its residual correction (<= 18 ulp): ~1e-14 relative on the tire forces
+// against the <= 4 ulp of the precise cores, which the look-back keeps (its errors are ranked).
+constexpr double kAtanRL[9] = {-0.3333333333333093, 0.19999999997724888, -0.14285713930378566,
+                               0.11111089649211055, -0.09090255952690657, 0.07681045202742948,
+                               -0.0655090730756309, 0.05168834935919362, -0.02723288406057488};
+constexpr double kSinWQL[9] = {-0.1666666666666666, 0.008333333333332372, -0.00019841269840984845,
+                               2.755731919144023e-06, -2.5052106522437073e-08, 1.605898387304835e-10,
+                               -7.646028139181475e-13, 2.7988830742041364e-15, -7.463851483197331e-18};
+constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s) (10 terms, fit error 6e-18), |a| <= 3:
+                                       // <= 3 ulp up to |a| = 2, then <= 2^-50 absolute (cancellation)
 
 // Constants of the fast cores, held in VGPRs for the whole kernel (FmK::load pins them
 // with an empty asm so the compiler cannot rematerialise them): a VOP3 v_fma_f64 reads a
@@ -191,29 +201,32 @@ struct FmK {
 #ifdef LLAMPC_ATAN_FULL
   double at[22];
 #else
-  double ar[11];
+  double ar[10];
   double tp8, pio4;
 #endif
-  double sw[11], sq[7], cq[7];
+  double sw[10], sq[7], cq[7];
   double pio2, two_pi, cw0, cw1, cw2, sixth, six, rmagic, rmagic2, one;
   double inv_pi, inv_3pi;                 // (2/pi)/2, (2/pi)/6: the scaled yaw's RK4 weights
 
   __device__ __forceinline__ static void pin(double& x) { asm volatile("" : "+v"(x)); }
+  // LEAN: the 9-term coefficient sets in ar[0..8] / sw[0..8] (the lean cores read no more)
+  template <bool LEAN = false>
   __device__ __forceinline__ static FmK load() {
     FmK k;
+    constexpr int nA = LEAN ? 9 : 10;
 #ifdef LLAMPC_ATAN_FULL
 #pragma unroll
     for (int i = 0; i < 22; ++i) { k.at[i] = kAtanQ[i]; pin(k.at[i]); }
 #else
 #pragma unroll
-    for (int i = 0; i < 11; ++i) { k.ar[i] = kAtanR[i]; pin(k.ar[i]); }
+    for (int i = 0; i < nA; ++i) { k.ar[i] = LEAN ? kAtanRL[i] : kAtanR[i]; pin(k.ar[i]); }
     k.tp8 = kTanPi8;
     k.pio4 = kPio4;
     pin(k.tp8);
     pin(k.pio4);
 #endif
 #pragma unroll
-    for (int i = 0; i < 11; ++i) { k.sw[i] = kSinWQ[i]; pin(k.sw[i]); }
+    for (int i = 0; i < nA; ++i) { k.sw[i] = LEAN ? kSinWQL[i] : kSinWQ[i]; pin(k.sw[i]); }
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
       k.sq[i] = kSinQ[i];
@@ -255,6 +268,7 @@ __device__ __forceinline__ double horner(const double* c, double s) {
 // reciprocal's relative error e0, r has e0^2 and the corrected quotient e0^4 + 1/2 ulp:
 // one step is enough for any e0 <= 2^-14 (v_rcp_f64 is far better; the atan2/atan ULP
 // tests, whose every call divides, bound the result).
+template <bool LEAN = false>
 __device__ __forceinline__ double div_fast(double num, double den) {
 #ifdef LLAMPC_ABL_NODIV   // diagnostic ablation builds only (tools/micro/ablate.sh)
   return num * den;
@@ -262,6 +276,7 @@ __device__ __forceinline__ double div_fast(double num, double den) {
   double r = __builtin_amdgcn_rcp(den);
   const double e = fma(-den, r, 1.0);
   r = fma(r, e, r);
+  if constexpr (LEAN) return num * r;         // lean cores: no residual step (<= 18 ulp)
   // the residual correction is needed: without it atan2 reaches 18 ulp for divisors just
   // below powers of two (v_rcp_f64 is least accurate there; tools/diag/ulp_probe.py)
   const double q = num * r;
@@ -321,6 +336,7 @@ __device__ __forceinline__ double vmin_abs2(double a, double b) {  // min(|a|, |
 // word only), so the polynomial covers |t| <= tan(pi/8).  n - d and n + d are rounded once
 // each (relative 2^-53 on t); the offset add rounds once: <= 2 ulp before the callers'
 // fix-ups (tests: test_fast_cores_ulp_on_domain).
+template <bool LEAN = false>
 __device__ __forceinline__ double atan_ratio_k(double n, double d, const FmK& K) {
 #ifdef LLAMPC_ATAN_FULL
   const double t = div_fast(n, d);
@@ -329,9 +345,9 @@ __device__ __forceinline__ double atan_ratio_k(double n, double d, const FmK& K)
 #else
   const bool red = n > K.tp8 * d;
   const double sf = __hiloint2double(red ? 0x3FF00000 : 0, 0);
-  const double t = div_fast(fma(-sf, d, n), fma(sf, n, d));
+  const double t = div_fast<LEAN>(fma(-sf, d, n), fma(sf, n, d));
   const double s = t * t;
-  return fma(sf, K.pio4, fma(t * s, horner<11>(K.ar, s), t));
+  return fma(sf, K.pio4, fma(t * s, horner<LEAN ? 9 : 10>(K.ar, s), t));
 #endif
 }
 
@@ -344,39 +360,44 @@ __device__ __host__ __forceinline__ bool atan2_fast_ok(double y, double x) {
 // hi = max(|y|, |x|), the divisor: hi in [2^-1000, 2^999] lies inside the domain (the
 // rollout checks its running extremes once, dyn.hpp Dom).  x enters as |x| (the callers'
 // x is |vx| or the clamped vx >= vmin, so passing vx itself saves materialising |vx|).
+template <bool LEAN = false>
 __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K, double& hi) {
   const double ay = fabs(y);
   hi = vmax_abs2(y, x);
-  const double r = atan_ratio_k(vmin_abs2(y, x), hi, K);
+  const double r = atan_ratio_k<LEAN>(vmin_abs2(y, x), hi, K);
   const double o = (ay > fabs(x)) ? K.pio2 - r : r;   // no pi/2 tail: <= 2 ulp (measured)
   return copysign(o, y);
 }
+template <bool LEAN = false>
 __device__ __forceinline__ double atan2_fast(double y, double x, const FmK& K) {
   double hi;
-  return atan2_fast(y, x, K, hi);
+  return atan2_fast<LEAN>(y, x, K, hi);
 }
 
 // atan(z) on the domain |z| <= 2^1000: the reciprocal branch as a division by max(|z|, 1)
 // (exact when |z| <= 1).
 __device__ __host__ __forceinline__ bool atan_fast_ok(double z) { return fabs(z) <= 0x1p1000; }
 // hz = max(|z|, 1), the divisor: hz <= 2^1000 is the domain.
+template <bool LEAN = false>
 __device__ __forceinline__ double atan_fast(double z, const FmK& K, double& hz) {
   const double az = fabs(z);
   hz = vmax_abs(z, K.one);
-  const double r = atan_ratio_k(vmin_abs(z, K.one), hz, K);
+  const double r = atan_ratio_k<LEAN>(vmin_abs(z, K.one), hz, K);
   const double o = (az > 1.0) ? K.pio2 - r : r;   // no pi/2 tail: <= 2 ulp (measured)
   return copysign(o, z);
 }
+template <bool LEAN = false>
 __device__ __forceinline__ double atan_fast(double z, const FmK& K) {
   double hz;
-  return atan_fast(z, K, hz);
+  return atan_fast<LEAN>(z, K, hz);
 }
 
 // sin(a) for |a| <= kSinWideMax, one polynomial (the Pacejka argument C*atan(.) is
 // bounded by |C| pi/2, so |C| <= 1.9 keeps every call in range).
+template <bool LEAN = false>
 __device__ __forceinline__ double sin_wide(double a, const FmK& K) {
   const double s = a * a;
-  return fma(a * s, horner<11>(K.sw, s), a);
+  return fma(a * s, horner<LEAN ? 9 : 10>(K.sw, s), a);
 }
 
 // sincos(a) for |a| <= kSinCosMax (NaN/inf -> not ok): Cody-Waite reduction, quadrant

@@ -910,7 +910,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       sk.ch[0].nsB = 0.0;
     }
     const FusedK fq = make_fused(veh, sk, Ts, kScaled);
-    const fm::FmK K = fm::FmK::load();
+    const fm::FmK K = fm::FmK::load<kLeanLA && INTEG == 0>();
     for (int j = 0; j < cpl; ++j) {
       const int c = g + j * G;
       if (c >= C) break;
@@ -1822,6 +1822,9 @@ __global__ __launch_bounds__(kBlock) void math_kernel(int32_t fn, const double* 
     case 7: fm::sincos_fast(a[i], &s, &c, K); r = s; break;
     case 8: fm::sincos_fast(a[i], &s, &c, K); r = c; break;
     case 9: r = fm::div6(a[i], K); break;
+    case 10: r = fm::atan2_fast<true>(a[i], b[i], fm::FmK::load<true>()); break;
+    case 11: r = fm::atan_fast<true>(a[i], fm::FmK::load<true>()); break;
+    case 12: r = fm::sin_wide<true>(a[i], fm::FmK::load<true>()); break;
     default: r = __builtin_nan("");
   }
   out[i] = r;

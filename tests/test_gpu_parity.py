@@ -631,6 +631,29 @@ def test_fast_cores_ulp_on_domain(nat):
     np.testing.assert_array_equal(_math(nat, 9, v), v / 6.0)
 
 
+def test_lean_cores_accuracy_on_domain(nat):
+    """The look-ahead's lean cores (math fn 10-12: 9-term atan and sin_wide, division without
+    its residual step) on the same domains vs NumPy: atan2 / atan within 128 ulp (~3e-14
+    relative), sin_wide within 16 ulp for |a| <= 2 and 2^-47 absolute up to 3 — far inside
+    the 1e-7 rollout tolerance and the north star's 1e-5, the rollouts' own fused-RK4
+    roundings being of the same order."""
+    rng = np.random.RandomState(2)
+    n = 1 << 20
+    y = np.concatenate([rng.uniform(-3, 3, n), rng.standard_cauchy(n), [0.0, -0.0, 1.0, -1.0, 1e-300, 5.0]])
+    x = np.concatenate([rng.uniform(0, 4, n), np.abs(rng.standard_cauchy(n)), [1.0, 1.0, 0.0, 0.0, 0.0, 3.0]])
+    ok = (np.abs(y) + x >= 2.0 ** -1000) & (np.abs(y) + x <= 2.0 ** 1000)
+    u_a2 = _ulp(_math(nat, 10, y[ok], x[ok]), np.arctan2(y[ok], x[ok]))
+    z = np.concatenate([rng.uniform(-2, 2, n), rng.standard_cauchy(n) * 10, [0.0, -0.0, 1.0, -1.0, 1e300, -1e-300]])
+    u_a = _ulp(_math(nat, 11, z), np.arctan(z))
+    a = rng.uniform(-2, 2, n)
+    u_s = _ulp(_math(nat, 12, a), np.sin(a))
+    print(f"lean cores: atan2 {u_a2:.1f} ulp, atan {u_a:.1f} ulp, sin_wide |a|<=2 {u_s:.1f} ulp")
+    assert u_a2 <= 128 and u_a <= 128 and u_s <= 16
+    a = np.concatenate([rng.uniform(-3, 3, n), [3.0, -3.0, 0.0, -0.0, 1e-300]])
+    err = np.abs(_math(nat, 12, a) - np.sin(a))
+    assert np.all(err <= 16 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -47), err.max()
+
+
 def test_lookahead_out_of_domain_fallback(nat):
     """Rollouts whose operands leave the fast cores' domains take the general evaluation
     (dyn.hpp rhs_fast): models with |C| > 1.9, a yaw beyond 2^20 pi/2, a standing start

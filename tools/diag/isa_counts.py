@@ -15,7 +15,7 @@ subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++
                cwd=tmp, check=True, stderr=subprocess.DEVNULL)
 asm = open(f"{tmp}/kernels-hip-amdgcn-amd-amdhsa-gfx950.s").read().split("\n")
 for lpm in (4, 2, 1):
-    s = next(i for i, l in enumerate(asm) if re.match(rf"^_ZN6llampc11plan_kernelILi0ELb1ELi{lpm}ELi0E\S+:", l))
+    s = next(i for i, l in enumerate(asm) if re.match(rf"^_ZN6llampc11plan_kernelILi0ELb1ELi{lpm}ELi0ELb0E\S+:", l))
     e = next(i for i in range(s, len(asm)) if "s_endpgm" in asm[i])
     body = asm[s:e]
     labels = {m.group(1): i for i, l in enumerate(body) if (m := re.match(r"^(\.LBB\d+_\d+):", l))}

@@ -75,10 +75,10 @@ T8 = mp.tan(mp.pi / 8)
 for nR in (9, 10, 11, 12):
     cR, eR = fit(QA, 0, T8 * T8, nR)
     print(f"QR n={nR} chebyfit err {float(eR):.3e}", file=sys.stderr)
-cR, _ = fit(QA, 0, T8 * T8, 11)
+cR, _ = fit(QA, 0, T8 * T8, 10)
 
-cW, eW = fit(QS, 0, 9.0, 11)
-print(f"QW n=11 chebyfit err {float(eW):.3e}", file=sys.stderr)
+cW, eW = fit(QS, 0, 9.0, 10)
+print(f"QW n=10 chebyfit err {float(eW):.3e}", file=sys.stderr)
 
 atan_f = lambda t, c: t + t * (t * t) * horner(c, t * t)
 sin_f = lambda r, c: r + r * (r * r) * horner(c, r * r)
