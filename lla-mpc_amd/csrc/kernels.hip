@@ -820,13 +820,22 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       sx[2 * e + 1] = a.xref[(H + 1) + e];
     }
   }
+  // Shared xref: ONE FmK for the staging below and the rollouts (the staging uses its sincos
+  // constants, the same in the lean and precise sets) instead of materialising the ~50
+  // constants twice on the prologue's critical path; the raceline variant keeps two loads
+  // (holding them across its prologue spilled, round 1).
+  fm::FmK K0;
+  if constexpr (!XM) K0 = fm::FmK::load<kLeanLA && INTEG == 0>();
   if (STAGE) {
     // [k][c] -> (pwm, delta, sin delta, cos delta): the steering's sincos depends only on the
     // shared candidates, so it is formed once per block here (same evaluation as
     // make_input_fast: the fast core on its domain, the general function off it).  RK4
     // stages the fused stages' input terms instead: (F0, F1, h/m sin d, h/m cos d,
     // h lf/Iz cos d, delta) — dyn.hpp fused_in, with the shared constants of make_fused.
-    const fm::FmK K = fm::FmK::load();
+    const fm::FmK K = [&] {
+      if constexpr (XM) return fm::FmK::load();
+      else return K0;
+    }();
     const FusedK fq0 = make_fused(a.veh, make_stage<1>(a.veh, Tire{}, 0), a.Ts, LPM == 4);
     for (int e = (int)threadIdx.x - soff; e < C * H; e += kBlock - soff) {
       if (e < 0) break;
@@ -910,7 +919,10 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       sk.ch[0].nsB = 0.0;
     }
     const FusedK fq = make_fused(veh, sk, Ts, kScaled);
-    const fm::FmK K = fm::FmK::load<kLeanLA && INTEG == 0>();
+    const fm::FmK K = [&] {
+      if constexpr (XM) return fm::FmK::load<kLeanLA && INTEG == 0>();
+      else return K0;
+    }();
     for (int j = 0; j < cpl; ++j) {
       const int c = g + j * G;
       if (c >= C) break;
