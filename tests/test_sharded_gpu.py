@@ -132,14 +132,15 @@ def test_bench_spawns_its_own_ranks():
     """`python bench.py --gpus 2` with no launcher (no RANK in the environment) starts its two
     rank processes itself (the parent never touches the GPU) and rank 0 prints ONE JSON line
     for the whole job — rehearsed on one GPU (LLAMPC_SAME_DEVICE=1, gloo for the host-side
-    collectives; the records travel through the peer mailboxes)."""
+    collectives; the records travel through the peer mailboxes) — extras included: C = 64
+    ticks and BASELINE config 5 (two tracks) sharded over both ranks."""
     import json
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
                                                               "MASTER_ADDR", "MASTER_PORT")}
     env.update(LLAMPC_DIST_BACKEND="gloo", LLAMPC_SAME_DEVICE="1")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "40",
-                        "--warmup", "5", "--ticks", "4", "--n-per-gpu", "2000", "--no-extra",
+                        "--warmup", "5", "--ticks", "4", "--n-per-gpu", "2000",
                         "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -148,3 +149,7 @@ def test_bench_spawns_its_own_ranks():
     assert rec["n_gpus"] == 2 and rec["config"]["N_models_total"] == 4000
     assert rec["config"]["transport"] == "peer" and rec["config"]["transport_fallback"] is None
     assert rec["value"] > 0 and rec["plan_call_us"]["p50"] > 0
+    # the extras run on every rank: C = 64 ticks and BASELINE config 5 sharded over the ranks
+    assert rec["C64"]["ms_per_step"] > 0
+    c5 = rec["config5"]
+    assert c5["N_per_track"] == 4000 and c5["transport"] == ["peer", "peer"] and c5["p99_us"] > 0
