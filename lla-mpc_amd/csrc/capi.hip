@@ -184,6 +184,8 @@ struct llampc_bank {
   uint64_t hseq = 0;
   uint64_t async_seq = 0;          // the outstanding llampc_plan_async tick's tag (0: copy path)
   int64_t launches = 0;            // plan-kernel launches enqueued on this bank (llampc_bank_launches)
+  uint64_t* d_wq = nullptr;        // work-queue unit counter (monotonic; launch_plan's WQ layout)
+  uint64_t wq_base = 0;            // the counter's value at the next launch's start
 };
 
 namespace {
@@ -435,11 +437,15 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
     lal.blk_tag = b->d_blk_tag;
     lal.seq = seq;
     lal.poll = poll;
+    lal.wq = b->d_wq;
+    lal.wq_base = b->wq_base;
   }
+  int64_t wq_adv = 0;
   {
     TimedLaunch tl(b, 0, s);
-    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s, pk));
+    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s, pk, &wq_adv));
   }
+  b->wq_base += (uint64_t)wq_adv;        // the work-queue takes this launch makes (0: static layout)
   b->seq = seq;
   if (px) px->seq = px_seq;
   b->launches++;
@@ -589,7 +595,8 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
       (rc = dev_alloc(&b->d_best_cand, n)) || (rc = dev_alloc(&b->d_best_cost, n)) ||
       (rc = dev_alloc(&b->d_err, n)) || (rc = dev_alloc(&b->d_wmean, n)) ||
       (rc = dev_alloc(&b->d_out, 1)) || (rc = dev_alloc(&b->d_tickets, 2)) ||
-      (rc = dev_alloc(&b->d_la_tag, 3 * (size_t)n)) || (rc = dev_alloc(&b->d_blk_tag, 5 * (size_t)lab)))
+      (rc = dev_alloc(&b->d_la_tag, 3 * (size_t)n)) || (rc = dev_alloc(&b->d_blk_tag, 5 * (size_t)lab)) ||
+      (rc = dev_alloc(&b->d_wq, 1)))
     return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&b->h_out), sizeof(llampc_plan_out), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(out) failed"));
@@ -606,6 +613,7 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
       hipMemset(b->d_tickets, 0, 2 * sizeof(unsigned)) != hipSuccess ||
       hipMemset(b->d_la_tag, 0, 3 * (size_t)n * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(b->d_blk_tag, 0, 5 * (size_t)lab * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(b->d_wq, 0, sizeof(uint64_t)) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "bank upload failed"));
   *out = b;
@@ -620,7 +628,7 @@ int llampc_bank_destroy(llampc_bank* b) {
     void* dptrs[] = {b->d_params, b->d_ring, b->d_am_val, b->d_am_idx, b->d_tk_val, b->d_tk_idx,
                      b->d_pv, b->d_pidx, b->d_pnf, b->d_best_cand, b->d_best_cost, b->d_in,
                      b->d_out, b->d_err, b->d_wmean, b->d_cost, b->d_tickets, b->d_rl,
-                     b->d_xref_pm, b->d_la_tag, b->d_blk_tag};
+                     b->d_xref_pm, b->d_la_tag, b->d_blk_tag, b->d_wq};
     for (void* p : dptrs)
       if (p) (void)hipFree(p);
     if (b->h_in) (void)hipHostFree(b->h_in);
@@ -657,9 +665,11 @@ int llampc_bank_reset(llampc_bank* b) {
   DeviceGuard g(b->device);
   HIP_TRY(hipMemsetAsync(b->d_ring, 0, (size_t)b->W * b->n * sizeof(double), b->stream));
   HIP_TRY(hipMemsetAsync(b->d_tickets, 0, 2 * sizeof(unsigned), b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_wq, 0, sizeof(uint64_t), b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   b->count = 0;
   b->slot = 0;
+  b->wq_base = 0;
   return LLAMPC_OK;
 }
 

@@ -691,7 +691,52 @@ __device__ __forceinline__ void copy_lds(double* dst, int count, Src src) {
 //   h/m cos, h lf/Iz cos, delta; else pwm, delta, sin, cos; then
 //   input-rate cost term, feasibility) when staged.
 // ------------------------------------------------------------------------------------
-template <int INTEG, bool STAGE, int LPM, int XM>
+// The block's partial of the look-ahead argmin over (model, candidate) in flattened order
+// (goff+n)*C + c — (v, key) per lane (kNoIndex: none) and the lanes' non-finite counts:
+// branch-free wave picks, one LDS exchange, thread 0 publishes (tagged words or plain).
+__device__ __forceinline__ void la_publish(const LookaheadLaunch& a, int blk, const Scratch& sc, int par,
+                                           double v, int64_t key, int nf) {
+  wave_pick_nl64(v, key);
+  const int nfw = wave_sum(nf);
+  double* sv = sc.sv + 4 * par;         // the buffer a span > 64 exchange did not use
+  int64_t* si = sc.si + 4 * par;
+  if ((threadIdx.x & 63) == 0) {
+    sv[threadIdx.x >> 6] = v;
+    si[threadIdx.x >> 6] = key;
+    sc.sn[threadIdx.x >> 6] = nfw;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int nfs = sc.sn[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) {
+      const bool t = (int)(si[w] != kNoIndex) & (int)less_bf<0>(sv[w], si[w], v, key);
+      v = t ? sv[w] : v;
+      key = t ? si[w] : key;
+      nfs += sc.sn[w];
+    }
+    if (a.poll) {
+      uint64_t* r = a.blk_tag + 5 * (int64_t)blk;
+      const uint64_t vb = (uint64_t)__double_as_longlong(v), kb = (uint64_t)key;
+      st_wt(&r[0], tag_word(a.seq, (uint32_t)(vb >> 32)));
+      st_wt(&r[1], tag_word(a.seq, (uint32_t)vb));
+      st_wt(&r[2], tag_word(a.seq, (uint32_t)(kb >> 32)));
+      st_wt(&r[3], tag_word(a.seq, (uint32_t)kb));
+      st_wt(&r[4], tag_word(a.seq, (uint32_t)nfs));
+    } else {
+      st_wt(&a.pv[blk], v);
+      st_wt(&a.pidx[blk], key);
+      st_wt(&a.pnf[blk], nfs);
+    }
+  }
+}
+
+// WQ (the throughput regime, launch_plan): a persistent layout — the grid holds one look-ahead
+// block per CU and each wave takes units of 64 / G models (one model at G = 64) from the
+// bank's work counter, so the staging prologue runs once per CU instead of once per 4 models
+// and no CU waits for a new block between units (v29 stamps at C = 64: prologue 3.4 us and
+// reduction 2 us of each 45 us block).
+template <int INTEG, bool STAGE, int LPM, int XM, bool WQ = false>
 __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int blk, int G, int cpl,
                                                 unsigned char* smem, const Scratch& sc) {
   LA_STAMP(blk, 0);
@@ -710,7 +755,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   const int mpb = kBlock / (G * LPM);
   const int soff = (XM && mpb < kBlock) ? mpb : 0;
   Tire t{};
-  if (live) t = load_tire(a.params, a.n, n);
+  if (!WQ && live) t = load_tire(a.params, a.n, n);
   double x0[6];
 #pragma unroll
   for (int m = 0; m < 6; ++m) x0[m] = a.x0[m];
@@ -902,6 +947,90 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
   // scalar
   constexpr bool kSplit = (INTEG == 0 && LPM == 4);
   const bool diagQP = a.cost.Q[1] == 0.0 && a.cost.Q[2] == 0.0 && a.cost.P[1] == 0.0 && a.cost.P[2] == 0.0;
+  if constexpr (WQ) {
+    static_assert(LPM == 1 && XM == 0, "work queue: LPM 1, shared xref");
+    // Unit u = models [u mpw, (u + 1) mpw) of one wave.  Lane 0 takes unit numbers from the
+    // monotonic counter (relaxed agent-scope add; this launch's numbers start at a.wq_base,
+    // and every wave makes exactly one take past the last unit, so the host knows where the
+    // next launch starts); the next take is issued before the current unit's rollouts and
+    // read after them, so its latency is hidden.
+    const int mpw = 64 / G;
+    const int64_t units = (a.n + mpw - 1) / mpw;
+    const int lm = (int)(threadIdx.x & 63) / G;
+    auto issue = [&]() -> uint64_t {
+      uint64_t v = 0;
+      if ((threadIdx.x & 63) == 0)
+        v = __hip_atomic_fetch_add(a.wq, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return v;
+    };
+    auto take = [&](uint64_t v) -> int64_t {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 0);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 0);
+      return (int64_t)((((uint64_t)hi << 32) | lo) - a.wq_base);
+    };
+    double vacc = __builtin_nan("");
+    int64_t kacc = kNoIndex;
+    int nfacc = 0;
+    const fm::FmK K = K0;
+    for (int64_t u = take(issue()); u < units;) {          // wave-uniform
+      const uint64_t nxt = issue();
+      const int64_t nm = u * mpw + lm;
+      const bool lv = nm < a.n;
+      double mv = __builtin_nan("");
+      int64_t mc = kNoIndex;
+      if (lv) {
+        const Tire tm = load_tire(a.params, a.n, nm);
+        const StageK sk = make_stage<1>(veh, tm, 0, INTEG == 0 ? Ts : 1.0);
+        const FusedK fq = make_fused(veh, sk, Ts, false);
+        for (int j = 0; j < cpl; ++j) {
+          const int c = g + j * G;
+          if (c >= C) break;
+          bool bad = false;
+          double J = rollout<INTEG, STAGE, 1, 0, true>(a, c, nm, x0, sx, su, veh, tm, sk, q, Ts, up0, up1, K, fq, bad);
+          if (__builtin_expect(__any(bad), 0)) {
+            bool unused = false;
+            if (bad) J = rollout<INTEG, STAGE, 1, 0, false>(a, c, nm, x0, sx, su, veh, tm, sk, q, Ts, up0, up1, K, fq, unused);
+          }
+          if (a.cost_out) a.cost_out[nm * C + c] = J;
+          nfacc += !isfinite(J);
+          if (less_nan_last(J, c, mv, mc)) {
+            mv = J;
+            mc = c;
+          }
+        }
+      }
+      for (int off = G >> 1; off >= 1; off >>= 1) {        // the model's argmin over its lanes
+        const double ov = __shfl_xor(mv, off, 64);
+        const int64_t oc = __shfl_xor(mc, off, 64);
+        if (less_nan_last(ov, oc, mv, mc)) {
+          mv = ov;
+          mc = oc;
+        }
+      }
+      if (lv && g == 0) {
+        if (a.poll) {
+          st_wt(&a.la_tag[nm], tag_word(a.seq, (uint32_t)(__double_as_longlong(mv) >> 32)));
+          st_wt(&a.la_tag[a.n + nm], tag_word(a.seq, (uint32_t)__double_as_longlong(mv)));
+          st_wt(&a.la_tag[2 * a.n + nm], tag_word(a.seq, (uint32_t)(int32_t)mc));
+        } else {
+          st_wt(&a.best_cand[nm], (int32_t)mc);
+          st_wt(&a.best_cost[nm], mv);
+        }
+        if (mc != kNoIndex) {
+          const int64_t key = (a.goff + nm) * C + mc;
+          if (less_bf<0>(mv, key, vacc, kacc)) {
+            vacc = mv;
+            kacc = key;
+          }
+        }
+      }
+      u = take(nxt);
+    }
+    LA_STAMP(blk, 2);
+    la_publish(a, blk, sc, 0, vacc, kacc, nfacc);
+    LA_STAMP(blk, 3);
+    return;
+  }
   if (live) {
     // LPM = 2: lane 0 of the pair evaluates the front chain, lane 1 the rear (dyn.hpp)
     // fused RK4 quads carry W = h omega and Psi = (2/pi) psi (make_fused): the chains'
@@ -1001,43 +1130,9 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       st_wt(&a.best_cost[n], bv);
     }
   }
-  // per-block argmin over (model, candidate) in flattened order (goff+n)*C + c: branch-free
-  // wave picks, one LDS exchange of the waves' picks and non-finite counts
-  int64_t key = (live && bc != kNoIndex && g == 0 && sub == 0) ? (a.goff + n) * C + bc : kNoIndex;
-  double v = (key == kNoIndex) ? __builtin_nan("") : bv;
-  wave_pick_nl64(v, key);
-  const int nfw = wave_sum(nf);
-  double* sv = sc.sv + 4 * par;         // the buffer the span > 64 exchange did not use
-  int64_t* si = sc.si + 4 * par;
-  if ((threadIdx.x & 63) == 0) {
-    sv[threadIdx.x >> 6] = v;
-    si[threadIdx.x >> 6] = key;
-    sc.sn[threadIdx.x >> 6] = nfw;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int nfs = sc.sn[0];
-#pragma unroll
-    for (int w = 1; w < kWaves; ++w) {
-      const bool t = (int)(si[w] != kNoIndex) & (int)less_bf<0>(sv[w], si[w], v, key);
-      v = t ? sv[w] : v;
-      key = t ? si[w] : key;
-      nfs += sc.sn[w];
-    }
-    if (a.poll) {
-      uint64_t* r = a.blk_tag + 5 * (int64_t)blk;
-      const uint64_t vb = (uint64_t)__double_as_longlong(v), kb = (uint64_t)key;
-      st_wt(&r[0], tag_word(a.seq, (uint32_t)(vb >> 32)));
-      st_wt(&r[1], tag_word(a.seq, (uint32_t)vb));
-      st_wt(&r[2], tag_word(a.seq, (uint32_t)(kb >> 32)));
-      st_wt(&r[3], tag_word(a.seq, (uint32_t)kb));
-      st_wt(&r[4], tag_word(a.seq, (uint32_t)nfs));
-    } else {
-      st_wt(&a.pv[blk], v);
-      st_wt(&a.pidx[blk], key);
-      st_wt(&a.pnf[blk], nfs);
-    }
-  }
+  // per-block argmin over (model, candidate) in flattened order (goff+n)*C + c
+  const int64_t key = (live && bc != kNoIndex && g == 0 && sub == 0) ? (a.goff + n) * C + bc : kNoIndex;
+  la_publish(a, blk, sc, par, (key == kNoIndex) ? __builtin_nan("") : bv, key, nf);
   LA_STAMP(blk, 3);
 }
 
@@ -1669,7 +1764,7 @@ __device__ __forceinline__ void peer_finish(const FinalLaunch& f, unsigned char*
 // (lb_final) while look-ahead blocks still run; the last block overall completes the
 // llampc_plan_out record (final_select).
 // ------------------------------------------------------------------------------------
-template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false>
+template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false, bool WQ = false>
 __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const LookaheadLaunch& la,
                                           const FinalLaunch& fin, int G, int cpl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1691,7 +1786,7 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
       return;
     }
   } else {
-    lookahead_block<INTEG, STAGE, LPM, XM>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
+    lookahead_block<INTEG, STAGE, LPM, XM, WQ>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
     if (fin.poll) return;                // published tagged records; no ticket
   }
   const unsigned expected = (unsigned)fin.nb_la + (fin.nb_lb > 0 ? 1u : 0u);
@@ -1702,10 +1797,10 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
 
 // PX: the sharded tick's fused peer exchange (a separate instantiation, so the plain tick's
 // code is unchanged: inlining it into every variant cost the headline tick 0.5 us)
-template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false>
+template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false, bool WQ = false>
 __global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
                                                       FinalLaunch fin, int G, int cpl) {
-  plan_body<INTEG, STAGE, LPM, XM, PX>(lb, la, fin, G, cpl);
+  plan_body<INTEG, STAGE, LPM, XM, PX, WQ>(lb, la, fin, G, cpl);
 }
 
 // The same tick with its inputs in the kernarg segment (InlinePack): the pointers are set to
@@ -1957,8 +2052,22 @@ static void allow_lds(KERN k) {
 
 template <int INTEG, bool STAGE, int LPM>
 static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
-                          int G, int cpl, size_t lds, hipStream_t s) {
+                          int G, int cpl, size_t lds, hipStream_t s, bool wq = false) {
   lds = std::max(lds, kOneBlockPerCuLds);
+  if constexpr (INTEG == LLAMPC_RK4 && LPM == 1) {
+    if (wq) {                            // work queue: given xref only (launch_plan checks)
+      if (f.px_G) {
+        allow_lds(plan_kernel<INTEG, STAGE, 1, 0, true, true>);
+        hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, true, true>), dim3(f.nb_lb + f.nb_la), dim3(kBlock),
+                           lds, s, lb, la, f, G, cpl);
+      } else {
+        allow_lds(plan_kernel<INTEG, STAGE, 1, 0, false, true>);
+        hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, false, true>), dim3(f.nb_lb + f.nb_la), dim3(kBlock),
+                           lds, s, lb, la, f, G, cpl);
+      }
+      return;
+    }
+  }
   if constexpr (INTEG == LLAMPC_RK4) {
     if (f.px_G) {                        // given xref only (launch_plan checks)
       allow_lds(plan_kernel<INTEG, STAGE, LPM, 0, true>);
@@ -1997,14 +2106,29 @@ bool plan_inline_ok(int32_t C, int32_t H, int32_t integrator, int32_t xref_mode)
 
 template <int INTEG, bool STAGE>
 static void launch_plan_l(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
-                          int G, int cpl, int lpm, size_t lds, hipStream_t s) {
+                          int G, int cpl, int lpm, size_t lds, hipStream_t s, bool wq = false) {
   if (lpm == 4) launch_plan_t<INTEG, STAGE, 4>(lb, la, f, G, cpl, lds, s);
   else if (lpm == 2) launch_plan_t<INTEG, STAGE, 2>(lb, la, f, G, cpl, lds, s);
-  else launch_plan_t<INTEG, STAGE, 1>(lb, la, f, G, cpl, lds, s);
+  else launch_plan_t<INTEG, STAGE, 1>(lb, la, f, G, cpl, lds, s, wq);
+}
+
+// Compute units of the current device (cached): the work-queue layout launches one
+// look-ahead block per CU, minus the one the completing look-back block holds.
+static int device_cus() {
+  static int cus[64] = {};
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
+  if (!cus[d]) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || c < 2) c = 256;
+    cus[d] = c;
+  }
+  return cus[d];
 }
 
 hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
-                       hipStream_t s, const InlinePack* pk) {
+                       hipStream_t s, const InlinePack* pk, int64_t* wq_advance) {
+  if (wq_advance) *wq_advance = 0;
   LookbackLaunch lbv{};
   LookaheadLaunch lav{};
   int G = 1, cpl = 1, lpm = 1, integ = LLAMPC_RK4;
@@ -2054,6 +2178,21 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
   f.do_lb = lb != nullptr;
   f.do_la = la != nullptr;
   if (f.nb_lb + f.nb_la == 0) return hipErrorInvalidValue;
+  // Work queue (the throughput regime): LPM 1 with a model inside one wave (G <= 64), RK4 on
+  // the shared xref, device inputs, more look-ahead blocks than CUs — then one block per CU
+  // (minus the completing look-back block's) takes units of models from the bank's counter.
+  // LLAMPC_NO_WQ=1 keeps the block-per-models layout (A/B runs).
+  bool wq = false;
+  if (la && la->wq && lpm == 1 && G <= 64 && integ == LLAMPC_RK4 && la->xref_mode == LLAMPC_XREF_GIVEN &&
+      !pk && getenv("LLAMPC_NO_WQ") == nullptr) {
+    const int nw = std::max(1, device_cus() - 1);
+    if (f.nb_la > nw) {
+      const int64_t mpw = 64 / G;
+      f.nb_la = nw;
+      wq = true;
+      if (wq_advance) *wq_advance = (la->n + mpw - 1) / mpw + (int64_t)nw * kWaves;
+    }
+  }
   if (f.px_G) {                          // fused peer exchange: RK4, given xref, device inputs
     if (pk || integ != LLAMPC_RK4 || (la && la->xref_mode == LLAMPC_XREF_RACELINE) || f.px_G > kPeerFuseMax)
       return hipErrorInvalidValue;
@@ -2070,8 +2209,8 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
   }
   switch (integ) {
     case LLAMPC_RK4:
-      if (stage) launch_plan_l<0, true>(lbv, lav, f, G, cpl, lpm, lds, s);
-      else launch_plan_l<0, false>(lbv, lav, f, G, cpl, lpm, lds, s);
+      if (stage) launch_plan_l<0, true>(lbv, lav, f, G, cpl, lpm, lds, s, wq);
+      else launch_plan_l<0, false>(lbv, lav, f, G, cpl, lpm, lds, s, wq);
       break;
     case LLAMPC_EULER_NLP:
       if (stage) launch_plan_l<1, true>(lbv, lav, f, G, cpl, lpm, lds, s);

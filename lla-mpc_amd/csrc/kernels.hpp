@@ -55,6 +55,10 @@ struct LookaheadLaunch {
   uint64_t* blk_tag;                     // [blocks][5]: partial value hi, lo, key hi, lo, nf
   uint32_t seq;                          // this launch's tag (never 0)
   int32_t poll;
+  // work queue (launch_plan decides: LPM 1, G <= 64, more look-ahead blocks than CUs): the
+  // bank's monotonic unit counter and this launch's base (capi advances it per launch)
+  uint64_t* wq;
+  uint64_t wq_base;
 };
 
 // What the ticket winners of the plan launch need (see plan_kernel).
@@ -113,8 +117,10 @@ size_t raceline_lds_bytes(int32_t n, int32_t M);
 // the completion stages run by ticket winners; writes f.out.  f.nb_* / f.do_* are set here.
 // pk != null: the inputs are in *pk (see InlinePack); needs a look-ahead with RK4, the
 // given xref and U staged in LDS (plan_inline_ok), else hipErrorInvalidValue.
+// wq_advance (optional out): the work-queue counter increments this launch makes (0 when
+// it runs the static block-per-models layout).
 hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
-                       hipStream_t s, const InlinePack* pk = nullptr);
+                       hipStream_t s, const InlinePack* pk = nullptr, int64_t* wq_advance = nullptr);
 bool plan_inline_ok(int32_t C, int32_t H, int32_t integrator, int32_t xref_mode);
 hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
                         llampc_plan_out* merged, hipStream_t s);
