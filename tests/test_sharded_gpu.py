@@ -18,12 +18,13 @@ from conftest import REPO, PKG_ROOT, golden
 
 pytestmark = pytest.mark.gpu
 
-H, C, W, K, T = 20, 3, 3, 7, 6
+H, W, K, T = 20, 3, 7, 6
 
 
-def n_models(world):
-    """3001 models (ragged shards) up to world 4; BASELINE config 4's 8 x 10^4 at world 8."""
-    return 80000 if world == 8 else 3001
+def n_models(world, C=3):
+    """3001 models (ragged shards) up to world 4; BASELINE config 4's 8 x 10^4 at world 8;
+    6001 at C = 64 (each shard's look-ahead then runs the work-queue layout)."""
+    return 6001 if C == 64 else (80000 if world == 8 else 3001)
 
 
 def _free_port():
@@ -32,7 +33,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _ticks():
+def _ticks(C=3):
     d = golden("dyn_slice.npz")
     s, u = d["states"], d["inputs"]
     rng = np.random.RandomState(8)
@@ -44,7 +45,7 @@ def _ticks():
     return out
 
 
-def _worker(rank, world, port, q, transport):
+def _worker(rank, world, port, q, transport, C=3):
     try:
         if transport == "peer-split":
             os.environ["LLAMPC_PEER_SPLIT"] = "1"
@@ -63,9 +64,9 @@ def _worker(rank, world, port, q, transport):
         from llampc.mpc.sharded import ShardedBank, _bytes_of
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        sb = ShardedBank(generate_bank(n_models(world), seed=12), rank, world, 0, W=W)
+        sb = ShardedBank(generate_bank(n_models(world, C), seed=12), rank, world, 0, W=W)
         assert sb.transport == transport, (sb.transport, transport)
-        pins = [sb.make_plan_in(sb.stage(*a)["pack"], C, H, K=K, current_model=5) for a in _ticks()]
+        pins = [sb.make_plan_in(sb.stage(*a)["pack"], C, H, K=K, current_model=5) for a in _ticks(C)]
         torch.cuda.synchronize()
         outs = []
         for pin in pins:                        # back to back: no synchronisation between ticks
@@ -84,12 +85,13 @@ def _worker(rank, world, port, q, transport):
         q.put((rank, None, traceback.format_exc()))
 
 
-CASES = ([(w, "peer") for w in (2, 3, 4, 8)] + [(w, "host") for w in (2, 3, 8)] +
-         [(w, "peer-split") for w in (2, 4)] + [(w, "peer-ticket") for w in (2, 3, 8)])
+CASES = ([(w, "peer", 3) for w in (2, 3, 4, 8)] + [(w, "host", 3) for w in (2, 3, 8)] +
+         [(w, "peer-split", 3) for w in (2, 4)] + [(w, "peer-ticket", 3) for w in (2, 3, 8)] +
+         [(2, "peer", 64), (3, "peer-ticket", 64)])
 
 
-@pytest.mark.parametrize("world,transport", CASES)
-def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
+@pytest.mark.parametrize("world,transport,C", CASES)
+def test_sharded_tick_equals_unsharded_on_gpu(world, transport, C):
     """peer-ticket: LLAMPC_NO_POLL=1, so the record's look-back half is written by lb_final in
     another block than the one that pushes it to the peers (the sc1 hand-off of peer_finish)."""
     import torch.multiprocessing as mp
@@ -102,7 +104,7 @@ def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, transport)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, transport, C)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -113,8 +115,8 @@ def test_sharded_tick_equals_unsharded_on_gpu(world, transport):
     for p in procs:
         p.join(timeout=30)
     ref = []
-    with ModelBank(generate_bank(n_models(world), seed=12), W=W, device=0) as b:
-        for a in _ticks():
+    with ModelBank(generate_bank(n_models(world, C), seed=12), W=W, device=0) as b:
+        for a in _ticks(C):
             ref.append(nat.plan_out_to_dict(b.plan_raw(*a, K=K, current_model=5)[0]))
     for rank in range(world):
         for t in range(T):
