@@ -279,7 +279,7 @@ def cpu_baseline_sharded(args, ticks, nproc, seconds, seed):
                       f"each (own window), records merged per tick; N={N}, H={H}, C={C}, {el:.1f} s"}
 
 
-def spawn_ranks(n: int) -> int:
+def spawn_ranks(n: int, cmd=None) -> int:
     """`bench.py --gpus N` (N > 1) started WITHOUT a launcher (no RANK in the environment):
     start N rank processes of this same command line, one per GPU, with the environment
     torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE,
@@ -292,7 +292,7 @@ def spawn_ranks(n: int) -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),

@@ -408,3 +408,30 @@ def test_plan_in_builder_pointers_and_fields():
     assert (pin.C, pin.H, pin.K, pin.integrator, pin.do_lookback) == (1, 7, 4, nat.EULER_NLP, 0)
     assert (pin.nan_policy, pin.current_model, pin.Ts, pin.xref_mode) == (nat.NAN_IGNORE, 17, 0.01, nat.XREF_RACELINE)
     assert bytes(pin.cost) == bytes(cost)
+
+
+def test_bench_spawn_ranks_environment_and_failure():
+    """bench.py's self-spawn of `--gpus N` (no launcher): every rank gets torchrun's
+    environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, one shared free port),
+    the parent's status is 0 when all ranks succeed, and when one rank fails the others are
+    stopped and its exit status is returned (CPU only: the ranks are stand-in scripts)."""
+    import importlib.util
+    import sys
+    import tempfile
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    with tempfile.TemporaryDirectory() as tmp:
+        ok = ("import os, sys; open(os.path.join(%r, os.environ['RANK']), 'w').write("
+              "' '.join(os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')))") % tmp
+        assert bench.spawn_ranks(3, [sys.executable, "-c", ok]) == 0
+        got = [open(os.path.join(tmp, str(r))).read().split() for r in range(3)]
+        assert [g[:4] for g in got] == [[str(r), str(r), "3", "127.0.0.1"] for r in range(3)]
+        assert len({g[4] for g in got}) == 1
+        fail = ("import os, sys, time\n"
+                "if os.environ['RANK'] == '1': sys.exit(3)\n"
+                "time.sleep(60)\n")
+        import time
+        t0 = time.time()
+        assert bench.spawn_ranks(3, [sys.executable, "-c", fail]) == 3
+        assert time.time() - t0 < 30            # the sleeping ranks were stopped, not waited for
