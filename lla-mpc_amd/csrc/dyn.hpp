@@ -438,7 +438,21 @@ __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, doub
     f.Ffy = chain_fast<LEAN>(sk.ch[0], den, vy, om, d, dm, K);
     f.Fry = chain_fast<LEAN>(sk.ch[1], den, vy, om, 0.0, dm, K);
   }
-  fm::sincos_fast(psi, &f.sp, &f.cp, K);
+  if constexpr (SCALED && LPM == 1) {
+    // LPM = 1 with the scaled yaw Psi = (2/pi) psi (k_fused): the quad's fold in one lane —
+    // psi = r + k pi, sin psi = sin((-1)^k r), cos psi = sin((-1)^k (pi/2 - |r|)), both by
+    // sin_wide (|arg| <= pi/2).  As many instructions as sincos_fast, and the sincos
+    // polynomials' and Cody-Waite's 17 constants (34 VGPRs) are not live in the loop.
+    const double t2 = psi + K.rmagic2;                   // 2^53 (1.5 + 2k 2^-53): ulp 2
+    const double k2 = t2 - K.rmagic2;
+    const double r = (psi - k2) * K.pio2;
+    const int fs = __double2loint(t2) << 31;             // (-1)^k on both arguments
+    const double c = K.pio2 - fabs(r);
+    f.sp = fm::sin_wide<LEAN>(__hiloint2double(__double2hiint(r) ^ fs, __double2loint(r)), K);
+    f.cp = fm::sin_wide<LEAN>(__hiloint2double(__double2hiint(c) ^ fs, __double2loint(c)), K);
+  } else {
+    fm::sincos_fast(psi, &f.sp, &f.cp, K);
+  }
   return f;
 }
 
@@ -503,6 +517,18 @@ constexpr bool kLeanLA = true;
 struct FusedK {
   double h, hm, hIlf, hIlr, m1, m0, m2, m3;   // hm = h/m; m1 = hm k1, m0 = hm k0,
 };                                            // m2 = hm k2, m3 = -hm k3 (StageK)
+
+// The fused rollouts that carry the scaled yaw state (W = h omega, Psi = (2/pi) psi, see
+// make_fused): the LPM-4 quad (round 2) and, from round 3, the LPM-1 lane (its sin/cos psi by
+// the fold of forces_fast; -DLLAMPC_NO_SCALED1 keeps LPM 1 on sincos_fast for A/B runs).
+// LPM 2 keeps omega and psi.
+constexpr bool scaled_yaw(int lpm) {
+#ifdef LLAMPC_NO_SCALED1
+  return lpm == 4;
+#else
+  return lpm == 4 || lpm == 1;
+#endif
+}
 // SCALED (the LPM = 4 quad): the rollout state carries W = h omega and Psi = (2/pi) psi
 // instead of omega and psi.  Then the yaw increment IS W (no h omega product), vy W and vx W
 // are the h vy omega / h vx omega terms of the velocity increments, the omega increment
@@ -536,7 +562,7 @@ __device__ __forceinline__ void k_fused(const StageK& sk, const FusedK& q, doubl
                                         double hmsd, double hmcd, double c5a, double d, double Bd,
                                         const double* y, double* k, const fm::FmK& K, Dom& dm) {
   const double vx = y[3], vy = y[4], om = y[5];
-  constexpr bool kScaled = (LPM == 4);    // om = W = h omega, y[2] = Psi (make_fused)
+  constexpr bool kScaled = scaled_yaw(LPM);   // om = W = h omega, y[2] = Psi (make_fused)
   const StageF f = forces_fast<LPM, SPLIT, kScaled, kLeanLA>(sk, vx, vy, om, d, y[2], K, dm, Bd);
   // h sin(psi), h cos(psi): LPM = 4 lanes 2/3 scale their sine by h already (make_stage)
   const double hsp = (LPM == 4) ? f.sp : q.h * f.sp, hcp = (LPM == 4) ? f.cp : q.h * f.cp;
@@ -575,7 +601,7 @@ __device__ __forceinline__ void step_fused(const StageK& sk, const FusedK& q, do
   y[1] = acc[1] = 0.0;
   k_fused<LPM, SPLIT>(sk, q, F0, F1, hmsd, hmcd, c5a, u.d, Bd, x, k, K, dm);
   // the quad's yaw is Psi = (2/pi) psi with increment W (make_fused): weights x 2/pi
-  constexpr bool kScaled = (LPM == 4);
+  constexpr bool kScaled = scaled_yaw(LPM);
   const double c2 = kScaled ? K.inv_pi : 0.5, c4 = kScaled ? K.two_pi : 1.0,
                c6 = kScaled ? K.inv_3pi : K.sixth;
 #pragma unroll

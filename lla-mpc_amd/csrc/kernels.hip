@@ -71,7 +71,20 @@ __device__ unsigned long long g_rl_ph[1024][4];         // raceline prologue pha
       g_stamps[l][slot][1] = __builtin_amdgcn_s_memrealtime();                           \
     }                                                                                    \
   } while (0)
+// work-queue layout: per wave, per unit j < 16, (s_memtime, s_memrealtime) at [0] the unit
+// taken, [1] its Pacejka row loaded, [2] rolled out, [3] done (the tagged stores issued)
+__device__ unsigned long long g_wq_unit[256][8][16][4][2];
+#define WQ_STAMP(blk, j, slot)                                                           \
+  do {                                                                                   \
+    if ((threadIdx.x & 63) == 0 && (blk) < 256 && (j) < 16) {                            \
+      g_wq_unit[blk][threadIdx.x >> 6][j][slot][0] = __builtin_amdgcn_s_memtime();       \
+      g_wq_unit[blk][threadIdx.x >> 6][j][slot][1] = __builtin_amdgcn_s_memrealtime();   \
+    }                                                                                    \
+  } while (0)
 #else
+#define WQ_STAMP(blk, j, slot) \
+  do {                         \
+  } while (0)
 #define STAMP(slot) \
   do {              \
   } while (0)
@@ -574,7 +587,7 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
 #pragma unroll
   for (int m = 0; m < 6; ++m) x[m] = x0[m];
   if (SPLIT) x[0] = sk.pc ? x0[1] : x0[0];
-  if (FAST && INTEG == 0 && LPM == 4) {   // the quad's scaled yaw and yaw rate (make_fused)
+  if (FAST && INTEG == 0 && scaled_yaw(LPM)) {   // the scaled yaw and yaw rate (make_fused)
     x[2] = x0[2] * K.two_pi;
     x[5] = x0[5] * Ts;
   }
@@ -694,8 +707,12 @@ __device__ __forceinline__ void copy_lds(double* dst, int count, Src src) {
 // The block's partial of the look-ahead argmin over (model, candidate) in flattened order
 // (goff+n)*C + c — (v, key) per lane (kNoIndex: none) and the lanes' non-finite counts:
 // branch-free wave picks, one LDS exchange, thread 0 publishes (tagged words or plain).
+template <int NW = kWaves>
 __device__ __forceinline__ void la_publish(const LookaheadLaunch& a, int blk, const Scratch& sc, int par,
                                            double v, int64_t key, int nf) {
+  // NW = 8 (the work-queue block) uses both halves of sv / si (par = 0 there) and sn[4..8)
+  // (the scratch pad up to kScratchBytes)
+  static_assert(NW == kWaves || NW == 8, "4- or 8-wave blocks");
   wave_pick_nl64(v, key);
   const int nfw = wave_sum(nf);
   double* sv = sc.sv + 4 * par;         // the buffer a span > 64 exchange did not use
@@ -709,7 +726,7 @@ __device__ __forceinline__ void la_publish(const LookaheadLaunch& a, int blk, co
   if (threadIdx.x == 0) {
     int nfs = sc.sn[0];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) {
+    for (int w = 1; w < NW; ++w) {
       const bool t = (int)(si[w] != kNoIndex) & (int)less_bf<0>(sv[w], si[w], v, key);
       v = t ? sv[w] : v;
       key = t ? si[w] : key;
@@ -740,6 +757,7 @@ template <int INTEG, bool STAGE, int LPM, int XM, bool WQ = false>
 __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int blk, int G, int cpl,
                                                 unsigned char* smem, const Scratch& sc) {
   LA_STAMP(blk, 0);
+  constexpr int BT = WQ ? wq_threads(STAGE) : kBlock;   // threads of this block
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);
   double* su = sx + 2 * (a.H + 1);
   const int H = a.H, C = a.C;
@@ -860,7 +878,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     __threadfence_block();
     RL_STAMP(blk, 3);
   } else {
-    for (int e = threadIdx.x; e <= H; e += kBlock) {
+    for (int e = threadIdx.x; e <= H; e += BT) {
       sx[2 * e] = a.xref[e];
       sx[2 * e + 1] = a.xref[(H + 1) + e];
     }
@@ -881,8 +899,8 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       if constexpr (XM) return fm::FmK::load();
       else return K0;
     }();
-    const FusedK fq0 = make_fused(a.veh, make_stage<1>(a.veh, Tire{}, 0), a.Ts, LPM == 4);
-    for (int e = (int)threadIdx.x - soff; e < C * H; e += kBlock - soff) {
+    const FusedK fq0 = make_fused(a.veh, make_stage<1>(a.veh, Tire{}, 0), a.Ts, scaled_yaw(LPM));
+    for (int e = (int)threadIdx.x - soff; e < C * H; e += BT - soff) {
       if (e < 0) break;
       const int c = e / H, k = e - c * H;
       const double dl = a.U[2 * e + 1];
@@ -957,10 +975,22 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     const int mpw = 64 / G;
     const int64_t units = (a.n + mpw - 1) / mpw;
     const int lm = (int)(threadIdx.x & 63) / G;
-    auto issue = [&]() -> uint64_t {
+    // The take must stay in flight across the rollouts.  In v30 every unit waited for its
+    // round trip (ISA: s_waitcnt vmcnt(0) right after the atomic): the atomic optimizer
+    // rewrites an atomic on a uniform address into one lane's atomic plus a
+    // readfirstlane/prefix epilogue that uses the result at once.  So the address carries an
+    // opaque zero VGPR offset (not uniform to the compiler: no optimizer rewrite).  And with
+    // the row loads and the atomic both pending, the waitcnt pass cannot count them apart
+    // (a returning atomic and loads are different event kinds: it waits for vmcnt(0), i.e.
+    // for the atomic too, at the first use of the row); so the offset of each take is a zero
+    // that depends on the unit's Pacejka row (an asm reading the six values): the row is
+    // waited for first, then the atomic goes out and nothing waits for it until take().
+    uint32_t zoff;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zoff));
+    auto issue = [&](uint32_t off) -> uint64_t {
       uint64_t v = 0;
       if ((threadIdx.x & 63) == 0)
-        v = __hip_atomic_fetch_add(a.wq, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = __hip_atomic_fetch_add(a.wq + off, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return v;
     };
     auto take = [&](uint64_t v) -> int64_t {
@@ -972,16 +1002,29 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     int64_t kacc = kNoIndex;
     int nfacc = 0;
     const fm::FmK K = K0;
-    for (int64_t u = take(issue()); u < units;) {          // wave-uniform
-      const uint64_t nxt = issue();
+#ifdef LLAMPC_STAMPS
+    int ju = 0;                                             // this wave's unit count
+#endif
+    for (int64_t u = take(issue(zoff)); u < units;) {      // wave-uniform
+      WQ_STAMP(blk, ju, 0);
       const int64_t nm = u * mpw + lm;
       const bool lv = nm < a.n;
+      Tire tm{};
+      if (lv) tm = load_tire(a.params, a.n, nm);
+      uint32_t dep;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(dep) : "v"(tm.Bf), "v"(tm.Cf), "v"(tm.Df), "v"(tm.Br), "v"(tm.Cr), "v"(tm.Dr));
+      WQ_STAMP(blk, ju, 1);
+      const uint64_t nxt = issue(dep);
       double mv = __builtin_nan("");
       int64_t mc = kNoIndex;
       if (lv) {
-        const Tire tm = load_tire(a.params, a.n, nm);
-        const StageK sk = make_stage<1>(veh, tm, 0, INTEG == 0 ? Ts : 1.0);
-        const FusedK fq = make_fused(veh, sk, Ts, false);
+        constexpr bool kScaled = (INTEG == 0 && scaled_yaw(1));
+        StageK sk = make_stage<1>(veh, tm, 0, INTEG == 0 ? Ts : 1.0);
+        if (kScaled) {                  // the chains' lw / h turns W back into omega
+          sk.ch[0].lw = sk.ch[0].lw / Ts;
+          sk.ch[1].lw = sk.ch[1].lw / Ts;
+        }
+        const FusedK fq = make_fused(veh, sk, Ts, kScaled);
         for (int j = 0; j < cpl; ++j) {
           const int c = g + j * G;
           if (c >= C) break;
@@ -1007,6 +1050,8 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
           mc = oc;
         }
       }
+      WQ_STAMP(blk, ju, 2);
+      const int64_t un = take(nxt);                         // before the unit's stores
       if (lv && g == 0) {
         if (a.poll) {
           st_wt(&a.la_tag[nm], tag_word(a.seq, (uint32_t)(__double_as_longlong(mv) >> 32)));
@@ -1024,10 +1069,14 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
           }
         }
       }
-      u = take(nxt);
+      WQ_STAMP(blk, ju, 3);
+#ifdef LLAMPC_STAMPS
+      ++ju;
+#endif
+      u = un;
     }
     LA_STAMP(blk, 2);
-    la_publish(a, blk, sc, 0, vacc, kacc, nfacc);
+    la_publish<BT / 64>(a, blk, sc, 0, vacc, kacc, nfacc);
     LA_STAMP(blk, 3);
     return;
   }
@@ -1035,10 +1084,11 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
     // LPM = 2: lane 0 of the pair evaluates the front chain, lane 1 the rear (dyn.hpp)
     // fused RK4 quads carry W = h omega and Psi = (2/pi) psi (make_fused): the chains'
     // lw / h turns W back into omega
-    constexpr bool kScaled = (INTEG == 0 && LPM == 4);
+    constexpr bool kScaled = (INTEG == 0 && scaled_yaw(LPM));
     StageK sk = make_stage<LPM>(veh, t, sub, INTEG == 0 ? Ts : 1.0);
     if (kScaled) sk.ch[0].lw = sk.ch[0].lw / Ts;
-    if (kScaled && sub >= 2) {
+    if (kScaled && LPM == 1) sk.ch[1].lw = sk.ch[1].lw / Ts;
+    if (kScaled && LPM == 4 && sub >= 2) {
       // lanes 2/3 run their (discarded) chain on zero operands — yy = z = 0, no extra
       // instruction: fewer toggling bits, a higher clock (A/B 28.86 -> 28.61 us/tick).
       // (Freezing the unused yaw of lanes 0/1 as well, by per-lane RK4 weights 0: 28.98.)
@@ -1770,6 +1820,12 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Scratch sc(smem);
   int* flag = reinterpret_cast<int*>(smem + 144);
+  // WQ launches run kBlockWQ threads per block: every role but the work-queue look-ahead is
+  // written for kBlock and its surplus waves leave at once (s_barrier waits for the waves
+  // that have not ended)
+  if constexpr (WQ && wq_threads(STAGE) > kBlock) {
+    if ((int)blockIdx.x < fin.nb_lb && threadIdx.x >= kBlock) return;
+  }
   if ((int)blockIdx.x < fin.nb_lb) {
     lookback_block(lb, blockIdx.x, sc);
     if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
@@ -1788,6 +1844,9 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
   } else {
     lookahead_block<INTEG, STAGE, LPM, XM, WQ>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
     if (fin.poll) return;                // published tagged records; no ticket
+    if constexpr (WQ && wq_threads(STAGE) > kBlock) {
+      if (threadIdx.x >= kBlock) return;
+    }
   }
   const unsigned expected = (unsigned)fin.nb_la + (fin.nb_lb > 0 ? 1u : 0u);
   if (!ticket_last(&fin.tickets[1], expected, flag)) return;
@@ -1798,7 +1857,7 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
 // PX: the sharded tick's fused peer exchange (a separate instantiation, so the plain tick's
 // code is unchanged: inlining it into every variant cost the headline tick 0.5 us)
 template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false, bool WQ = false>
-__global__ __launch_bounds__(kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
+__global__ __launch_bounds__(WQ ? wq_threads(STAGE) : kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
                                                       FinalLaunch fin, int G, int cpl) {
   plan_body<INTEG, STAGE, LPM, XM, PX, WQ>(lb, la, fin, G, cpl);
 }
@@ -2058,11 +2117,11 @@ static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, c
     if (wq) {                            // work queue: given xref only (launch_plan checks)
       if (f.px_G) {
         allow_lds(plan_kernel<INTEG, STAGE, 1, 0, true, true>);
-        hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, true, true>), dim3(f.nb_lb + f.nb_la), dim3(kBlock),
+        hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, true, true>), dim3(f.nb_lb + f.nb_la), dim3(wq_threads(STAGE)),
                            lds, s, lb, la, f, G, cpl);
       } else {
         allow_lds(plan_kernel<INTEG, STAGE, 1, 0, false, true>);
-        hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, false, true>), dim3(f.nb_lb + f.nb_la), dim3(kBlock),
+        hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, false, true>), dim3(f.nb_lb + f.nb_la), dim3(wq_threads(STAGE)),
                            lds, s, lb, la, f, G, cpl);
       }
       return;
@@ -2190,7 +2249,7 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
       const int64_t mpw = 64 / G;
       f.nb_la = nw;
       wq = true;
-      if (wq_advance) *wq_advance = (la->n + mpw - 1) / mpw + (int64_t)nw * kWaves;
+      if (wq_advance) *wq_advance = (la->n + mpw - 1) / mpw + (int64_t)nw * (wq_threads(stage) / 64);
     }
   }
   if (f.px_G) {                          // fused peer exchange: RK4, given xref, device inputs
@@ -2240,6 +2299,14 @@ extern "C" int llampc_debug_la_wave(unsigned long long* out) {
 }
 extern "C" int llampc_debug_la_all(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_all), sizeof(g_la_all)) == hipSuccess ? 0 : -2;
+}
+extern "C" int llampc_debug_wq_units(unsigned long long* out) {   // [256][8][16][4][2]
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wq_unit), sizeof(g_wq_unit)) == hipSuccess ? 0 : -2;
+}
+extern "C" int llampc_debug_wq_reset() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_wq_unit)) != hipSuccess) return -2;
+  return hipMemset(p, 0, sizeof(g_wq_unit)) == hipSuccess ? 0 : -2;
 }
 extern "C" int llampc_debug_la_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_stamps), sizeof(g_la_stamps)) == hipSuccess ? 0 : -2;

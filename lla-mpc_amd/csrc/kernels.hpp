@@ -11,6 +11,18 @@
 namespace llampc {
 
 constexpr int kBlock = 256;            // 4 waves of 64 lanes
+// The work-queue layout's look-ahead blocks (throughput regime): 8 waves, one block per CU,
+// so each SIMD interleaves two rollout waves (a lone fp64 wave issues ~4.7 cycles per
+// instruction against the VALU's 4).  The other roles of that launch use 256 threads (the
+// rest of their waves exit at once).  -DLLAMPC_WQ_BLOCK=256 keeps one wave per SIMD (A/B).
+#ifdef LLAMPC_WQ_BLOCK
+constexpr int kBlockWQ = LLAMPC_WQ_BLOCK;
+#else
+constexpr int kBlockWQ = 512;
+#endif
+// Threads per block of a work-queue launch: 8 waves when the candidates are staged in LDS
+// (the unstaged variant's rollout would spill at two waves per SIMD).
+constexpr int wq_threads(bool stage) { return stage ? kBlockWQ : kBlock; }
 
 // Cost constants pre-scaled for the kernel (rate bounds multiplied by Ts).
 struct CostK {
