@@ -309,7 +309,11 @@ enum llampc_math_fn { LLAMPC_MATH_ATAN2_XPOS = 0, LLAMPC_MATH_ATAN = 1, LLAMPC_M
                       LLAMPC_MATH_DIV6 = 9,
                       /* the look-ahead's lean cores (fastmath.hpp kAtanRL / kSinWQL) */
                       LLAMPC_MATH_ATAN2_LEAN = 10, LLAMPC_MATH_ATAN_LEAN = 11,
-                      LLAMPC_MATH_SIN_WIDE_LEAN = 12 };
+                      LLAMPC_MATH_SIN_WIDE_LEAN = 12,
+                      /* the LPM-1 look-ahead lane's paired lean cores (front and rear division
+                         through one reciprocal): out[i] = the first result of the pair
+                         (a[i], a[n-1-i]) — atan2 with x = b[i], or atan */
+                      LLAMPC_MATH_ATAN2_PAIR = 13, LLAMPC_MATH_ATAN_PAIR = 14 };
 int llampc_math_batch(int32_t fn, const double* a, const double* b, int64_t n, double* out,
                       int32_t device);
 

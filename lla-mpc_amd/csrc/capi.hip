@@ -1245,9 +1245,9 @@ extern "C" int llampc_integrate_batch(const double* x0, const double* u, int64_t
 extern "C" int llampc_math_batch(int32_t fn, const double* a, const double* b, int64_t n,
                                  double* out, int32_t device) {
   if (!a || !out || ((fn == LLAMPC_MATH_ATAN2_XPOS || fn == LLAMPC_MATH_ATAN2_FAST ||
-                      fn == LLAMPC_MATH_ATAN2_LEAN) && !b))
+                      fn == LLAMPC_MATH_ATAN2_LEAN || fn == LLAMPC_MATH_ATAN2_PAIR) && !b))
     return fail(LLAMPC_E_ARG, "NULL argument");
-  if (fn < LLAMPC_MATH_ATAN2_XPOS || fn > LLAMPC_MATH_SIN_WIDE_LEAN) return fail(LLAMPC_E_ARG, "fn %d", fn);
+  if (fn < LLAMPC_MATH_ATAN2_XPOS || fn > LLAMPC_MATH_ATAN_PAIR) return fail(LLAMPC_E_ARG, "fn %d", fn);
   if (n <= 0) return LLAMPC_OK;
   int dev, rc;
   if ((rc = resolve_device(device, &dev))) return rc;

@@ -292,7 +292,23 @@ struct Dom {
   __device__ __forceinline__ bool ok() const {
     return (int)(hi <= 0x1p999) & (int)(lo >= 0x1p-1000) & (int)(ps <= fm::kSinCosMax);
   }
+  // chain_pair (one reciprocal per front/rear pair): the atan2 divisors in [2^-500, 2^499]
+  // and the atan divisors' product (>= 1) at most 2^499, so every divisor and product of
+  // two stays a normal number (fastmath.hpp atan_ratio_pair)
+  __device__ __forceinline__ bool ok_paired() const {
+    return (int)(hi <= 0x1p499) & (int)(lo >= 0x1p-500) & (int)(ps <= fm::kSinCosMax);
+  }
 };
+
+// -DLLAMPC_PAIR_LA: the LPM-1 look-ahead lane evaluates its front and rear chains with one
+// reciprocal per division pair (chain_pair; lean cores only).  A/B only: 16 -> 8 v_rcp_f64 but
+// 843 -> 858 instructions per step, and C = 64 ran 375-380 -> 383-385 us per tick
+// (profiles/r03/v31/ab_pair_c64.log), so the default keeps two chain_fast.
+#ifdef LLAMPC_PAIR_LA
+constexpr bool kPairLA = true;
+#else
+constexpr bool kPairLA = false;
+#endif
 
 // F = D sin(C atan(B slip)) with slip = dsel - atan2(yy, den) for the front tire
 // (dsel = delta) and atan2(yy, den) for the rear (dsel = 0); yy = lf om + vy | lr om - vy
@@ -308,6 +324,25 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
   dm.lo = fm::vmin(dm.lo, h2);
   dm.hi = fm::vmax(dm.hi, h2);
   return c.D * fm::sin_wide<LEAN>(c.C * at, K);
+}
+
+// Both chains of an LPM-1 lane (front: dsel = delta, rear: dsel = 0) with their divisions
+// paired (fastmath.hpp atan2_fast_pair / atan_fast_pair): the same lean evaluation as two
+// chain_fast<true> up to the division's roundings; the domain is Dom::ok_paired.
+__device__ __forceinline__ void chain_pair(const Chain& cf, const Chain& cr, double den, double vy,
+                                           double om, double d, Dom& dm, const fm::FmK& K,
+                                           double& Ff, double& Fr) {
+  const double yf = fma(cf.lw, om, cf.sg * vy), yr = fma(cr.lw, om, cr.sg * vy);
+  double af, ar, hf, hr, dp;
+  fm::atan2_fast_pair(yf, yr, den, K, af, ar, hf, hr, dp);
+  const double zf = cf.B * fma(-cf.sg, af, d), zr = cr.B * fma(-cr.sg, ar, 0.0);
+  double tf, tr, dz;
+  fm::atan_fast_pair(zf, zr, K, tf, tr, dz);
+  dm.lo = fm::vmin(dm.lo, fm::vmin(hf, hr));
+  dm.hi = fm::vmax(dm.hi, fm::vmax(hf, hr));
+  dm.hi = fm::vmax(dm.hi, dz);
+  Ff = cf.D * fm::sin_wide<true>(cf.C * tf, K);
+  Fr = cr.D * fm::sin_wide<true>(cr.C * tr, K);
 }
 
 // LPM = 4: the quad's lanes run ONE instruction stream — lanes 0/1 the front/rear chain,
@@ -434,6 +469,8 @@ __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, doub
     const double r = chain_fast<LEAN>(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
     f.Ffy = dpp_bcast<kPair0>(r);
     f.Fry = dpp_bcast<kPair1>(r);
+  } else if constexpr (LEAN && kPairLA) {
+    chain_pair(sk.ch[0], sk.ch[1], den, vy, om, d, dm, K, f.Ffy, f.Fry);
   } else {
     f.Ffy = chain_fast<LEAN>(sk.ch[0], den, vy, om, d, dm, K);
     f.Fry = chain_fast<LEAN>(sk.ch[1], den, vy, om, 0.0, dm, K);

@@ -392,6 +392,59 @@ __device__ __forceinline__ double atan_fast(double z, const FmK& K) {
   return atan_fast<LEAN>(z, K, hz);
 }
 
+// Two independent reduced-ratio atans with ONE reciprocal (the LPM-1 lane's front and rear
+// chains, lean cores only): 1/den_f = den_r / (den_f den_r) and 1/den_r = den_f / (den_f
+// den_r), the product's reciprocal with one Newton step.  v_rcp_f64 issues for 16 cycles
+// against 4 for an FMA, so the pair costs 44 VALU cycles instead of 56.  Valid while both
+// divisors lie in [2^-500, 2^500] (the product then stays a normal number): the callers'
+// domain record (dyn.hpp Dom::ok_paired) checks that.  dprod = the product, for that record.
+__device__ __forceinline__ void atan_ratio_pair(double nf, double df, double nr, double dr,
+                                                const FmK& K, double& of, double& orr,
+                                                double& dprod) {
+  const bool redf = nf > K.tp8 * df, redr = nr > K.tp8 * dr;
+  const double sff = __hiloint2double(redf ? 0x3FF00000 : 0, 0);
+  const double sfr = __hiloint2double(redr ? 0x3FF00000 : 0, 0);
+  const double denf = fma(sff, nf, df), denr = fma(sfr, nr, dr);
+  const double D = denf * denr;
+  double r = __builtin_amdgcn_rcp(D);
+  const double e = fma(-D, r, 1.0);
+  r = fma(r, e, r);
+  const double tf = fma(-sff, df, nf) * (denr * r);
+  const double tr = fma(-sfr, dr, nr) * (denf * r);
+  const double sf2 = tf * tf, sr2 = tr * tr;
+  of = fma(sff, K.pio4, fma(tf * sf2, horner<9>(K.ar, sf2), tf));
+  orr = fma(sfr, K.pio4, fma(tr * sr2, horner<9>(K.ar, sr2), tr));
+  dprod = D;
+}
+
+// atan2(y_f, x) and atan2(y_r, x) (x >= 0) by atan_ratio_pair; hf / hr = the divisors
+// max(|y|, |x|) for the domain record, dprod the reciprocal's product.
+__device__ __forceinline__ void atan2_fast_pair(double yf, double yr, double x, const FmK& K,
+                                                double& af, double& ar, double& hf, double& hr,
+                                                double& dprod) {
+  hf = vmax_abs2(yf, x);
+  hr = vmax_abs2(yr, x);
+  double rf, rr;
+  atan_ratio_pair(vmin_abs2(yf, x), hf, vmin_abs2(yr, x), hr, K, rf, rr, dprod);
+  const double of = (fabs(yf) > fabs(x)) ? K.pio2 - rf : rf;
+  const double orr = (fabs(yr) > fabs(x)) ? K.pio2 - rr : rr;
+  af = copysign(of, yf);
+  ar = copysign(orr, yr);
+}
+
+// atan(z_f) and atan(z_r) by atan_ratio_pair; dprod = the product of the divisors
+// max(|z|, 1) (+ the reduction's share), >= 1: the domain record bounds it from above.
+__device__ __forceinline__ void atan_fast_pair(double zf, double zr, const FmK& K, double& af,
+                                               double& ar, double& dprod) {
+  double rf, rr;
+  atan_ratio_pair(vmin_abs(zf, K.one), vmax_abs(zf, K.one), vmin_abs(zr, K.one),
+                  vmax_abs(zr, K.one), K, rf, rr, dprod);
+  const double of = (fabs(zf) > 1.0) ? K.pio2 - rf : rf;
+  const double orr = (fabs(zr) > 1.0) ? K.pio2 - rr : rr;
+  af = copysign(of, zf);
+  ar = copysign(orr, zr);
+}
+
 // sin(a) for |a| <= kSinWideMax, one polynomial (the Pacejka argument C*atan(.) is
 // bounded by |C| pi/2, so |C| <= 1.9 keeps every call in range).
 template <bool LEAN = false>

@@ -668,7 +668,11 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   // the domain, once per rollout: a NaN operand reaches x[0..1] (every chain output feeds
   // the later stages' positions, the last stage's feeds vx, vy, omega only through a NaN
   // state that the position update already carries), so a non-finite J is re-run too
-  if (FAST) bad = (int)bad | (int)!sk.sok | (int)!dm.ok() | (int)!(fabs(J) <= __DBL_MAX__);
+  if (FAST) {
+    constexpr bool kPaired = INTEG == 0 && LPM == 1 && kLeanLA && kPairLA;   // dyn.hpp chain_pair
+    const bool dok = kPaired ? dm.ok_paired() : dm.ok();
+    bad = (int)bad | (int)!sk.sok | (int)!dok | (int)!(fabs(J) <= __DBL_MAX__);
+  }
   if (STAGE) feas = feas_s != 0.0;
   if (!feas) J = __builtin_inf();
   return J;
@@ -1991,6 +1995,15 @@ __global__ __launch_bounds__(kBlock) void math_kernel(int32_t fn, const double* 
     case 10: r = fm::atan2_fast<true>(a[i], b[i], fm::FmK::load<true>()); break;
     case 11: r = fm::atan_fast<true>(a[i], fm::FmK::load<true>()); break;
     case 12: r = fm::sin_wide<true>(a[i], fm::FmK::load<true>()); break;
+    case 13:   // paired atan2 (dyn.hpp chain_pair): partner element n-1-i, the same x
+    case 14: { // paired atan: partner element n-1-i
+      const int64_t j = n - 1 - i;
+      double af, ar, hf, hr, dp;
+      if (fn == 13) fm::atan2_fast_pair(a[i], a[j], b[i], fm::FmK::load<true>(), af, ar, hf, hr, dp);
+      else fm::atan_fast_pair(a[i], a[j], fm::FmK::load<true>(), af, ar, dp);
+      r = af;
+      break;
+    }
     default: r = __builtin_nan("");
   }
   out[i] = r;

@@ -652,6 +652,18 @@ def test_lean_cores_accuracy_on_domain(nat):
     a = np.concatenate([rng.uniform(-3, 3, n), [3.0, -3.0, 0.0, -0.0, 1e-300]])
     err = np.abs(_math(nat, 12, a) - np.sin(a))
     assert np.all(err <= 16 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -47), err.max()
+    # the paired cores of the LPM-1 look-ahead lane (math fn 13/14: front and rear division
+    # through one reciprocal, partner = element n-1-i) on their domain (Dom::ok_paired:
+    # atan2 divisors max(|y|, x) in [2^-500, 2^499], atan divisor products <= 2^499)
+    ok2 = ok & (np.maximum(np.abs(y), x) >= 2.0 ** -500) & (np.maximum(np.abs(y), x) <= 2.0 ** 499)
+    yy, xx = y[ok2], x[ok2]
+    part = np.maximum(np.abs(yy[::-1]), xx) >= 2.0 ** -500
+    got = _math(nat, 13, yy, xx)
+    u_p2 = _ulp(got[part], np.arctan2(yy, xx)[part])
+    zz = z[np.abs(z) <= 2.0 ** 240]
+    u_p = _ulp(_math(nat, 14, zz), np.arctan(zz))
+    print(f"paired cores: atan2 {u_p2:.1f} ulp, atan {u_p:.1f} ulp")
+    assert u_p2 <= 128 and u_p <= 128
 
 
 def test_lookahead_out_of_domain_fallback(nat):
