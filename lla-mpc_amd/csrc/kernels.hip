@@ -1827,11 +1827,20 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
   // WQ launches run kBlockWQ threads per block: every role but the work-queue look-ahead is
   // written for kBlock and its surplus waves leave at once (s_barrier waits for the waves
   // that have not ended)
+  // block roles: look-back blocks first in the grid (dispatch order); -DLLAMPC_LA_FIRST puts
+  // the look-ahead blocks first (A/B)
+#ifdef LLAMPC_LA_FIRST
+  const bool is_lb = (int)blockIdx.x >= fin.nb_la;
+  const int lb_blk = (int)blockIdx.x - fin.nb_la, la_blk = (int)blockIdx.x;
+#else
+  const bool is_lb = (int)blockIdx.x < fin.nb_lb;
+  const int lb_blk = (int)blockIdx.x, la_blk = (int)blockIdx.x - fin.nb_lb;
+#endif
   if constexpr (WQ && wq_threads(STAGE) > kBlock) {
-    if ((int)blockIdx.x < fin.nb_lb && threadIdx.x >= kBlock) return;
+    if (is_lb && threadIdx.x >= kBlock) return;
   }
-  if ((int)blockIdx.x < fin.nb_lb) {
-    lookback_block(lb, blockIdx.x, sc);
+  if (is_lb) {
+    lookback_block(lb, lb_blk, sc);
     if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
     if (fin.full) {
       lb_final(fin, smem);
@@ -1846,7 +1855,7 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
       return;
     }
   } else {
-    lookahead_block<INTEG, STAGE, LPM, XM, WQ>(la, blockIdx.x - fin.nb_lb, G, cpl, smem, sc);
+    lookahead_block<INTEG, STAGE, LPM, XM, WQ>(la, la_blk, G, cpl, smem, sc);
     if (fin.poll) return;                // published tagged records; no ticket
     if constexpr (WQ && wq_threads(STAGE) > kBlock) {
       if (threadIdx.x >= kBlock) return;
