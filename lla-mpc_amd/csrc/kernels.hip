@@ -757,11 +757,11 @@ __device__ __forceinline__ void la_publish(const LookaheadLaunch& a, int blk, co
 // bank's work counter, so the staging prologue runs once per CU instead of once per 4 models
 // and no CU waits for a new block between units (v29 stamps at C = 64: prologue 3.4 us and
 // reduction 2 us of each 45 us block).
-template <int INTEG, bool STAGE, int LPM, int XM, bool WQ = false>
+template <int INTEG, bool STAGE, int LPM, int XM, int WQ = 0>
 __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int blk, int G, int cpl,
                                                 unsigned char* smem, const Scratch& sc) {
   LA_STAMP(blk, 0);
-  constexpr int BT = WQ ? wq_threads(STAGE) : kBlock;   // threads of this block
+  constexpr int BT = wq_threads(WQ);   // threads of this block
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);
   double* su = sx + 2 * (a.H + 1);
   const int H = a.H, C = a.C;
@@ -1818,7 +1818,7 @@ __device__ __forceinline__ void peer_finish(const FinalLaunch& f, unsigned char*
 // (lb_final) while look-ahead blocks still run; the last block overall completes the
 // llampc_plan_out record (final_select).
 // ------------------------------------------------------------------------------------
-template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false, bool WQ = false>
+template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false, int WQ = 0>
 __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const LookaheadLaunch& la,
                                           const FinalLaunch& fin, int G, int cpl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1836,7 +1836,7 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
   const bool is_lb = (int)blockIdx.x < fin.nb_lb;
   const int lb_blk = (int)blockIdx.x, la_blk = (int)blockIdx.x - fin.nb_lb;
 #endif
-  if constexpr (WQ && wq_threads(STAGE) > kBlock) {
+  if constexpr (wq_threads(WQ) > kBlock) {
     if (is_lb && threadIdx.x >= kBlock) return;
   }
   if (is_lb) {
@@ -1857,7 +1857,7 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
   } else {
     lookahead_block<INTEG, STAGE, LPM, XM, WQ>(la, la_blk, G, cpl, smem, sc);
     if (fin.poll) return;                // published tagged records; no ticket
-    if constexpr (WQ && wq_threads(STAGE) > kBlock) {
+    if constexpr (wq_threads(WQ) > kBlock) {
       if (threadIdx.x >= kBlock) return;
     }
   }
@@ -1869,8 +1869,8 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
 
 // PX: the sharded tick's fused peer exchange (a separate instantiation, so the plain tick's
 // code is unchanged: inlining it into every variant cost the headline tick 0.5 us)
-template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false, bool WQ = false>
-__global__ __launch_bounds__(WQ ? wq_threads(STAGE) : kBlock) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
+template <int INTEG, bool STAGE, int LPM, int XM, bool PX = false, int WQ = 0>
+__global__ __launch_bounds__(wq_threads(WQ)) void plan_kernel(LookbackLaunch lb, LookaheadLaunch la,
                                                       FinalLaunch fin, int G, int cpl) {
   plan_body<INTEG, STAGE, LPM, XM, PX, WQ>(lb, la, fin, G, cpl);
 }
@@ -2131,21 +2131,29 @@ static void allow_lds(KERN k) {
   }
 }
 
+template <int INTEG, bool STAGE, int PX, int WQ>
+static void launch_plan_wq(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
+                           int G, int cpl, size_t lds, hipStream_t s) {
+  allow_lds(plan_kernel<INTEG, STAGE, 1, 0, PX, WQ>);
+  hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, PX, WQ>), dim3(f.nb_lb + f.nb_la), dim3(wq_threads(WQ)),
+                     lds, s, lb, la, f, G, cpl);
+}
+
 template <int INTEG, bool STAGE, int LPM>
 static void launch_plan_t(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
-                          int G, int cpl, size_t lds, hipStream_t s, bool wq = false) {
+                          int G, int cpl, size_t lds, hipStream_t s, int wq = 0) {
   lds = std::max(lds, kOneBlockPerCuLds);
   if constexpr (INTEG == LLAMPC_RK4 && LPM == 1) {
     if (wq) {                            // work queue: given xref only (launch_plan checks)
-      if (f.px_G) {
-        allow_lds(plan_kernel<INTEG, STAGE, 1, 0, true, true>);
-        hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, true, true>), dim3(f.nb_lb + f.nb_la), dim3(wq_threads(STAGE)),
-                           lds, s, lb, la, f, G, cpl);
-      } else {
-        allow_lds(plan_kernel<INTEG, STAGE, 1, 0, false, true>);
-        hipLaunchKernelGGL((plan_kernel<INTEG, STAGE, 1, 0, false, true>), dim3(f.nb_lb + f.nb_la), dim3(wq_threads(STAGE)),
-                           lds, s, lb, la, f, G, cpl);
+      if constexpr (STAGE) {
+        if (wq == 2) {
+          if (f.px_G) launch_plan_wq<INTEG, STAGE, 1, 2>(lb, la, f, G, cpl, lds, s);
+          else launch_plan_wq<INTEG, STAGE, 0, 2>(lb, la, f, G, cpl, lds, s);
+          return;
+        }
       }
+      if (f.px_G) launch_plan_wq<INTEG, STAGE, 1, 1>(lb, la, f, G, cpl, lds, s);
+      else launch_plan_wq<INTEG, STAGE, 0, 1>(lb, la, f, G, cpl, lds, s);
       return;
     }
   }
@@ -2187,7 +2195,7 @@ bool plan_inline_ok(int32_t C, int32_t H, int32_t integrator, int32_t xref_mode)
 
 template <int INTEG, bool STAGE>
 static void launch_plan_l(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
-                          int G, int cpl, int lpm, size_t lds, hipStream_t s, bool wq = false) {
+                          int G, int cpl, int lpm, size_t lds, hipStream_t s, int wq = 0) {
   if (lpm == 4) launch_plan_t<INTEG, STAGE, 4>(lb, la, f, G, cpl, lds, s);
   else if (lpm == 2) launch_plan_t<INTEG, STAGE, 2>(lb, la, f, G, cpl, lds, s);
   else launch_plan_t<INTEG, STAGE, 1>(lb, la, f, G, cpl, lds, s, wq);
@@ -2260,18 +2268,28 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
   f.do_la = la != nullptr;
   if (f.nb_lb + f.nb_la == 0) return hipErrorInvalidValue;
   // Work queue (the throughput regime): LPM 1 with a model inside one wave (G <= 64), RK4 on
-  // the shared xref, device inputs, more look-ahead blocks than CUs — then one block per CU
-  // (minus the completing look-back block's) takes units of models from the bank's counter.
-  // LLAMPC_NO_WQ=1 keeps the block-per-models layout (A/B runs).
-  bool wq = false;
+  // the shared xref, device inputs, at least 1.75 rounds of look-ahead blocks per CU — then one
+  // block per CU (minus the completing look-back block's) takes units of models from the
+  // bank's counter: 8 waves per block (two rollout waves per SIMD) from 4 units per wave
+  // slot of the 4-wave layout on, else 4 waves.  C = 64 N-sweep on one box (static / 4-wave /
+  // 8-wave, us per tick; profiles/r03/v31/c64_sweep.txt): N = 1500: 92.0 / 99.5 / 106.9;
+  // 2000: 128.1 / 106.5 / 155.8; 3000: 163.9 / 137.7 / 164.4; 5000: 239.4 / 206.3 / 209.5;
+  // 10^4: 468.7 / 391.2 / 372.6; 2 10^4: 899.7 / 732.2 / 681.4 — the 8-wave layout's second
+  // wave of a SIMD only fills the first one's bubbles, so with few units per wave the launch
+  // waits for those slow units.  LLAMPC_NO_WQ=1 keeps the block-per-models layout,
+  // LLAMPC_WQ_WAVES=4|8 forces a work-queue block size (A/B runs).
+  int wq = 0;
   if (la && la->wq && lpm == 1 && G <= 64 && integ == LLAMPC_RK4 && la->xref_mode == LLAMPC_XREF_GIVEN &&
       !pk && getenv("LLAMPC_NO_WQ") == nullptr) {
     const int nw = std::max(1, device_cus() - 1);
-    if (f.nb_la > nw) {
+    const char* force = getenv("LLAMPC_WQ_WAVES");
+    const int forced = force ? atoi(force) : 0;
+    if ((int64_t)f.nb_la * 4 >= (int64_t)nw * 7 || (forced && f.nb_la > nw)) {
       const int64_t mpw = 64 / G;
+      const int64_t units = (la->n + mpw - 1) / mpw;
       f.nb_la = nw;
-      wq = true;
-      if (wq_advance) *wq_advance = (la->n + mpw - 1) / mpw + (int64_t)nw * (wq_threads(stage) / 64);
+      wq = (stage && (forced ? forced == 8 : units >= 4 * (int64_t)nw * kWaves)) ? 2 : 1;
+      if (wq_advance) *wq_advance = units + (int64_t)nw * (wq_threads(wq) / 64);
     }
   }
   if (f.px_G) {                          // fused peer exchange: RK4, given xref, device inputs

@@ -20,9 +20,11 @@ constexpr int kBlockWQ = LLAMPC_WQ_BLOCK;
 #else
 constexpr int kBlockWQ = 512;
 #endif
-// Threads per block of a work-queue launch: 8 waves when the candidates are staged in LDS
-// (the unstaged variant's rollout would spill at two waves per SIMD).
-constexpr int wq_threads(bool stage) { return stage ? kBlockWQ : kBlock; }
+// Work-queue layouts (plan kernel template argument WQ): 0 = none (block per models), 1 = one
+// 4-wave block per CU, 2 = one 8-wave block per CU (two rollout waves per SIMD; staged launches
+// only — the unstaged rollout would spill at 256 VGPRs).  launch_plan picks by the size of the
+// queue (C = 64 N-sweep, profiles/r03/v31/c64_sweep.txt).
+constexpr int wq_threads(int wq) { return wq == 2 ? kBlockWQ : kBlock; }
 
 // Cost constants pre-scaled for the kernel (rate bounds multiplied by Ts).
 struct CostK {

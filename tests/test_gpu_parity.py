@@ -893,7 +893,8 @@ def test_polled_completion_equals_ticket_completion(nat):
 def test_work_queue_layout_equals_static_and_oracle(nat, monkeypatch):
     """The throughput layout (launch_plan's work queue: one look-ahead block per CU, waves
     taking units of models from the bank's counter) at N = 3000, C = 64 (750 static blocks >
-    the CUs) and C = 40 (G = 64, ragged candidates): every record field equal to the static
+    the CUs) and C = 40 (G = 64, ragged candidates), with 4-wave and (forced) 8-wave blocks:
+    every record field equal to the static
     block-per-models layout (LLAMPC_NO_WQ=1) tick after tick — polled and ticket completion —
     costs equal to the oracle's at 1e-7, and the counter's base carried correctly across
     ticks, a reset and a second bank."""
@@ -905,7 +906,9 @@ def test_work_queue_layout_equals_static_and_oracle(nat, monkeypatch):
     rng = np.random.RandomState(13)
     Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
     p = generate_bank(N, seed=4)
-    for C in (64, 40):
+    for C, waves in ((64, None), (40, None), (64, "8"), (40, "8")):
+        if waves:                       # the 8-wave layout (launch_plan picks 4 waves here)
+            monkeypatch.setenv("LLAMPC_WQ_WAVES", waves)
         a_bank = ModelBank(p, W=W, device=0)
         b_bank = ModelBank(p, W=W, device=0)
         try:
@@ -937,6 +940,45 @@ def test_work_queue_layout_equals_static_and_oracle(nat, monkeypatch):
         finally:
             a_bank.close()
             b_bank.close()
+
+
+@pytest.mark.parametrize("N,C", [(6000, 20), (10000, 7)])
+def test_work_queue_several_models_per_wave(nat, monkeypatch, N, C):
+    """The work queue with units of several models per wave (G = 32: two models of 20
+    candidates; G = 8: eight models of 7 — lanes of one wave then read different Pacejka rows
+    and reduce over G-lane groups): records equal to the static layout, polled and ticket
+    completion, costs and the look-ahead argmin equal to the oracle's."""
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    H, W = 20, 2
+    rng = np.random.RandomState(17)
+    Q, R, P = np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2))
+    p = generate_bank(N, seed=5)
+    a_bank = ModelBank(p, W=W, device=0)
+    b_bank = ModelBank(p, W=W, device=0)
+    try:
+        for t in range(1, W + 2):
+            U = np.repeat(u[:, t:t + H].T[None], C, axis=0)
+            U[1:] += rng.uniform(-0.03, 0.03, U[1:].shape)
+            U[:, :, 1] = np.clip(U[:, :, 1], -0.35, 0.35)
+            xref = s[:2, t:t + H + 1] + 0.01
+            args = (s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1])
+            if t == W + 1:
+                monkeypatch.setenv("LLAMPC_NO_POLL", "1")
+            o, _, _, costs = a_bank.plan_raw(*args, K=5, current_model=3, return_costs=(t == W))
+            monkeypatch.setenv("LLAMPC_NO_WQ", "1")
+            w = b_bank.plan_raw(*args, K=5, current_model=3)[0]
+            monkeypatch.delenv("LLAMPC_NO_WQ")
+            monkeypatch.delenv("LLAMPC_NO_POLL", raising=False)
+            _same_records(o, w)
+            if costs is not None:
+                cref = O.mpc_cost(O.rollout_rk4(shared(), tuple(p), s[:, t], U, TS), U, xref, u[:, t - 1], Q, R, P)
+                close(costs.ravel(), cref, RTOL_ROLL)
+                assert (o.la_best_model, o.la_best_cand) == divmod(int(np.argmin(np.where(np.isnan(cref), np.inf, cref))), C)
+    finally:
+        a_bank.close()
+        b_bank.close()
 
 
 def test_poll_bound_scales_with_launch_work(nat, monkeypatch):

@@ -47,6 +47,9 @@ def _ticks(C=3):
 
 def _worker(rank, world, port, q, transport, C=3):
     try:
+        if transport.endswith("-wq8"):         # the 8-wave work-queue layout at this size
+            os.environ["LLAMPC_WQ_WAVES"] = "8"
+            transport = transport[:-4]
         if transport == "peer-split":
             os.environ["LLAMPC_PEER_SPLIT"] = "1"
             transport = "peer"
@@ -87,7 +90,7 @@ def _worker(rank, world, port, q, transport, C=3):
 
 CASES = ([(w, "peer", 3) for w in (2, 3, 4, 8)] + [(w, "host", 3) for w in (2, 3, 8)] +
          [(w, "peer-split", 3) for w in (2, 4)] + [(w, "peer-ticket", 3) for w in (2, 3, 8)] +
-         [(2, "peer", 64), (3, "peer-ticket", 64)])
+         [(2, "peer", 64), (3, "peer-ticket", 64), (2, "peer-wq8", 64), (3, "peer-ticket-wq8", 64)])
 
 
 @pytest.mark.parametrize("world,transport,C", CASES)
