@@ -6,4 +6,13 @@ vectorized`` (look-back scoring), the new fused tick ``llampc.mpc.plan`` and the
 ``llampc.mpc.ModelBank`` device handle, backed by hand-written HIP kernels in
 ``libllampc_hip.so`` (C ABI: include/llampc.h).  There is no CPU fallback.
 """
+import os as _os
+
+# Kernel arguments in device memory: the tick's blocks read their launch descriptors (and
+# through them the inputs) with scalar loads first, and with kernargs in host memory every
+# tick measured 5 us longer (31.3-32.3 vs 26.1-26.9 us, DESIGN.md §7).  HIP reads this when it
+# initialises, so it takes effect when llampc is imported before the first HIP call (bench.py
+# sets it too); an explicit setting in the environment is kept.
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 __version__ = "0.1.0"
