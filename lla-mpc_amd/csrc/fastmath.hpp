@@ -184,12 +184,27 @@ constexpr double kTanPi8 = 0.41421356237309503;
 // tan(pi/8)) and 9-term sin_wide (2.3e-15 absolute to |a| = 3, <= 4 ulp to 2), and the
 // division without its residual correction (<= 18 ulp): ~1e-14 relative on the tire forces
 // against the <= 4 ulp of the precise cores, which the look-back keeps (its errors are ranked).
+// -DLLAMPC_LEAN_TERMS=8 (A/B): 8-term lean cores (atan 1.1e-13 relative, sin_wide 2.6e-13
+// absolute to |a| = 3, tools/fit_fastmath.py), 12 fewer instructions per LPM-4 step.
+#ifndef LLAMPC_LEAN_TERMS
+#define LLAMPC_LEAN_TERMS 9
+#endif
+constexpr int kLeanTerms = LLAMPC_LEAN_TERMS;
+#if LLAMPC_LEAN_TERMS == 8
+constexpr double kAtanRL[8] = {-0.33333333333266196, 0.19999999949854794, -0.142857081103604,
+                               0.11110819716745676, -0.09084101895346429, 0.07604800046078292,
+                               -0.06027307460946675, 0.03295679541870136};
+constexpr double kSinWQL[8] = {-0.16666666666665675, 0.008333333333192344, -0.0001984126980834366,
+                               2.7557316292288437e-06, -2.5051980053729585e-08, 1.6055987705856629e-10,
+                               -7.606702398667312e-13, 2.530093775325291e-15};
+#else
 constexpr double kAtanRL[9] = {-0.3333333333333093, 0.19999999997724888, -0.14285713930378566,
                                0.11111089649211055, -0.09090255952690657, 0.07681045202742948,
                                -0.0655090730756309, 0.05168834935919362, -0.02723288406057488};
 constexpr double kSinWQL[9] = {-0.1666666666666666, 0.008333333333332372, -0.00019841269840984845,
                                2.755731919144023e-06, -2.5052106522437073e-08, 1.605898387304835e-10,
                                -7.646028139181475e-13, 2.7988830742041364e-15, -7.463851483197331e-18};
+#endif
 constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s) (10 terms, fit error 6e-18), |a| <= 3:
                                        // <= 3 ulp up to |a| = 2, then <= 2^-50 absolute (cancellation)
 
@@ -213,7 +228,7 @@ struct FmK {
   template <bool LEAN = false>
   __device__ __forceinline__ static FmK load() {
     FmK k;
-    constexpr int nA = LEAN ? 9 : 10;
+    constexpr int nA = LEAN ? kLeanTerms : 10;
 #ifdef LLAMPC_ATAN_FULL
 #pragma unroll
     for (int i = 0; i < 22; ++i) { k.at[i] = kAtanQ[i]; pin(k.at[i]); }
@@ -347,7 +362,7 @@ __device__ __forceinline__ double atan_ratio_k(double n, double d, const FmK& K)
   const double sf = __hiloint2double(red ? 0x3FF00000 : 0, 0);
   const double t = div_fast<LEAN>(fma(-sf, d, n), fma(sf, n, d));
   const double s = t * t;
-  return fma(sf, K.pio4, fma(t * s, horner<LEAN ? 9 : 10>(K.ar, s), t));
+  return fma(sf, K.pio4, fma(t * s, horner<LEAN ? kLeanTerms : 10>(K.ar, s), t));
 #endif
 }
 
@@ -412,8 +427,8 @@ __device__ __forceinline__ void atan_ratio_pair(double nf, double df, double nr,
   const double tf = fma(-sff, df, nf) * (denr * r);
   const double tr = fma(-sfr, dr, nr) * (denf * r);
   const double sf2 = tf * tf, sr2 = tr * tr;
-  of = fma(sff, K.pio4, fma(tf * sf2, horner<9>(K.ar, sf2), tf));
-  orr = fma(sfr, K.pio4, fma(tr * sr2, horner<9>(K.ar, sr2), tr));
+  of = fma(sff, K.pio4, fma(tf * sf2, horner<kLeanTerms>(K.ar, sf2), tf));
+  orr = fma(sfr, K.pio4, fma(tr * sr2, horner<kLeanTerms>(K.ar, sr2), tr));
   dprod = D;
 }
 
@@ -450,7 +465,7 @@ __device__ __forceinline__ void atan_fast_pair(double zf, double zr, const FmK& 
 template <bool LEAN = false>
 __device__ __forceinline__ double sin_wide(double a, const FmK& K) {
   const double s = a * a;
-  return fma(a * s, horner<LEAN ? 9 : 10>(K.sw, s), a);
+  return fma(a * s, horner<LEAN ? kLeanTerms : 10>(K.sw, s), a);
 }
 
 // sincos(a) for |a| <= kSinCosMax (NaN/inf -> not ok): Cody-Waite reduction, quadrant
