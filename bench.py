@@ -39,7 +39,9 @@ for _p in (REPO, os.path.join(REPO, "lla-mpc_amd")):
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector spec
-TIMING_STRIDE = 8               # HIP-event pairs bracket groups of 8 consecutive plan launches
+# ONE HIP-event pair brackets the whole timed loop (stride = --steps): each event record costs
+# ~5 us of stream time (kernel trace, profiles/r03/s3_ramp: a 10.2 us gap at every group
+# boundary), so the old groups of 8 added ~1.3 us to every timed tick
 TIMING_SAMPLE = 16              # with the exchange: one plan launch in 16 bracketed alone
 FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation (excl. transcendentals)
 # Issue roofline: instructions per rollout step of the fast look-ahead loop, per lane, by lane
@@ -375,14 +377,15 @@ def main():
     for i in range(args.warmup):
         step(i)
     if not args.no_timing:
-        # event pairs bracket groups of TIMING_STRIDE consecutive launches of the timed loop:
-        # the kernel's mean duration measured live, the events' own cost spread over a group.
+        # one event pair brackets all K consecutive launches of the timed loop: the kernel's
+        # mean duration measured live (back-to-back launches: the trace shows no gap between
+        # them, so elapsed / K is the mean duration), the events' own cost spread over K.
         # With the exchange, a group would also hold the all-gathers and merges in between,
         # so ONE plan launch in every TIMING_SAMPLE gets its own pair (negative stride =
         # sampling; the bracketed launch reads ~2 us high, the events' own cost, and only
         # 1/TIMING_SAMPLE of the timed ticks carry events: measured 0.8 us/tick of event
         # cost at 1 in 8 on a forced 1-rank exchange, ~2 us with a pair on every tick)
-        stride = -TIMING_SAMPLE if sb.exchange else TIMING_STRIDE
+        stride = -TIMING_SAMPLE if sb.exchange else max(args.steps, 1)
         nat.check(lib.llampc_bank_timing(sb.bank.handle, stride, args.steps // abs(stride) + 8))
     torch.cuda.synchronize()
     if world > 1:
@@ -460,7 +463,7 @@ def main():
             "issue": issue_roofline(N_local, C, H, lpm_of(N_local, C), plan_ms),
             "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0]),
                           "bracket": f"one plan launch in every {TIMING_SAMPLE} per event pair" if sb.exchange else
-                                     f"groups of {TIMING_STRIDE} consecutive plan launches"},
+                                     f"one event pair around all {args.steps} timed plan launches"},
             "exchange": EXCHANGE_DESC[sb.transport] if sb.exchange else None,
             "host_issue_us_per_step": t_issue / args.steps * 1e6,
             "lpm": lpm_of(N_local, C),
