@@ -372,12 +372,11 @@ def main():
     def step(i):
         sb.launch(pins[i % T], stream)
 
-    if world > 1:                       # every rank's exchange waits for the others' records
-        dist.barrier()
-    for i in range(args.warmup):
-        step(i)
+    avg = (ctypes.c_double * 3)()
+    cnt = (ctypes.c_int64 * 3)()
     if not args.no_timing:
-        # one event pair brackets all K consecutive launches of the timed loop: the kernel's
+        # events created (and the stream synchronised) before the warmup, so the gap between
+        # the warmup and the timed loop is the synchronize alone; one event pair brackets all K consecutive launches of the timed loop: the kernel's
         # mean duration measured live (back-to-back launches: the trace shows no gap between
         # them, so elapsed / K is the mean duration), the events' own cost spread over K.
         # With the exchange, a group would also hold the all-gathers and merges in between,
@@ -387,6 +386,12 @@ def main():
         # cost at 1 in 8 on a forced 1-rank exchange, ~2 us with a pair on every tick)
         stride = -TIMING_SAMPLE if sb.exchange else max(args.steps, 1)
         nat.check(lib.llampc_bank_timing(sb.bank.handle, stride, args.steps // abs(stride) + 8))
+    if world > 1:                       # every rank's exchange waits for the others' records
+        dist.barrier()
+    for i in range(args.warmup):
+        step(i)
+    if not args.no_timing:              # restart the count: the warmup launches are not timed
+        nat.check(lib.llampc_bank_timing_read(sb.bank.handle, avg, cnt))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -404,8 +409,6 @@ def main():
         el = max_over_ranks(el)
     ms = el / args.steps * 1e3
 
-    avg = (ctypes.c_double * 3)()
-    cnt = (ctypes.c_int64 * 3)()
     if not args.no_timing:
         nat.check(lib.llampc_bank_timing_read(sb.bank.handle, avg, cnt))
         nat.check(lib.llampc_bank_timing(sb.bank.handle, 0, 1))
