@@ -565,6 +565,23 @@ def extras(args, sb, stream, world, rank=0):
         out["sync_plan_latency_us"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                        "ticks": int(lat.size),
                                        "note": "host-pointer llampc_plan from Python: inputs as kernel arguments, record via pinned host memory + completion-tag spin"}
+        # the same call paced at the controller's period (rt.py: Ts = 0.02 s simulated, a 1 kHz
+        # loop in BASELINE config 5): the GPU idles ~0.96 ms between ticks, so every tick runs
+        # in the cold-clock regime that back-to-back ticks leave after ~600 launches
+        period = 1e-3
+        lat = []
+        nxt = time.perf_counter() + period
+        for i in range(1050):
+            while time.perf_counter() < nxt:
+                pass
+            nxt += period
+            t0 = time.perf_counter()
+            sb.bank.plan_raw(pk[0:6], pk[6:8], pk[8:14], U, xref, pk[14:16], K=args.K)
+            lat.append(time.perf_counter() - t0)
+        lat = np.array(lat[50:]) * 1e6
+        out["paced_plan_latency_us"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
+                                        "max": float(lat.max()), "ticks": int(lat.size), "period_us": period * 1e6,
+                                        "note": "sync_plan_latency's call, one tick per 1 ms period (busy-wait pacing)"}
         out["config5"] = concurrent_tracks(args)
     else:
         out["config5"] = concurrent_tracks_sharded(args, world, rank, sb.device)
