@@ -42,7 +42,7 @@ FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector spec
 # ONE HIP-event pair brackets the whole timed loop (stride = --steps): each event record costs
 # ~5 us of stream time (kernel trace, profiles/r03/s3_ramp: a 10.2 us gap at every group
 # boundary), so the old groups of 8 added ~1.3 us to every timed tick
-TIMING_SAMPLE = 16              # with the exchange: one plan launch in 16 bracketed alone
+TIMING_SAMPLE = 64              # with the exchange: one plan launch in 64 bracketed alone (each pair ~10 us of stream time)
 FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation (excl. transcendentals)
 # Issue roofline: instructions per rollout step of the fast look-ahead loop, per lane, by lane
 # split (tools/diag/isa_counts.py on the current sources), and the chip's fp64 VALU issue
