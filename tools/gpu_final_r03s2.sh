@@ -3,6 +3,7 @@
 # self-spawned bench, rocprofv3 kernel trace, config-3 bench, PMC passes at C=1 and C=64, and
 # the stamps diagnostics (C=1 timeline, work-queue units at C=64).
 # usage (gpurun): bash tools/gpu_final_r03s2.sh gpurun_out/<tag>
+# (the stamps diagnostics need libllampc_hip_stamps.so: `make -C lla-mpc_amd/csrc stamps` first)
 set -o pipefail
 OUT=${1:?out dir}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
