@@ -24,6 +24,8 @@
  *                                  (SURVEY.md §8e): RCCL all-gather, or xGMI mailboxes
  *  llampc_dynamics_batch           Dynamic.calc_forces_batch (llampc/models/dynamic.py:
  *                                  117-154), Dynamic._diffequation_batch (:98-115)
+ *  llampc_ctl_*                    the control loop body rt.py:278-366 on the device
+ *                                  (ConstantSpeed, selection, look-ahead, mu-hat, state)
  *  llampc_integrate_batch          Model._integrate_batch (model.py:32-40, RK4),
  *                                  Model._integrate/odeintRK6 (model.py:18-30,
  *                                  llampc/utils/rk6.py:13-28) and the NLP Euler form
@@ -41,6 +43,7 @@ extern "C" {
 #define LLAMPC_ABI_VERSION 1
 #define LLAMPC_KMAX 32          /* max top-K (rt.py:69 uses K=10) */
 #define LLAMPC_WMAX 128         /* max look-back window (rt.py:67 uses W=10) */
+#define LLAMPC_HMAX 64          /* max horizon of the controller tick (rt.py:52 uses 20) */
 
 enum llampc_status {
   LLAMPC_OK = 0,
@@ -278,6 +281,74 @@ int llampc_exchange_peer(llampc_mailbox* mb, const void* d_local, void* d_merged
 int llampc_plan_exchange(llampc_bank* bank, const llampc_plan_in* in, void* d_local, void* d_merged,
                          llampc_mailbox* mb, void* stream);
 int llampc_mailbox_destroy(llampc_mailbox* mb);
+
+/* ---- controller tick (the whole control step on the device) ------------------------- */
+/* One LLA-MPC control step of rt.py:269-366 in ONE kernel launch, the controller state kept
+ * on the device between ticks (replaces the host loop body rt.py:278-366: ConstantSpeed with
+ * mu-hat, planner.py:12-67 + track.py:147-160; the per-tick solve, nmpc.py:161-203 — here a
+ * candidate search; the look-back selection rt.py:347-366; the mu-hat estimator rt.py:326-344):
+ *   reference   ConstantSpeed(x_t, projidx, mu-hat, v_factor) once the window has been full
+ *               for a tick (rt.py:278-282), ConstantSpeed(x_t, projidx) before; the start arc
+ *               length from `prefix` (one entry per projection index, the reference's own sum);
+ *               lap wrap projidx > lap_projidx -> 0 (rt.py:287-296)
+ *   candidates  C sequences: candidate 0 = the previous chosen sequence shifted one step (or
+ *               u_{t-1} held), candidate c >= 1 adds Philox4x32-10 noise (four-word sum, unit
+ *               variance) x sigma_j, clipped to cost.umin/umax and, in order over the horizon,
+ *               to |du| <= cost.rate_max Ts (oracle/llampc_oracle.py candidates_ctl)
+ *   look-back   the transition (x_{t-1}, u_{t-1}) -> x_t from tick 2 on (rt.py:347)
+ *   look-ahead  ticks t <= W: the nominal model (nlp_initial, rt.py:300-301); afterwards the
+ *               selected model (nlp_bank[current_model_idx], rt.py:303) and the K top-K models,
+ *               every candidate, RK4 + the NLP objective (llampc_plan's look-ahead)
+ *   mu-hat      warm-up split (rt.py:326-330), then the top-K Dr / Df means (rt.py:331-344)
+ * The bank must carry a raceline (llampc_bank_set_raceline) and is driven by the controller
+ * from its creation on (its window advances with the ticks). */
+typedef struct llampc_ctl_cfg {
+  int32_t C, H, K, nan_policy;   /* candidates, horizon (<= LLAMPC_HMAX), top-K, look-back NaN */
+  double Ts;
+  double v_factor;               /* ConstantSpeed scale once mu-hat is used (rt.py:73: 0.9)  */
+  double mu_init;                /* rt.py:327 (1.0)                                          */
+  int32_t S;                     /* mu-hat smoothing window (rt.py:68: 20), <= 64            */
+  int32_t lap_projidx;           /* rt.py:287 (ETHZ 656, ETHZMobil 440)                      */
+  double sigma[2];               /* candidate noise std per input (pwm, steer)              */
+  uint64_t seed;
+  double nominal[6];             /* warm-up model (Bf, Cf, Df, Br, Cr, Dr), rt.py:207       */
+  llampc_cost cost;              /* objective, bounds and rate bound of the look-ahead       */
+  int32_t debug_inputs;          /* 1: keep each tick's xref and U (llampc_ctl_inputs)       */
+  int32_t reserved;
+} llampc_ctl_cfg;
+
+typedef struct llampc_ctl_out {
+  llampc_plan_out plan;          /* the tick record (sel_model / sel_cand: the chosen control;
+                                    la_best_*: over the rolled-out models only; -1 while warm) */
+  int64_t tick;
+  int32_t projidx;               /* planner state after this tick (lap wrap applied)         */
+  int32_t warm;                  /* 1: planned with the nominal model (tick <= W)            */
+  double mu_used, scale_used;    /* curr_mu / scale of this tick's reference                 */
+  double mu_pred;                /* mu-hat after this tick (NaN until the first update)      */
+  double dr_mean, df_mean;       /* what this tick appended to the Dr / Df histories          */
+  double u_seq[LLAMPC_HMAX][2];  /* [H][2]: the chosen control sequence; u_seq[0] is applied  */
+} llampc_ctl_out;
+
+typedef struct llampc_ctl llampc_ctl;
+/* points [2][np]: the raceline polyline project_fast projects on (track.raceline);
+ * prefix [np-1]: prefix[p] = sum of the segment lengths of points 0..p+1 (planner.py:29-36's
+ * start arc length for projection index p). */
+int llampc_ctl_create(llampc_bank* bank, const llampc_ctl_cfg* cfg, const double* points, int32_t np,
+                      const double* prefix, llampc_ctl** out);
+/* x_t [6] (host): one control step, blocking; the record comes back through pinned host memory. */
+int llampc_ctl_tick(llampc_ctl* ctl, const double* x_t, llampc_ctl_out* out);
+/* The same step enqueued (x_t copied into the launch); at most one outstanding per controller;
+ * controllers of different banks (e.g. two tracks) overlap on the device. */
+int llampc_ctl_tick_async(llampc_ctl* ctl, const double* x_t);
+int llampc_ctl_wait(llampc_ctl* ctl, llampc_ctl_out* out);
+/* ConstantSpeed (planner.py:12-67) alone on the device with the controller's tables and Ts:
+ * x0 [2], v0, horizon H (<= LLAMPC_HMAX), projidx, curr_mu, scale -> xref [2][H+1], the new
+ * projidx (no lap wrap) and vr.  Blocking; leaves the controller state alone. */
+int llampc_ctl_reference(llampc_ctl* ctl, const double* x0, double v0, int32_t H, int32_t projidx, double curr_mu,
+                         double scale, double* xref, int32_t* projidx_out, double* vr);
+/* The last tick's reference xref [2][H+1] and candidates U [C][H][2] (cfg.debug_inputs = 1). */
+int llampc_ctl_inputs(llampc_ctl* ctl, double* xref, double* U);
+int llampc_ctl_destroy(llampc_ctl* ctl);
 
 /* ---- raw batched dynamics (Dynamic API parity) ---------------------------------- */
 /* x [n][6], u [n][2]; params [6][P] with P == 1 (one model broadcast) or P == n.

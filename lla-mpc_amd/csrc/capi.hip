@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+#include "ctl.hpp"
 #include "kernels.hpp"
 #include "merge.hpp"
 
@@ -184,8 +185,7 @@ struct llampc_bank {
   uint64_t hseq = 0;
   uint64_t async_seq = 0;          // the outstanding llampc_plan_async tick's tag (0: copy path)
   int64_t launches = 0;            // plan-kernel launches enqueued on this bank (llampc_bank_launches)
-  uint64_t* d_wq = nullptr;        // work-queue unit counter (monotonic; launch_plan's WQ layout)
-  uint64_t wq_base = 0;            // the counter's value at the next launch's start
+  uint64_t* d_wq = nullptr;        // work-queue unit counter (0 between launches; launch_plan's WQ layout)
 };
 
 namespace {
@@ -438,14 +438,12 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
     lal.seq = seq;
     lal.poll = poll;
     lal.wq = b->d_wq;
-    lal.wq_base = b->wq_base;
   }
-  int64_t wq_adv = 0;
+  f.wq = b->d_wq;
   {
     TimedLaunch tl(b, 0, s);
-    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s, pk, &wq_adv));
+    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s, pk));
   }
-  b->wq_base += (uint64_t)wq_adv;        // the work-queue takes this launch makes (0: static layout)
   b->seq = seq;
   if (px) px->seq = px_seq;
   b->launches++;
@@ -669,7 +667,6 @@ int llampc_bank_reset(llampc_bank* b) {
   HIP_TRY(hipStreamSynchronize(b->stream));
   b->count = 0;
   b->slot = 0;
-  b->wq_base = 0;
   return LLAMPC_OK;
 }
 
@@ -1116,6 +1113,348 @@ int llampc_mailbox_destroy(llampc_mailbox* mb) {
   if (mb->own) (void)hipFree(mb->own);
   if (mb->d_box) (void)hipFree(mb->d_box);
   delete mb;
+  return LLAMPC_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------
+// Controller tick (ctl.hip): the control loop body rt.py:278-366 as ONE launch per step, the
+// controller state resident on the device between steps.
+// ------------------------------------------------------------------------------------
+static_assert(sizeof(llampc_ctl_cfg) == 280, "llampc_ctl_cfg layout (llampc/_native.py CtlCfg)");
+static_assert(sizeof(llampc_ctl_out) == sizeof(llampc_plan_out) + 56 + 16 * LLAMPC_HMAX, "llampc_ctl_out layout");
+
+struct llampc_ctl {
+  llampc_bank* b = nullptr;
+  llampc_ctl_cfg cfg{};
+  CtlState* d_st = nullptr;
+  double* d_pts = nullptr;               // points [2][np] | prefix [np - 1]
+  int32_t np = 0;
+  llampc_ctl_out* h_out = nullptr;       // pinned, coherent; d_out is its device alias
+  llampc_ctl_out* d_out = nullptr;
+  uint64_t* h_tag = nullptr;             // completion tag (pinned), d_tag its alias
+  uint64_t* d_tag = nullptr;
+  uint64_t hseq = 0;
+  uint64_t* d_sel_tag = nullptr;         // [kCtlSlotsMax]
+  uint64_t* d_slot_tag = nullptr;        // [kCtlSlotsMax][4]
+  unsigned* d_tickets = nullptr;         // [1]
+  double* d_dbg = nullptr;               // xref [2][H+1] | U [C][H][2] (debug_inputs)
+  uint32_t seq = 0;
+  int64_t t = 0;
+  bool pending = false;
+  uint64_t pend_seq = 0;
+  std::mutex mu;
+};
+
+extern "C" {
+
+int llampc_ctl_destroy(llampc_ctl* c) {
+  if (!c) return LLAMPC_OK;
+  {
+    DeviceGuard g(c->b ? c->b->device : 0);
+    if (c->b && c->b->stream) (void)hipStreamSynchronize(c->b->stream);
+    void* d[] = {c->d_st, c->d_pts, c->d_sel_tag, c->d_slot_tag, c->d_tickets, c->d_dbg};
+    for (void* p : d)
+      if (p) (void)hipFree(p);
+    if (c->h_out) (void)hipHostFree(c->h_out);
+    if (c->h_tag) (void)hipHostFree(c->h_tag);
+  }
+  delete c;
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_create(llampc_bank* b, const llampc_ctl_cfg* cfg, const double* points, int32_t np,
+                      const double* prefix, llampc_ctl** out) {
+  if (!out) return fail(LLAMPC_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (!b || !cfg || !points || !prefix) return fail(LLAMPC_E_ARG, "NULL argument");
+  const llampc_ctl_cfg& k = *cfg;
+  if (k.C < 1 || k.H < 1 || k.H > LLAMPC_HMAX || k.K < 1 || k.K > LLAMPC_KMAX)
+    return fail(LLAMPC_E_ARG, "C=%d H=%d (1..%d) K=%d (1..%d)", k.C, k.H, LLAMPC_HMAX, k.K, LLAMPC_KMAX);
+  if (k.S < 1 || k.S > kCtlSMax) return fail(LLAMPC_E_ARG, "S=%d outside [1, %d]", k.S, kCtlSMax);
+  if (!(k.Ts > 0) || !std::isfinite(k.Ts)) return fail(LLAMPC_E_ARG, "Ts must be finite > 0");
+  if (np < 2) return fail(LLAMPC_E_ARG, "np=%d < 2", np);
+  if (k.nan_policy != LLAMPC_NAN_FIRST && k.nan_policy != LLAMPC_NAN_IGNORE) return fail(LLAMPC_E_ARG, "nan_policy");
+  if (!b->d_rl) return fail(LLAMPC_E_STATE, "the controller needs the bank's raceline (llampc_bank_set_raceline)");
+  const int R = lookback_r(b->n, k.K);
+  const int nb_lb = lookback_blocks_r(b->n, R);
+  size_t poll_off = 0;
+  const size_t lds = ctl_lds_bytes(k.H, k.C, b->rl_n, nb_lb, k.K, &poll_off);
+  if (lds > 160 * 1024)
+    return fail(LLAMPC_E_ARG, "controller tick needs %zu B of LDS (> 160 KiB): C*H=%d too large for this track", lds,
+                k.C * k.H);
+  DeviceGuard g(b->device);
+  auto* c = new llampc_ctl();
+  c->b = b;
+  c->cfg = k;
+  c->np = np;
+  auto cleanup = [&](int code) {
+    llampc_ctl_destroy(c);
+    return code;
+  };
+  int rc;
+  if ((rc = dev_alloc(&c->d_st, 1)) || (rc = dev_alloc(&c->d_pts, 3 * (size_t)np - 1)) ||
+      (rc = dev_alloc(&c->d_sel_tag, kCtlSlotsMax)) || (rc = dev_alloc(&c->d_slot_tag, 4 * (size_t)kCtlSlotsMax)) ||
+      (rc = dev_alloc(&c->d_tickets, 1)))
+    return cleanup(rc);
+  if (k.debug_inputs && (rc = dev_alloc(&c->d_dbg, 2 * (size_t)(k.H + 1) + 2 * (size_t)k.C * k.H))) return cleanup(rc);
+  if (hipHostMalloc(reinterpret_cast<void**>(&c->h_out), sizeof(llampc_ctl_out),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_tag), 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(controller record) failed"));
+  *c->h_tag = 0;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_out), c->h_out, 0) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_tag), c->h_tag, 0) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_HIP, "hipHostGetDevicePointer(controller record) failed"));
+  CtlState st{};
+  st.mu_pred = std::nan("");
+  st.current_model = 0;                  // rt.py:264: the nominal model's index
+  if (hipMemcpy(c->d_st, &st, sizeof st, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_pts, points, 2 * (size_t)np * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_pts + 2 * (size_t)np, prefix, ((size_t)np - 1) * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->d_sel_tag, 0, kCtlSlotsMax * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->d_slot_tag, 0, 4 * kCtlSlotsMax * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->d_tickets, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return cleanup(fail(LLAMPC_E_HIP, "controller upload failed"));
+  *out = c;
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
+  if (!c || !x_t) return fail(LLAMPC_E_ARG, "controller/x_t is NULL");
+  std::lock_guard<std::mutex> lc(c->mu);
+  if (c->pending) return fail(LLAMPC_E_STATE, "a controller tick is outstanding: call llampc_ctl_wait");
+  llampc_bank* b = c->b;
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (b->async_pending) return fail(LLAMPC_E_STATE, "an async plan tick is outstanding on the bank");
+  DeviceGuard g(b->device);
+  const llampc_ctl_cfg& k = c->cfg;
+  const int64_t t = c->t;
+  const int32_t W = b->W;
+  const bool do_lb = t >= 2;             // rt.py:347 (the transition idt -> idt+1 from idt >= 1)
+  const bool warm = t <= W;              // rt.py:300-301
+  int32_t count = b->count;
+  if (do_lb) count = std::min(count + 1, W);
+  const bool full = do_lb && count >= W;
+  if (!warm && !full)
+    return fail(LLAMPC_E_STATE, "tick %lld: the look-back window is not full after the warm-up (was the bank reset?)",
+                (long long)t);
+  CtlLaunch L{};
+  const int R = lookback_r(b->n, k.K);
+  // look-back (rt.py:347-366 on the bank's ring)
+  L.lb.params = b->d_params;
+  L.lb.n = b->n;
+  L.lb.goff = b->goff;
+  L.lb.veh = b->veh;
+  L.lb.x_prev = c->d_st->x_prev;
+  L.lb.u_prev = c->d_st->u_prev;
+  L.lb.Ts = k.Ts;
+  L.lb.ring = b->d_ring;
+  L.lb.W = W;
+  L.lb.slot = b->slot;
+  L.lb.full = full;
+  L.lb.K = k.K;
+  L.lb.nan_first = k.nan_policy == LLAMPC_NAN_FIRST;
+  L.lb.R = R;
+  L.lb.wm_keep = 0;
+  L.lb.wm_buf = b->d_wmean;
+  L.lb.am_val = b->d_am_val;
+  L.lb.am_idx = b->d_am_idx;
+  L.lb.tk_val = b->d_tk_val;
+  L.lb.tk_idx = b->d_tk_idx;
+  // look-ahead constants (RK4 on the bank's vehicle, the NLP objective)
+  L.la.params = b->d_params;
+  L.la.n = b->n;
+  L.la.goff = b->goff;
+  L.la.veh = integrator_veh(b->veh, LLAMPC_RK4);
+  L.la.C = k.C;
+  L.la.H = k.H;
+  L.la.integrator = LLAMPC_RK4;
+  L.la.Ts = k.Ts;
+  L.la.cost = make_cost(k.cost, k.Ts);
+  L.la.xref_mode = LLAMPC_XREF_GIVEN;
+  {
+    const size_t m = (size_t)b->rl_n - 1;
+    L.la.rl.knots = b->d_rl;
+    L.la.rl.xy = b->d_rl + b->rl_n;
+    L.la.rl.speed = L.la.rl.xy + 8 * m;
+    L.la.rl.mus = L.la.rl.speed + 4 * m * b->rl_M;
+    L.la.rl.n = b->rl_n;
+    L.la.rl.M = b->rl_M;
+    L.la.rl.hmin = b->rl_hmin;
+    L.la.rl.vmax = b->rl_vmax;
+    L.la.rl.wcap = b->rl_n - 1;
+  }
+  // lb_final's view
+  L.fin.out = &c->d_out->plan;
+  L.fin.do_lb = do_lb;
+  L.fin.do_la = 1;
+  L.fin.full = full;
+  L.fin.window_count = do_lb ? count : b->count;
+  L.fin.K = k.K;
+  L.fin.nan_first = k.nan_policy == LLAMPC_NAN_FIRST;
+  L.fin.nb_lb = do_lb ? lookback_blocks_r(b->n, R) : 1;
+  L.fin.C = k.C;
+  L.fin.n = b->n;
+  L.fin.goff = b->goff;
+  L.fin.params = b->d_params;
+  L.fin.am_val = b->d_am_val;
+  L.fin.am_idx = b->d_am_idx;
+  L.fin.tk_val = b->d_tk_val;
+  L.fin.tk_idx = b->d_tk_idx;
+  // controller
+  const uint64_t hs = c->hseq + 1;
+  const uint32_t seq = next_seq(c->seq);
+  L.st = c->d_st;
+  L.out = c->d_out;
+  L.host_tag = c->d_tag;
+  L.host_seq = hs;
+  L.sel_tag = c->d_sel_tag;
+  L.slot_tag = c->d_slot_tag;
+  L.tickets = c->d_tickets;
+  L.dbg = c->d_dbg;
+  L.pts = c->d_pts;
+  L.prefix = c->d_pts + 2 * (size_t)c->np;
+  L.tick = (uint64_t)t;
+  L.seed = k.seed;
+  for (int j = 0; j < 6; ++j) {
+    L.x_t[j] = x_t[j];
+    L.nominal[j] = k.nominal[j];
+  }
+  const double sqrt3 = std::sqrt(3.0);
+  for (int j = 0; j < 2; ++j) {
+    L.nscale[j] = sqrt3 * k.sigma[j];    // sqrt(3) sigma_j, one rounding (ctl.hpp ctl_cand_raw)
+    L.rate[j] = k.cost.rate_max[j] < 0 ? -1.0 : k.cost.rate_max[j] * k.Ts;
+    L.umin[j] = k.cost.umin[j];
+    L.umax[j] = k.cost.umax[j];
+  }
+  L.mu_fixed = 1.0;                      // ConstantSpeed's defaults (rt.py:282)
+  L.scale_fixed = 1.0;
+  L.v_factor = k.v_factor;
+  L.mu_init = k.mu_init;
+  L.seq = seq;
+  {
+    const uint64_t units = (poll_bound_ticks(b->n, k.C, k.H) + 0xFFFF) >> 16;
+    L.poll = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(units, 1), UINT32_MAX);
+  }
+  L.np = c->np;
+  L.lap_projidx = k.lap_projidx;
+  L.do_lb = do_lb;
+  L.warm = warm;
+  L.use_mu = t > W + 1;                  // rt.py:278
+  L.full = full;
+  L.nslots = warm ? 1 : k.K + 1;
+  L.G = lookahead_group(k.C);
+  L.cpl = (k.C + L.G - 1) / L.G;
+  const int lpm = 4 * L.G <= kBlock ? 4 : (2 * L.G <= kBlock ? 2 : 1);
+  L.mpb = kBlock / (L.G * lpm);
+  L.S = k.S;
+  L.K = k.K;
+  L.nb_lb = L.fin.nb_lb;
+  L.nb_la = (L.nslots + L.mpb - 1) / L.mpb;
+  size_t lds = ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &L.poll_off);
+  lds = std::max<size_t>(lds, 82 * 1024); // one block per CU, as the plan launch (sc1 hand-offs)
+  {
+    TimedLaunch tl(b, 0, b->stream);
+    HIP_TRY(launch_ctl(L, lpm, lds, b->stream));
+  }
+  c->hseq = hs;
+  c->seq = seq;
+  c->t = t + 1;
+  c->pending = true;
+  c->pend_seq = hs;
+  b->launches++;
+  if (do_lb) {
+    b->slot = (b->slot + 1) % W;
+    b->count = count;
+  }
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
+  if (!c || !out) return fail(LLAMPC_E_ARG, "controller/out is NULL");
+  std::lock_guard<std::mutex> lc(c->mu);
+  if (!c->pending) return fail(LLAMPC_E_STATE, "no controller tick outstanding");
+  c->pending = false;
+  DeviceGuard g(c->b->device);
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t spins = 0;
+  while (__atomic_load_n(c->h_tag, __ATOMIC_ACQUIRE) != c->pend_seq) {
+    __builtin_ia32_pause();
+    if ((++spins & 0xFFF) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      HIP_TRY(hipStreamSynchronize(c->b->stream));
+      if (__atomic_load_n(c->h_tag, __ATOMIC_ACQUIRE) == c->pend_seq) break;
+      return fail(LLAMPC_E_DEVICE, "controller tick %llu: completion tag never arrived", (unsigned long long)c->pend_seq);
+    }
+  }
+  std::memcpy(out, const_cast<const llampc_ctl_out*>(c->h_out), sizeof(llampc_ctl_out));
+  if (out->plan.status)
+    return fail(LLAMPC_E_DEVICE, "controller tick record status %d (an in-launch wait timed out)", out->plan.status);
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_tick(llampc_ctl* c, const double* x_t, llampc_ctl_out* out) {
+  if (!out) return fail(LLAMPC_E_ARG, "out is NULL");
+  int rc = llampc_ctl_tick_async(c, x_t);
+  return rc ? rc : llampc_ctl_wait(c, out);
+}
+
+int llampc_ctl_reference(llampc_ctl* c, const double* x0, double v0, int32_t H, int32_t projidx, double curr_mu,
+                         double scale, double* xref, int32_t* projidx_out, double* vr) {
+  if (!c || !x0 || !xref) return fail(LLAMPC_E_ARG, "NULL argument");
+  if (H < 1 || H > LLAMPC_HMAX) return fail(LLAMPC_E_ARG, "H=%d outside [1, %d]", H, LLAMPC_HMAX);
+  if (projidx < 0 || projidx > c->np - 2) return fail(LLAMPC_E_ARG, "projidx=%d outside [0, %d]", projidx, c->np - 2);
+  std::lock_guard<std::mutex> lc(c->mu);
+  llampc_bank* b = c->b;
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  const size_t n = 2 * (size_t)(H + 1) + 2;
+  double* d = nullptr;
+  if (int rc = dev_alloc(&d, n)) return rc;
+  CsLaunch a{};
+  const size_t m = (size_t)b->rl_n - 1;
+  a.rl.knots = b->d_rl;
+  a.rl.xy = b->d_rl + b->rl_n;
+  a.rl.speed = a.rl.xy + 8 * m;
+  a.rl.mus = a.rl.speed + 4 * m * b->rl_M;
+  a.rl.n = b->rl_n;
+  a.rl.M = b->rl_M;
+  a.rl.hmin = b->rl_hmin;
+  a.rl.vmax = b->rl_vmax;
+  a.pts = c->d_pts;
+  a.prefix = c->d_pts + 2 * (size_t)c->np;
+  a.out = d;
+  a.x0 = x0[0];
+  a.y0 = x0[1];
+  a.v0 = v0;
+  a.mu = curr_mu;
+  a.scale = scale;
+  a.Ts = c->cfg.Ts;
+  a.np = c->np;
+  a.p0 = projidx;
+  a.H = H;
+  std::vector<double> h(n);
+  hipError_t e = launch_constant_speed(a, b->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d, n * sizeof(double), hipMemcpyDeviceToHost, b->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(b->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(LLAMPC_E_HIP, "llampc_ctl_reference: %s", hipGetErrorString(e));
+  std::memcpy(xref, h.data(), 2 * (size_t)(H + 1) * sizeof(double));
+  if (projidx_out) *projidx_out = (int32_t)h[2 * (H + 1)];
+  if (vr) *vr = h[2 * (H + 1) + 1];
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_inputs(llampc_ctl* c, double* xref, double* U) {
+  if (!c || !xref || !U) return fail(LLAMPC_E_ARG, "NULL argument");
+  if (!c->d_dbg) return fail(LLAMPC_E_STATE, "controller created without debug_inputs");
+  std::lock_guard<std::mutex> lc(c->mu);
+  DeviceGuard g(c->b->device);
+  HIP_TRY(hipStreamSynchronize(c->b->stream));
+  const size_t nx = 2 * (size_t)(c->cfg.H + 1), nu = 2 * (size_t)c->cfg.C * c->cfg.H;
+  HIP_TRY(hipMemcpy(xref, c->d_dbg, nx * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(U, c->d_dbg + nx, nu * sizeof(double), hipMemcpyDeviceToHost));
   return LLAMPC_OK;
 }
 

@@ -1,0 +1,603 @@
+// ctl.hip — the controller tick: one launch per LLA-MPC control step (ctl.hpp has the map to
+// the reference).  Roles by block index (look-back blocks first in dispatch order):
+//
+//   look-back blocks [0, nb_lb)   the plan launch's look-back (lookback_block: RK4 step of
+//                                 every model from the state's (x_{t-1}, u_{t-1}), error, ring,
+//                                 window mean, wave/block top-K lists); the last one (ticket)
+//                                 merges them (lb_final<SEL>), PUBLISHES the selection
+//                                 (top-K + argmin, tagged words) and completes the tick
+//                                 (ctl_complete).  Without a look-back (ticks 0, 1) block 0
+//                                 only completes.
+//   look-ahead blocks [nb_lb, ..) each: the raceline tables to LDS; the projection of x_t and
+//                                 ConstantSpeed with mu-hat (one lane walks, planner.py:
+//                                 24-65); the C candidates (Philox, every lane); then it WAITS
+//                                 for the selection (or, while the window fills, takes the
+//                                 nominal model) and rolls out its slots' models x C candidates
+//                                 (the plan kernel's fused RK4 rollout, candidates read from
+//                                 LDS) and publishes each slot's best candidate.
+//
+// Waiting: a look-ahead block waits only for the look-back ticket winner, a block of LOWER
+// index; workgroups are dispatched in index order (per XCD), so that block has been dispatched
+// and never waits on a look-ahead block before it publishes (the selection comes before its
+// own poll).  The completion waits only for look-ahead blocks, which then never wait again.
+// Every wait has a bound (status LLAMPC_STATUS_POLL_TIMEOUT, never expected).
+#include "plan_dev.hpp"
+#include "ctl.hpp"
+
+namespace llampc {
+
+// LDS layout of the controller launch (byte offsets; 16-B aligned regions).  Look-ahead
+// blocks: xref [H+1][2] | U [C][H][2] | knots [n + pad] | x/y rows [2][4][n-1] | the two
+// bracketing speed profiles [2][4][n-1] | misc.  The completing block: lb_final's region from
+// kScratchBytes, then its own area at poll_off (CtlPollLds).
+struct CtlLds {
+  size_t sx, ul, kn, xy, spd, misc, end;
+};
+__host__ __device__ __forceinline__ size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n) {
+  CtlLds L;
+  size_t o = kScratchBytes;
+  L.sx = o;
+  o = align16(o + 16 * (size_t)(H + 1));
+  L.ul = o;
+  o = align16(o + 16 * (size_t)C * H);
+  L.kn = o;
+  o = align16(o + 8 * (size_t)(n + kKnotPad));
+  L.xy = o;
+  o = align16(o + 64 * (size_t)(n - 1));
+  L.spd = o;
+  o = align16(o + 64 * (size_t)(n - 1));
+  L.misc = o;
+  L.end = o + 1024;
+  return L;
+}
+constexpr size_t kCtlPollBytes = 4096;   // ctl_complete's area (layout there)
+
+namespace {
+
+__device__ __forceinline__ bool ctl_late(uint64_t t0, uint32_t poll) {
+  return __builtin_amdgcn_s_memrealtime() - t0 > ((uint64_t)poll << 16);
+}
+
+// ------------------------------------------------------------------------------------
+// The completing block (after lb_final<true>, or alone on ticks without a look-back).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* smem, const CtlSel& cs) {
+#pragma clang fp contract(off)
+  const int tid = threadIdx.x;
+  const int H = c.la.H, C = c.la.C;
+  unsigned char* pl = smem + c.poll_off;
+  double* pdist = reinterpret_cast<double*>(pl);                  // [16]
+  double* pcost = reinterpret_cast<double*>(pl + 128);            // [kCtlSlotsMax]
+  int32_t* pcand = reinterpret_cast<int32_t*>(pl + 448);          // [kCtlSlotsMax]
+  int32_t* pnf = reinterpret_cast<int32_t*>(pl + 608);            // [kCtlSlotsMax]
+  double* praw = reinterpret_cast<double*>(pl + 768);             // [HMAX][2]
+  int32_t* pmisc = reinterpret_cast<int32_t*>(pl + 1792);         // sel_cand, pj, late
+  unsigned char* late_w = smem + kLateOff;
+  CtlState* st = c.st;
+  const int p0 = st->projidx;
+  const int segs = ctl_segments(p0, c.np);
+  if (tid < kCtlSegs && tid < segs)                                // track.py:155-157
+    pdist[tid] = ref_project_dist(c.x_t[0], c.x_t[1], c.pts[p0 + tid], c.pts[c.np + p0 + tid],
+                                  c.pts[p0 + tid + 1], c.pts[c.np + p0 + tid + 1]);
+  // every slot's result (tagged words of the look-ahead blocks)
+  int late = 0;
+  if (tid < c.nslots) {
+    uint64_t w[4];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = ld_wt(&c.slot_tag[4 * tid + q]);
+      if ((int)tag_ok(w[0], c.seq) & (int)tag_ok(w[1], c.seq) & (int)tag_ok(w[2], c.seq) & (int)tag_ok(w[3], c.seq))
+        break;
+      if (ctl_late(t0, c.poll)) {
+        late = 1;
+        break;
+      }
+    }
+    const uint32_t nfw = (uint32_t)w[3];
+    late |= (int)(nfw >> 31);
+    pcost[tid] = late ? __builtin_nan("") : __longlong_as_double((long long)join_words(w[0], w[1]));
+    pcand[tid] = late ? -1 : (int32_t)(uint32_t)w[2];
+    pnf[tid] = late ? 0 : (int32_t)(nfw & 0x7FFFFFFFu);
+  }
+  const int wl = __any(late);
+  if ((tid & 63) == 0) late_w[tid >> 6] = (unsigned char)wl;
+  __syncthreads();
+  if (tid == 0) {
+    const int ss = c.warm ? 0 : c.K;                               // the selected model's slot
+    pmisc[0] = pcand[ss];
+    pmisc[1] = segs >= 1 ? p0 + np_argmin(pdist, segs) : p0;       // planner.py:26-27
+    int anyl = 0;
+    for (int w = 0; w < kWaves; ++w) anyl |= late_w[w];
+    pmisc[2] = anyl;
+  }
+  __syncthreads();
+  // the chosen sequence: candidate sel_cand regenerated (the look-ahead blocks' generator)
+  const int scand = pmisc[0] >= 0 ? pmisc[0] : 0;
+  const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
+  const double up0 = st->u_prev[0], up1 = st->u_prev[1];
+  const double mu_used = c.use_mu ? ld_wt(&st->mu_pred) : c.mu_fixed;   // before the update below
+  if (tid < 2 * H) {
+    const int j = tid & 1;
+    praw[tid] = ctl_cand_raw(scand, tid >> 1, j, H, prev_seq, j ? up1 : up0, j ? c.nscale[1] : c.nscale[0],
+                             j ? c.umin[1] : c.umin[0], j ? c.umax[1] : c.umax[0], c.tick, c.seed, 0);
+  }
+  __syncthreads();
+  if (tid < 2) ctl_rate_chain(praw + tid, H, tid ? up1 : up0, tid ? c.rate[1] : c.rate[0]);
+  __syncthreads();
+  // the record
+  llampc_ctl_out* o = c.out;
+  llampc_plan_out* po = &o->plan;
+  const double nan = __builtin_nan("");
+  const bool warm = c.warm != 0;
+  if (tid < LLAMPC_KMAX) {
+    const int k = tid;
+    const bool have = !warm && k < c.K;
+    if (warm) {                         // no look-back selection yet (lb_final did not run)
+      po->topk[k] = -1;
+      po->topk_val[k] = po->topk_Df[k] = po->topk_Dr[k] = nan;
+    }
+    po->topk_cand[k] = have ? pcand[k] : -1;
+    po->topk_cost[k] = have ? pcost[k] : nan;
+  }
+  if (tid < 2 * H) {
+    const double v = praw[tid];
+    (&o->u_seq[0][0])[tid] = v;
+    (&st->useq[0][0])[tid] = v;
+  }
+  if (tid < 6) st->x_prev[tid] = c.x_t[tid];
+  if (tid < 2) st->u_prev[tid] = praw[tid];
+  if (tid == 0) {
+    const int ss = warm ? 0 : c.K;
+    const int64_t sel = warm ? st->current_model : c.fin.goff + (int64_t)cs.ids[c.K];
+    // look-ahead best over the rolled-out slots (flattened (model, candidate) order)
+    double lav = nan;
+    int64_t lai = kNoIndex;
+    int nf = 0;
+    for (int s = 0; s < c.nslots; ++s) {
+      nf += pnf[s];
+      if (warm || pcand[s] < 0 || cs.ids[s] == kNoLocal) continue;
+      const int64_t key = (c.fin.goff + (int64_t)cs.ids[s]) * C + pcand[s];
+      if (less_bf<0>(pcost[s], key, lav, lai)) {
+        lav = pcost[s];
+        lai = key;
+      }
+    }
+    po->window_count = c.fin.window_count;
+    po->window_full = c.fin.full;
+    po->K = c.K;
+    po->sel_owned = 1;
+    if (warm) {
+      po->lb_best = -1;
+      po->lb_best_val = nan;
+    }
+    po->sel_model = sel;
+    po->sel_cand = pcand[ss];
+    po->sel_cost = pcost[ss];
+    po->n_nonfinite = nf;
+    po->la_best_model = lai == kNoIndex ? -1 : lai / C;
+    po->la_best_cand = lai == kNoIndex ? -1 : (int32_t)(lai % C);
+    po->la_best_cost = lai == kNoIndex ? nan : lav;
+    po->status = pmisc[2] ? kPollTimeoutStatus : 0;
+    // mu-hat (rt.py:326-344): the warm-up split with g = 9.8, else the top-K means
+    const double mass = c.la.veh.mass, lf = c.la.veh.lf, lr = c.la.veh.lr;
+    double dr, df;
+    if (warm) {
+      dr = c.mu_init * mass * 9.8 * lr / (lf + lr);
+      df = c.mu_init * mass * 9.8 * lf / (lf + lr);
+    } else {
+      int kk = 0;
+      while (kk < c.K && cs.ids[kk] != kNoLocal) ++kk;
+      dr = np_pairwise_ring(cs.dr, 0, kk, LLAMPC_KMAX) / kk;
+      df = np_pairwise_ring(cs.df, 0, kk, LLAMPC_KMAX) / kk;
+    }
+    const int cnt = st->hist_count;
+    const int S = c.S;
+    st->dr_hist[cnt % S] = dr;
+    st->df_hist[cnt % S] = df;
+    const int tot = cnt + 1, nl = tot < S ? tot : S, first = (tot - nl) % S;
+    double mu_pred = st->mu_pred;
+    if (!warm)                                                     // rt.py:341
+      mu_pred = (np_pairwise_ring(st->dr_hist, first, nl, S) / nl + np_pairwise_ring(st->df_hist, first, nl, S) / nl) /
+                (9.81 * mass);
+    st->hist_count = tot;
+    st->mu_pred = mu_pred;
+    int pj = pmisc[1];
+    if (pj > c.lap_projidx) pj = 0;                                // rt.py:287-296
+    st->projidx = pj;
+    st->has_seq = 1;
+    if (!warm) st->current_model = sel;
+    o->tick = (int64_t)c.tick;
+    o->projidx = pj;
+    o->warm = c.warm;
+    o->mu_used = mu_used;
+    o->scale_used = c.use_mu ? c.v_factor : c.scale_fixed;
+    o->mu_pred = mu_pred;
+    o->dr_mean = dr;
+    o->df_mean = df;
+    __hip_atomic_store(&c.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(c.host_tag, c.host_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ------------------------------------------------------------------------------------
+// The device ConstantSpeed (planner.py:12-67), shared by the controller's look-ahead blocks
+// and llampc_ctl_reference: tables -> LDS, the projection, one lane's walk.
+// ------------------------------------------------------------------------------------
+// knots (+inf pad, RaceRef::step), x/y rows [2][4][n-1], the two speed profiles bracketing mu
+// as rows [2][4][n-1] (the walker's whole-lap window)
+__device__ __forceinline__ void cs_stage(const RacelineK& rl, const MuBracket& br, double* kn, double* xy, double* spd) {
+  const int nseg = rl.n - 1;
+  copy_lds<4>(kn, rl.n, [&](int e) { return rl.knots[e]; });
+  copy_lds<24>(xy, 8 * nseg, [&](int e) { return rl.xy[e]; });
+  const int q = 4 * nseg;
+  const double* slo = rl.speed + (size_t)br.lo * q;
+  const double* shi = rl.speed + (size_t)br.hi * q;
+  copy_lds<24>(spd, 2 * q, [&](int e) { return e < q ? slo[e] : shi[e - q]; });
+  if ((int)threadIdx.x < kKnotPad) kn[rl.n + threadIdx.x] = __builtin_inf();
+}
+
+// project_fast of (px, py) on points[:, p0 : p0 + 10] (track.py:147-160): threads < segs
+// write their segment's distance; returns the segment count
+__device__ __forceinline__ int cs_project(const double* pts, int np_, int p0, double px, double py, double* dist) {
+  const int segs = ctl_segments(p0, np_);
+  const int tid = threadIdx.x;
+  if (tid < kCtlSegs && tid < segs)
+    dist[tid] = ref_project_dist(px, py, pts[p0 + tid], pts[np_ + p0 + tid], pts[p0 + tid + 1], pts[np_ + p0 + tid + 1]);
+  return segs;
+}
+
+// One lane: projidx = p0 + argmin (planner.py:26-27), the start arc length from the prefix
+// table (:29-36), then H steps of :40-62 into sx [H+1][2]; returns projidx, vr (:63-64).
+__device__ __forceinline__ int cs_walk(const RacelineK& rl, const double* kn, const double* xy, const double* spd,
+                                       const double* prefix, const double* dist, int segs, int p0, double px,
+                                       double py, double v0, double mu, double scale, double Ts, int H, double* sx,
+                                       double* vr) {
+  const int pj = segs >= 1 ? p0 + np_argmin(dist, segs) : p0;
+  RaceRef rr;
+  rr.init(rl, kn, rl.mus, mu, prefix[pj], v0, scale, Ts, -1);
+  rr.lo = 0;                            // the LDS window holds the bracketing profiles as rows 0, 1
+  rr.hi = rr.single ? 0 : 1;
+  const SpeedWin sw{spd, 0, rl.n - 1};
+  sx[0] = px;                           // planner.py:33 xref[:, 0] = x0
+  sx[1] = py;
+  for (int k = 0; k < H; ++k) {
+    double xr, yr;
+    rr.step(rl, kn, xy, sw, xr, yr);
+    sx[2 * (k + 1)] = xr;
+    sx[2 * (k + 1) + 1] = yr;
+    if (k == 0) *vr = rr.v * scale;
+  }
+  return pj;
+}
+
+// ------------------------------------------------------------------------------------
+// A look-ahead block: the tick's reference and candidates (redundantly per block: they only
+// read the state and the tables), then its slots' rollouts.
+// ------------------------------------------------------------------------------------
+template <int LPM>
+__device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsigned char* smem, const Scratch& sc) {
+  const int tid = threadIdx.x;
+  const int H = c.la.H, C = c.la.C;
+  const RacelineK rl = c.la.rl;
+  const int nseg = rl.n - 1;
+  const CtlLds L = ctl_lds(H, C, rl.n);
+  double* sx = reinterpret_cast<double*>(smem + L.sx);
+  double* Ul = reinterpret_cast<double*>(smem + L.ul);
+  double* kn = reinterpret_cast<double*>(smem + L.kn);
+  double* xy = reinterpret_cast<double*>(smem + L.xy);
+  double* spd = reinterpret_cast<double*>(smem + L.spd);
+  double* dist = reinterpret_cast<double*>(smem + L.misc);              // [16]
+  uint32_t* slot_id = reinterpret_cast<uint32_t*>(smem + L.misc + 128);   // [mpb] (<= 64)
+  int32_t* sel_late = reinterpret_cast<int32_t*>(smem + L.misc + 384);    // [mpb]
+  double* x0 = reinterpret_cast<double*>(smem + L.misc + 640);            // [6] x_t (no kernarg address taken)
+  if (tid < 6) x0[tid] = c.x_t[0 + tid];
+  const CtlState* st = c.st;
+  const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
+  const int p0 = st->projidx;
+  // rt.py:278-282 (mu-hat read as an atomic load: a select between it and the kernel argument
+  // would be folded into a select of their addresses, which keeps the argument in scratch)
+  const double mu = c.use_mu ? ld_wt(&st->mu_pred) : c.mu_fixed;
+  const double scale = c.use_mu ? c.v_factor : c.scale_fixed;
+  const MuBracket br = mu_bracket(rl.mus, rl.M, mu);
+  // (a) tables: knots, x/y rows, the two speed profiles bracketing mu (cs_stage)
+  cs_stage(rl, br, kn, xy, spd);
+  // (b) project_fast of x_t on raceline[:, p0 : p0 + 10] (track.py:147-160)
+  const int segs = cs_project(c.pts, c.np, p0, c.x_t[0], c.x_t[1], dist);
+  // (c) the candidates before the rate clip, every (c, k, j)
+  {
+    const double up0 = st->u_prev[0], up1 = st->u_prev[1];
+    for (int e = tid; e < 2 * C * H; e += kBlock) {
+      const int cc = e / (2 * H), r = e - cc * 2 * H, j = r & 1;
+      Ul[e] = ctl_cand_raw(cc, r >> 1, j, H, prev_seq, j ? up1 : up0, j ? c.nscale[1] : c.nscale[0],
+                           j ? c.umin[1] : c.umin[0], j ? c.umax[1] : c.umax[0], c.tick, c.seed, 0);
+    }
+  }
+  __syncthreads();
+  // (d) lane 0 walks ConstantSpeed from the projection (planner.py:24-65); waves 1-3 run the
+  //     candidates' rate-clip chains meanwhile
+  if (tid == 0) {
+    double vr;
+    (void)cs_walk(rl, kn, xy, spd, c.prefix, dist, segs, p0, c.x_t[0], c.x_t[1], c.x_t[3], mu, scale, c.la.Ts, H, sx,
+                  &vr);
+  } else if (tid >= 64) {
+    for (int t = tid - 64; t < 2 * C; t += kBlock - 64) {
+      const int j = t & 1;
+      ctl_rate_chain(Ul + 2 * (size_t)(t >> 1) * H + j, H, st->u_prev[j], j ? c.rate[1] : c.rate[0]);
+    }
+  }
+  __syncthreads();
+  if (c.dbg && blk == 0) {              // tests: this tick's reference and candidates
+    for (int e = tid; e < 2 * (H + 1); e += kBlock) {
+      const int row = e / (H + 1), k = e - row * (H + 1);
+      c.dbg[e] = sx[2 * k + row];
+    }
+    for (int e = tid; e < 2 * C * H; e += kBlock) c.dbg[2 * (H + 1) + e] = Ul[e];
+  }
+  // (e) this block's slots: the selection (tagged words of the look-back ticket winner), or
+  //     the nominal model while the window fills
+  const int mpb = c.mpb;
+  if (tid < mpb) {
+    const int slot = blk * mpb + tid;
+    uint32_t id = kNoLocal;
+    int late = 0;
+    if (slot < c.nslots) {
+      if (c.warm) {
+        id = 0;
+      } else {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          const uint64_t w = ld_wt(&c.sel_tag[slot]);
+          if (tag_ok(w, c.seq)) {
+            id = (uint32_t)w;
+            break;
+          }
+          if (ctl_late(t0, c.poll)) {
+            late = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+    slot_id[tid] = id;
+    sel_late[tid] = late;
+  }
+  __syncthreads();
+  // (f) rollouts: lane layout of the plan kernel's look-ahead (G candidate lanes per model,
+  //     LPM lanes per rollout)
+  const int G = c.G, cpl = c.cpl;
+  const int sub = tid % LPM, cl = tid / LPM, g = cl & (G - 1), si = cl / G;
+  const int slot = blk * mpb + si;
+  const uint32_t id = si < mpb ? slot_id[si] : kNoLocal;
+  const bool live = slot < c.nslots && id != kNoLocal;
+  Tire t{};
+  if (live) {
+    if (c.warm) {
+      t.Bf = c.nominal[0];
+      t.Cf = c.nominal[1];
+      t.Df = c.nominal[2];
+      t.Br = c.nominal[3];
+      t.Cr = c.nominal[4];
+      t.Dr = c.nominal[5];
+    } else {
+      t = load_tire(c.la.params, c.la.n, id);
+    }
+  }
+  CostK q = c.la.cost;
+  VehK veh = c.la.veh;
+  double Ts = c.la.Ts;
+  for (int m = 0; m < 4; ++m) {
+    pin_vgpr(q.Q[m]);
+    pin_vgpr(q.R[m]);
+    pin_vgpr(q.P[m]);
+  }
+  for (int m = 0; m < 2; ++m) {
+    pin_vgpr(q.umin[m]);
+    pin_vgpr(q.umax[m]);
+    pin_vgpr(q.dmax[m]);
+  }
+  pin_vgpr(veh.lf);
+  pin_vgpr(veh.lr);
+  pin_vgpr(veh.mass);
+  pin_vgpr(veh.inv_mass);
+  pin_vgpr(veh.inv_Iz);
+  pin_vgpr(veh.Cm1);
+  pin_vgpr(veh.Cm2);
+  pin_vgpr(veh.Cr0);
+  pin_vgpr(veh.Cr2);
+  pin_vgpr(Ts);
+  const double up0 = st->u_prev[0], up1 = st->u_prev[1];
+  double bv = __builtin_nan("");
+  int64_t bc = kNoIndex;
+  int nf = 0;
+  constexpr bool kSplit = (LPM == 4);
+  const bool diagQP = c.la.cost.Q[1] == 0.0 && c.la.cost.Q[2] == 0.0 && c.la.cost.P[1] == 0.0 && c.la.cost.P[2] == 0.0;
+  if (live) {
+    constexpr bool kScaled = scaled_yaw(LPM);
+    StageK sk = make_stage<LPM>(veh, t, sub, Ts);
+    if (kScaled) sk.ch[0].lw = sk.ch[0].lw / Ts;
+    if (kScaled && LPM == 1) sk.ch[1].lw = sk.ch[1].lw / Ts;
+    if (kScaled && LPM == 4 && sub >= 2) {   // lanes 2/3: zero-operand chains (plan kernel)
+      sk.ch[0].lw = 0.0;
+      sk.ch[0].sg = 0.0;
+      sk.ch[0].B = 0.0;
+      sk.ch[0].nsB = 0.0;
+    }
+    const FusedK fq = make_fused(veh, sk, Ts, kScaled);
+    const fm::FmK K = fm::FmK::load<kLeanLA>();
+    for (int j = 0; j < cpl; ++j) {
+      const int cc = g + j * G;
+      if (cc >= C) break;
+      bool bad = false;
+      double J;
+      if (kSplit && diagQP)
+        J = rollout<0, false, LPM, 0, true, kSplit, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts, up0, up1, K,
+                                                         fq, bad);
+      else
+        J = rollout<0, false, LPM, 0, true, false, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts, up0, up1, K,
+                                                        fq, bad);
+      if (LPM == 2) {
+        const int bi = bad;
+        bad = __builtin_amdgcn_mov_dpp(bi, kPair0, 0xF, 0xF, false) | __builtin_amdgcn_mov_dpp(bi, kPair1, 0xF, 0xF, false);
+      } else if (LPM == 4) {
+        int bi = bad;
+        bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX1, 0xF, 0xF, false);
+        bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX2, 0xF, 0xF, false);
+        bad = bi;
+      }
+      if (__builtin_expect(__any(bad), 0)) {
+        bool unused = false;
+        if (bad)
+          J = rollout<0, false, LPM, 0, false, false, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts, up0, up1, K,
+                                                           fq, unused);
+      }
+      if (sub == 0) nf += !isfinite(J);
+      if (less_nan_last(J, cc, bv, bc)) {
+        bv = J;
+        bc = cc;
+      }
+    }
+  }
+  // (g) per-slot argmin over its candidates and non-finite count: xor shuffles inside a wave,
+  //     then across the slot's waves in LDS (a slot of 2 or 4 waves: G LPM in {128, 256})
+  const int span = G * LPM;
+  for (int off = (span < 64 ? span : 64) >> 1; off >= LPM; off >>= 1) {
+    const double ov = __shfl_xor(bv, off, 64);
+    const int64_t oc = __shfl_xor(bc, off, 64);
+    nf += __shfl_xor(nf, off, 64);
+    if (less_nan_last(ov, oc, bv, bc)) {
+      bv = ov;
+      bc = oc;
+    }
+  }
+  if (span > 64) {                      // block-uniform
+    if ((tid & 63) == 0) {
+      sc.sv[tid >> 6] = bv;
+      sc.si[tid >> 6] = bc;
+      sc.sn[tid >> 6] = nf;
+    }
+    __syncthreads();
+    const int w0 = (tid / span) * (span / 64);
+    bv = sc.sv[w0];
+    bc = sc.si[w0];
+    nf = sc.sn[w0];
+    for (int k = 1; k < span / 64; ++k) {
+      nf += sc.sn[w0 + k];
+      if (less_nan_last(sc.sv[w0 + k], sc.si[w0 + k], bv, bc)) {
+        bv = sc.sv[w0 + k];
+        bc = sc.si[w0 + k];
+      }
+    }
+  }
+  // (h) publish: cost (hi, lo), candidate, non-finite count | late << 31 (tagged words)
+  if (g == 0 && sub == 0 && si < mpb && slot < c.nslots) {
+    const uint64_t vb = (uint64_t)__double_as_longlong(bv);
+    const uint32_t nfw = (uint32_t)nf | ((uint32_t)sel_late[si] << 31);
+    uint64_t* w = c.slot_tag + 4 * (size_t)slot;
+    st_wt(&w[0], tag_word(c.seq, (uint32_t)(vb >> 32)));
+    st_wt(&w[1], tag_word(c.seq, (uint32_t)vb));
+    st_wt(&w[2], tag_word(c.seq, (uint32_t)(int32_t)bc));
+    st_wt(&w[3], tag_word(c.seq, nfw));
+  }
+}
+
+}  // namespace
+
+template <int LPM>
+__global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Scratch sc(smem);
+  int* flag = reinterpret_cast<int*>(smem + kFlagOff);
+  const int blk = (int)blockIdx.x;
+  if (blk >= c.nb_lb) {
+    ctl_lookahead<LPM>(c, blk - c.nb_lb, smem, sc);
+    return;
+  }
+  unsigned char* pl = smem + c.poll_off;
+  CtlSel cs{c.sel_tag, c.seq, reinterpret_cast<uint32_t*>(pl + 2048), reinterpret_cast<double*>(pl + 2304),
+            reinterpret_cast<double*>(pl + 2624)};
+  if (c.do_lb) {
+    // x_now: this tick's x_t through LDS (pointing into the kernel argument itself would make
+    // the compiler copy the whole argument to scratch)
+    double* xl = reinterpret_cast<double*>(pl + 3072);
+    if (threadIdx.x < 6) xl[threadIdx.x] = c.x_t[0 + threadIdx.x];
+    __syncthreads();
+    LookbackLaunch lb = c.lb;           // x_prev / u_prev: the state
+    lb.x_now = xl;
+    lookback_block(lb, blk, sc);
+    if (!ticket_last(&c.tickets[0], (unsigned)c.nb_lb, flag)) return;
+    if (c.full) {
+      lb_final<true>(c.fin, smem, &cs);
+      __threadfence_system();           // the record's look-back half (pinned host memory)
+    }
+    __syncthreads();
+  }
+  ctl_complete(c, smem, cs);
+}
+
+// llampc_ctl_reference: ConstantSpeed alone (one block), into out = xref [2][H+1], projidx,
+// vr.  LDS: xref | knots | x/y | two profiles | dists (the controller's layout with C = 0).
+__global__ __launch_bounds__(kBlock) void cs_kernel(CsLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const CtlLds L = ctl_lds(a.H, 0, a.rl.n);
+  double* sx = reinterpret_cast<double*>(smem + L.sx);
+  double* kn = reinterpret_cast<double*>(smem + L.kn);
+  double* xy = reinterpret_cast<double*>(smem + L.xy);
+  double* spd = reinterpret_cast<double*>(smem + L.spd);
+  double* dist = reinterpret_cast<double*>(smem + L.misc);
+  const MuBracket br = mu_bracket(a.rl.mus, a.rl.M, a.mu);
+  cs_stage(a.rl, br, kn, xy, spd);
+  const int segs = cs_project(a.pts, a.np, a.p0, a.x0, a.y0, dist);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double vr = 0.0;
+    const int pj = cs_walk(a.rl, kn, xy, spd, a.prefix, dist, segs, a.p0, a.x0, a.y0, a.v0, a.mu, a.scale, a.Ts, a.H,
+                           sx, &vr);
+    a.out[2 * (a.H + 1)] = (double)pj;
+    a.out[2 * (a.H + 1) + 1] = vr;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * (a.H + 1); e += kBlock) {
+    const int row = e / (a.H + 1), k = e - row * (a.H + 1);
+    a.out[e] = sx[2 * k + row];
+  }
+}
+
+hipError_t launch_constant_speed(const CsLaunch& a, hipStream_t s) {
+  const CtlLds L = ctl_lds(a.H, 0, a.rl.n);
+  allow_lds(cs_kernel);
+  hipLaunchKernelGGL(cs_kernel, dim3(1), dim3(kBlock), L.end, s, a);
+  return hipGetLastError();
+}
+
+size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off) {
+  const CtlLds L = ctl_lds(H, C, n);
+  const size_t M = (size_t)nb_lb * K, Lb = nb_lb;    // lb_final's region (launch_plan's formula)
+  const size_t lbf = kScratchBytes + 8 * (3 * M + Lb) + sizeof(Ent) * Lb * kWaves + 4 * (3 * M + Lb + LLAMPC_KMAX + 2) + 8 + 16;
+  const size_t rank = kScratchBytes + (size_t)kWaves * kRankBytes + kBlockMergeBytes;
+  size_t off = std::max(L.end, std::max(lbf, rank));
+  off = align16(off);
+  *poll_off = off;
+  return off + kCtlPollBytes;
+}
+
+hipError_t launch_ctl(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s) {
+  const dim3 grid(c.nb_lb + c.nb_la), block(kBlock);
+  if (lpm == 4) {
+    allow_lds(ctl_kernel<4>);
+    hipLaunchKernelGGL(ctl_kernel<4>, grid, block, lds, s, c);
+  } else if (lpm == 2) {
+    allow_lds(ctl_kernel<2>);
+    hipLaunchKernelGGL(ctl_kernel<2>, grid, block, lds, s, c);
+  } else {
+    allow_lds(ctl_kernel<1>);
+    hipLaunchKernelGGL(ctl_kernel<1>, grid, block, lds, s, c);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace llampc

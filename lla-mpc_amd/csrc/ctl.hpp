@@ -1,0 +1,237 @@
+// ctl.hpp — the controller tick (llampc_ctl_*, include/llampc.h): the whole LLA-MPC control
+// step of rt.py:269-366 in ONE launch on the device — reference trajectory from the raceline
+// library (planner.py:12-67 with mu-hat, the projection of track.py:147-160 / projection.py:
+// 11-38), candidate control sequences (counter-based sampling; the build's stand-in for the
+// per-tick IPOPT solve, nmpc.py:161-203), look-back + window + selection (rt.py:347-366), the
+// look-ahead of the selected model and the top-K (rt.py:300-305), the mu-hat estimator
+// (rt.py:326-344) and the controller state (x_{t-1}, u_{t-1}, the chosen sequence, projidx).
+//
+// The pure functions here are __host__ __device__ so a host harness (tests/native) checks
+// them bitwise against the NumPy restatement of the test suite (tests/test_ctl_native.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kernels.hpp"
+#include "llampc.h"
+
+namespace llampc {
+
+constexpr int kCtlSlotsMax = LLAMPC_KMAX + 1;   // look-ahead models: top-K + the selection
+constexpr int kCtlSMax = 64;                    // mu-hat smoothing window (rt.py:68 uses 20)
+constexpr int kCtlSegs = 9;                     // project_fast over raceline[:, p:p+10]
+
+// Device-resident controller state, written by the block that completes a tick and read by
+// the next tick's blocks (stream order between the launches).
+struct CtlState {
+  double x_prev[6];               // x_{t-1}     (the look-back transition's start)
+  double u_prev[2];               // u_{t-1}     (applied input: the chosen sequence's first)
+  double useq[LLAMPC_HMAX][2];    // the last chosen sequence (the candidates' base)
+  double mu_pred;                 // mu-hat (rt.py:341); NaN until the first update
+  double dr_hist[kCtlSMax];       // the last S appended Dr / Df means, ring by count % S
+  double df_hist[kCtlSMax];
+  int64_t current_model;          // rt.py:264 / 363 (global index)
+  int32_t hist_count;             // means appended so far
+  int32_t projidx;                // planner state (rt.py:279, 296)
+  int32_t has_seq;                // a chosen sequence exists (tick >= 1)
+  int32_t pad;
+};
+
+// ---- counter-based sampling ------------------------------------------------------------
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11; the Random123 / rocRAND generator):
+// 10 rounds, the key bumped after each.  Known answers checked in tests (Random123 kat).
+struct Philox4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ Philox4 philox4x32_10(Philox4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = Philox4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Unit-variance noise of element i = (c H + k) 2 + j of tick `tick`: the four words of one
+// Philox call summed (a 4-term Irwin-Hall variate, exact in fp64: < 2^34), centred; the
+// caller scales by sqrt(3) sigma_j (variance 1/3 per uniform sum of four -> 1).
+__host__ __device__ __forceinline__ double ctl_z(uint32_t i, uint64_t tick, uint64_t seed, uint32_t stream) {
+  const Philox4 w = philox4x32_10(Philox4{i, (uint32_t)tick, (uint32_t)(tick >> 32), stream}, (uint32_t)seed,
+                                  (uint32_t)(seed >> 32));
+  const uint64_t s = (uint64_t)w.x + w.y + w.z + w.w;
+  return (double)s * 0x1p-32 - 2.0;
+}
+
+// np.clip for float64 (numpy clip.cpp: _NPY_MIN(_NPY_MAX(x, lo), hi), NaN passes through)
+__host__ __device__ __forceinline__ double np_clip(double x, double lo, double hi) {
+  const double y = (x != x) ? x : (x > lo ? x : lo);
+  return (y != y) ? y : (y < hi ? y : hi);
+}
+
+// Candidate element before the rate clip: base + noise (c >= 1), then the input bounds.
+// base = the previous chosen sequence shifted one step (or uprev held); noise = z nscale_j
+// with nscale_j = sqrt(3) sigma_j: two roundings, reproducible in NumPy.
+__host__ __device__ __forceinline__ double ctl_cand_raw(int c, int k, int j, int H, const double* prev_seq /*[H][2] or null*/,
+                                                        double up_j, double ns_j, double lo_j, double hi_j, uint64_t tick,
+                                                        uint64_t seed, uint32_t stream) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+  const double base = prev_seq ? prev_seq[2 * (k + 1 < H ? k + 1 : H - 1) + j] : up_j;
+  double u = base;
+  if (c > 0) {
+    const double z = ctl_z((uint32_t)((c * H + k) * 2 + j), tick, seed, stream);
+    const double noise = z * ns_j;
+    u = base + noise;
+  }
+  return np_clip(u, lo_j, hi_j);
+}
+
+// The rate clip of one (candidate, input) chain in order over k (controller.py
+// CandidateGenerator / nmpc.py:104-105): u_k <- clip(u_k, u_{k-1} - r, u_{k-1} + r), u_{-1} =
+// uprev; r = rate_max Ts (< 0: unbounded).  u points at element (c, 0, j), stride 2.
+__host__ __device__ __forceinline__ void ctl_rate_chain(double* u, int H, double up, double r) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+  if (!(r >= 0.0)) return;
+  double prev = up;
+  for (int k = 0; k < H; ++k) {
+    const double lo = prev - r, hi = prev + r;
+    prev = np_clip(u[2 * k], lo, hi);
+    u[2 * k] = prev;
+  }
+}
+
+// ---- projection (track.py:147-160, projection.py:11-38) ---------------------------------
+// numpy's 2-element dot as this stack computes it (x0 y0 rounded, then fused with x1 y1;
+// checked on 10^5 pairs against np.dot) and np.linalg.norm(v, 2) = sqrt(v . v).
+__host__ __device__ __forceinline__ double np_dot2(double a0, double a1, double b0, double b1) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+  const double p = a0 * b0;
+  return fma(a1, b1, p);
+}
+__host__ __device__ __forceinline__ double np_norm2(double a0, double a1) { return sqrt(np_dot2(a0, a1, a0, a1)); }
+
+// Projection(point, [x1, x2]) -> distance of the point to its projection (the foot point if
+// it lies inside the segment, else the nearer vertex), in the reference's operation order.
+__host__ __device__ __forceinline__ double ref_project_dist(double px, double py, double ax, double ay, double bx, double by) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+  double dx = bx - ax, dy = by - ay;
+  const double n1 = np_norm2(dx, dy);
+  dx = dx / n1;                                    // dir1 /= norm(dir1)
+  dy = dy / n1;
+  const double t = np_dot2(px - ax, py - ay, dx, dy);
+  const double sx = dx * t, sy = dy * t;           // x1 + dir1 * dot(x - x1, dir1)
+  double qx = ax + sx, qy = ay + sy;
+  const double d2x = qx - ax, d2y = qy - ay, d3x = qx - bx, d3y = qy - by;
+  const double n2 = np_norm2(d2x, d2y), n3 = np_norm2(d3x, d3y);
+  if (n2 > 0 && n3 > 0) {
+    const double e2x = d2x / n2, e2y = d2y / n2, e3x = d3x / n3, e3y = d3y / n3;
+    const bool on_line = np_norm2(e2x - e3x, e2y - e3y) > 1e-10;
+    if (!on_line) {
+      if (np_norm2(ax - qx, ay - qy) < np_norm2(bx - qx, by - qy)) {
+        qx = ax;
+        qy = ay;
+      } else {
+        qx = bx;
+        qy = by;
+      }
+    }
+  }
+  return np_norm2(px - qx, py - qy);
+}
+
+// np.argmin over dist[0..m) (first minimum; the first NaN if there is one).
+__host__ __device__ __forceinline__ int np_argmin(const double* d, int m) {
+  int b = 0;
+  for (int i = 1; i < m; ++i) {
+    if (d[b] != d[b]) break;
+    if (d[i] != d[i] || d[i] < d[b]) b = i;
+  }
+  return b;
+}
+
+// Segments project_fast tests from projection index p on a polyline of np points:
+// raceline[:, p:p+10] holds min(10, np - p) points.
+__host__ __device__ __forceinline__ int ctl_segments(int p, int np_) {
+  const int pts = np_ - p < kCtlSegs + 1 ? np_ - p : kCtlSegs + 1;
+  return pts - 1;
+}
+
+// numpy's pairwise sum (loops_utils.h pairwise_sum, n <= 128) of v[first..first+n) read
+// through a ring of `cap` entries (np.mean(np.array(hist)[-S:]) = this / n).
+__host__ __device__ __forceinline__ double np_pairwise_ring(const double* v, int first, int n, int cap) {
+  auto at = [&](int i) {
+    int s = first + i;
+    while (s >= cap) s -= cap;
+    return v[s];
+  };
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += at(i);
+    return r;
+  }
+  double r[8];
+  for (int j = 0; j < 8; ++j) r[j] = at(j);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += at(i + j);
+  double s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) s += at(i);
+  return s;
+}
+
+// The controller launch (ctl.hip ctl_kernel): every field set by the host (capi.hip
+// llampc_ctl_*) except the look-back's x_now, which the kernel points at x_t.
+struct CtlLaunch {
+  LookbackLaunch lb;          // x_prev / u_prev -> the state (host), x_now -> x_t (kernel)
+  LookaheadLaunch la;         // params, veh, cost, C, H, Ts, rl (U and xref: LDS)
+  FinalLaunch fin;            // lb_final's view (out = &out->plan, nb_lb, K, lists)
+  CtlState* st;
+  llampc_ctl_out* out;        // device alias of the pinned host record
+  uint64_t* host_tag;
+  uint64_t host_seq;
+  uint64_t* sel_tag;          // [kCtlSlotsMax]   selection (lb_final<true>)
+  uint64_t* slot_tag;         // [kCtlSlotsMax][4] slot results: cost hi, lo, cand, nf | late << 31
+  unsigned* tickets;          // [1] the look-back ticket
+  double* dbg;                // null, or this tick's xref [2][H+1] then U [C][H][2]
+  const double* pts;          // raceline points [2][np] (project_fast's polyline)
+  const double* prefix;       // [np - 1] start arc length per projection index
+  uint64_t tick, seed;
+  double x_t[6];
+  double nominal[6];          // Bf, Cf, Df, Br, Cr, Dr (the warm-up model)
+  double nscale[2], rate[2];  // sqrt(3) sigma_j; rate_max_j Ts (< 0: none)
+  double umin[2], umax[2];
+  double mu_fixed, scale_fixed, v_factor, mu_init;
+  size_t poll_off;
+  uint32_t seq, poll;         // tag of this launch; poll bound (2^16 s_memrealtime units)
+  int32_t np, lap_projidx;
+  int32_t do_lb, warm, use_mu, full, nslots, mpb, G, cpl, S, K;
+  int32_t nb_lb, nb_la;
+};
+
+// llampc_ctl_reference's launch: ConstantSpeed alone (planner.py:12-67) on the device.
+struct CsLaunch {
+  RacelineK rl;
+  const double* pts;          // [2][np]
+  const double* prefix;       // [np - 1]
+  double* out;                // [2][H+1] xref, then projidx, vr
+  double x0, y0, v0, mu, scale, Ts;
+  int32_t np, p0, H;
+};
+hipError_t launch_constant_speed(const CsLaunch& a, hipStream_t s);
+
+// LDS bytes of the controller launch and the completing block's area offset (ctl.hip).
+size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off);
+hipError_t launch_ctl(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s);
+
+}  // namespace llampc

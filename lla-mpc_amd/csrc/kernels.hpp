@@ -70,9 +70,9 @@ struct LookaheadLaunch {
   uint32_t seq;                          // this launch's tag (never 0)
   int32_t poll;
   // work queue (launch_plan decides: LPM 1, G <= 64, more look-ahead blocks than CUs): the
-  // bank's monotonic unit counter and this launch's base (capi advances it per launch)
+  // bank's unit counter, 0 at every launch's start (the block completing the record resets it
+  // after every take of the launch, final_write)
   uint64_t* wq;
-  uint64_t wq_base;
 };
 
 // What the ticket winners of the plan launch need (see plan_kernel).
@@ -110,6 +110,9 @@ struct FinalLaunch {
   int32_t px_G, px_rank;
   uint32_t px_seq;
   uint32_t px_bound;                      // poll bound, units of 2^16 s_memrealtime ticks
+  // the work-queue unit counter (LookaheadLaunch::wq): reset to 0 by final_write, which runs
+  // after every look-ahead block has published (so after every take of the launch)
+  uint64_t* wq;
 };
 
 // Tick inputs in the kernarg segment (host-pointer ticks whose pack fits): x_prev[6],
@@ -124,6 +127,8 @@ int lookback_blocks(int64_t n);
 int lookahead_group(int32_t C);
 int lookahead_lpm(int64_t n, int32_t C, int32_t integrator);
 int lookahead_blocks(int64_t n, int32_t C, int lpm);
+int lookback_r(int64_t n, int32_t K);               // models per look-back lane
+int lookback_blocks_r(int64_t n, int R);
 size_t lookahead_lds_bytes(int32_t C, int32_t H, bool* stage_u);
 size_t raceline_lds_bytes(int32_t n, int32_t M);
 
@@ -131,11 +136,35 @@ size_t raceline_lds_bytes(int32_t n, int32_t M);
 // the completion stages run by ticket winners; writes f.out.  f.nb_* / f.do_* are set here.
 // pk != null: the inputs are in *pk (see InlinePack); needs a look-ahead with RK4, the
 // given xref and U staged in LDS (plan_inline_ok), else hipErrorInvalidValue.
-// wq_advance (optional out): the work-queue counter increments this launch makes (0 when
-// it runs the static block-per-models layout).
 hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
-                       hipStream_t s, const InlinePack* pk = nullptr, int64_t* wq_advance = nullptr);
+                       hipStream_t s, const InlinePack* pk = nullptr);
 bool plan_inline_ok(int32_t C, int32_t H, int32_t integrator, int32_t xref_mode);
+// The plan-kernel variant groups (plan_dev.hpp; one translation unit per group, plan_*.hip):
+// (integrator, lanes per rollout) with the staged / unstaged inputs and, for RK4 at LPM 1, the
+// work-queue layouts; the inline-pack host ticks per LPM.
+template <int INTEG, int LPM>
+void launch_plan_group(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f, int G,
+                       int cpl, bool stage, size_t lds, hipStream_t s, int wq);
+template <int LPM>
+void launch_plan_inline_group(const LookbackLaunch& lb, const LookaheadLaunch& la, const FinalLaunch& f,
+                              int G, int cpl, size_t lds, hipStream_t s, const InlinePack& pk);
+#define LLAMPC_PLAN_GROUP_DECL(I, L)                                                               \
+  extern template void launch_plan_group<I, L>(const LookbackLaunch&, const LookaheadLaunch&,      \
+                                               const FinalLaunch&, int, int, bool, size_t,          \
+                                               hipStream_t, int)
+LLAMPC_PLAN_GROUP_DECL(0, 4);
+LLAMPC_PLAN_GROUP_DECL(0, 2);
+LLAMPC_PLAN_GROUP_DECL(0, 1);
+LLAMPC_PLAN_GROUP_DECL(1, 4);
+LLAMPC_PLAN_GROUP_DECL(1, 2);
+LLAMPC_PLAN_GROUP_DECL(1, 1);
+LLAMPC_PLAN_GROUP_DECL(2, 1);
+extern template void launch_plan_inline_group<4>(const LookbackLaunch&, const LookaheadLaunch&, const FinalLaunch&,
+                                                 int, int, size_t, hipStream_t, const InlinePack&);
+extern template void launch_plan_inline_group<2>(const LookbackLaunch&, const LookaheadLaunch&, const FinalLaunch&,
+                                                 int, int, size_t, hipStream_t, const InlinePack&);
+extern template void launch_plan_inline_group<1>(const LookbackLaunch&, const LookaheadLaunch&, const FinalLaunch&,
+                                                 int, int, size_t, hipStream_t, const InlinePack&);
 hipError_t launch_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_first,
                         llampc_plan_out* merged, hipStream_t s);
 // Peer exchange of the sharded tick (peer_exchange_kernel): mailbox g is [2][G][kRecWords]

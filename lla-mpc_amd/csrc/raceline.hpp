@@ -77,6 +77,36 @@ __device__ __host__ __forceinline__ double spline_at(const double* c, int m, int
 constexpr int kAhead = 8;
 constexpr int kKnotPad = kAhead;
 
+// mu -> the bracketing speed profiles (planner.py:48-62): below mus[0] -> profile 0, above
+// mus[M-1] -> the last; else i = first mus[i] >= mu, lo = i-1 (i == 0 wraps to M-1, as the
+// reference's negative index does); v = (v_lo wa) / den + (v_hi wb) / den.
+struct MuBracket {
+  int lo, hi;
+  bool single;               // mu outside [mus[0], mus[M-1]]: one profile, no interpolation
+  double wa, wb, den;
+};
+__device__ __host__ __forceinline__ MuBracket mu_bracket(const double* mus, int M, double mu) {
+  MuBracket b;
+  b.single = mu < mus[0] || mu > mus[M - 1];        // NaN: the interpolation branch, as the
+  if (b.single) {                                   // reference's comparisons fall through
+    b.lo = b.hi = (mu > mus[M - 1]) ? M - 1 : 0;
+    b.wa = 1.0;
+    b.wb = 0.0;
+    b.den = 1.0;
+  } else {
+    // i = the first mus[i] >= mu among i < M - 1, else M - 1 (NaN mu: M - 1): with mus
+    // ascending, the count of !(mus[j] >= mu), j < M - 1 — independent reads, no loop
+    int i = 0;
+    for (int j = 0; j < M - 1; ++j) i += (int)!(mus[j] >= mu);
+    b.hi = i;
+    b.lo = (i == 0) ? M - 1 : i - 1;
+    b.wa = mus[b.hi] - mu;
+    b.wb = mu - mus[b.lo];
+    b.den = mus[b.hi] - mus[b.lo];
+  }
+  return b;
+}
+
 struct RaceRef {
   double s, v, L, scale, Ts;
   double wa, wb, den;        // v = (v_lo (hi-mu)) / (hi-lo) + (v_hi (mu-lo)) / (hi-lo)
@@ -84,37 +114,24 @@ struct RaceRef {
   int lo, hi, seg;
   bool single;               // mu outside [mus[0], mus[M-1]]: one profile, no interpolation
 
-  // mu -> bracketing profiles (planner.py:48-62): below mus[0] -> profile 0, above
-  // mus[M-1] -> the last; else i = first mus[i] >= mu, lo = i-1 (i == 0 wraps to M-1, as
-  // the reference's negative index does).
+  // mu -> bracketing profiles (mu_bracket).
   // seg0 >= 0: the start segment (the same for every model of a launch: the caller's one
   // bisection); < 0: bisect here.
   __device__ __host__ __forceinline__ void init(const RacelineK& r, const double* knots_lds,
                                        const double* mus_lds, double mu, double s0, double v0,
                                        double scale_, double Ts_, int seg0 = -1) {
-    const int M = r.M;
     L = knots_lds[r.n - 1];
     scale = scale_;
     Ts = Ts_;
     s = s0;
     v = fmax(v0, 0.01);                                             // planner.py:34
-    single = mu < mus_lds[0] || mu > mus_lds[M - 1];   // NaN: the interpolation branch, as the
-    if (single) {                                   // reference's comparisons fall through
-      lo = hi = (mu > mus_lds[M - 1]) ? M - 1 : 0;
-      wa = 1.0;
-      wb = 0.0;
-      den = 1.0;
-    } else {
-      // i = the first mus[i] >= mu among i < M - 1, else M - 1 (NaN mu: M - 1): with mus
-      // ascending, the count of !(mus[j] >= mu), j < M - 1 — independent reads, no loop
-      int i = 0;
-      for (int j = 0; j < M - 1; ++j) i += (int)!(mus_lds[j] >= mu);
-      hi = i;
-      lo = (i == 0) ? M - 1 : i - 1;
-      wa = mus_lds[hi] - mu;
-      wb = mu - mus_lds[lo];
-      den = mus_lds[hi] - mus_lds[lo];
-    }
+    const MuBracket b = mu_bracket(mus_lds, r.M, mu);
+    lo = b.lo;
+    hi = b.hi;
+    single = b.single;
+    wa = b.wa;
+    wb = b.wb;
+    den = b.den;
     // initial segment: bisect-right on the knots, clamped to the last segment
     if (seg0 >= 0) {
       seg = seg0;

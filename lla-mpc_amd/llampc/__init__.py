@@ -10,9 +10,12 @@ import os as _os
 
 # Kernel arguments in device memory: the tick's blocks read their launch descriptors (and
 # through them the inputs) with scalar loads first, and with kernargs in host memory every
-# tick measured 5 us longer (31.3-32.3 vs 26.1-26.9 us).  HIP reads this when it
-# initialises, so it takes effect when llampc is imported before the first HIP call (bench.py
-# sets it too); an explicit setting in the environment is kept.
-_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+# tick measured 5 us longer (31.3-32.3 vs 26.1-26.9 us).  Device kernargs are
+# this ROCm's default; HIP_FORCE_DEV_KERNARG changes kernarg placement for EVERY HIP user of
+# the process (torch included), so importing llampc only sets it when asked to
+# (LLAMPC_SET_DEV_KERNARG=1, before the first HIP call; an explicit setting is kept).  bench.py
+# and the tests set it themselves (INTEGRATION.md "Process environment").
+if _os.environ.get("LLAMPC_SET_DEV_KERNARG") == "1":
+    _os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 __version__ = "0.1.0"

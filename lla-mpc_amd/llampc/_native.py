@@ -69,6 +69,22 @@ class PlanOut(C.Structure):
 
 
 PLAN_OUT_BYTES = C.sizeof(PlanOut)
+HMAX = 64
+
+
+class CtlCfg(C.Structure):
+    """llampc_ctl_cfg (include/llampc.h): the controller tick's configuration."""
+    _fields_ = [("C", C.c_int32), ("H", C.c_int32), ("K", C.c_int32), ("nan_policy", C.c_int32),
+                ("Ts", C.c_double), ("v_factor", C.c_double), ("mu_init", C.c_double),
+                ("S", C.c_int32), ("lap_projidx", C.c_int32), ("sigma", C.c_double * 2), ("seed", C.c_uint64),
+                ("nominal", C.c_double * 6), ("cost", Cost), ("debug_inputs", C.c_int32), ("reserved", C.c_int32)]
+
+
+class CtlOut(C.Structure):
+    """llampc_ctl_out: the tick record plus the controller's own fields."""
+    _fields_ = [("plan", PlanOut), ("tick", C.c_int64), ("projidx", C.c_int32), ("warm", C.c_int32),
+                ("mu_used", C.c_double), ("scale_used", C.c_double), ("mu_pred", C.c_double),
+                ("dr_mean", C.c_double), ("df_mean", C.c_double), ("u_seq", (C.c_double * 2) * HMAX)]
 
 # name -> (restype, argtypes); exactly the symbols include/llampc.h declares.
 _SIGNATURES = {
@@ -113,6 +129,14 @@ _SIGNATURES = {
     "llampc_plan_exchange": (C.c_int, [C.c_void_p, C.POINTER(PlanIn), C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p]),
     "llampc_mailbox_destroy": (C.c_int, [C.c_void_p]),
+    "llampc_ctl_create": (C.c_int, [C.c_void_p, C.POINTER(CtlCfg), _dp, C.c_int32, _dp, C.POINTER(C.c_void_p)]),
+    "llampc_ctl_tick": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "llampc_ctl_tick_async": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "llampc_ctl_wait": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "llampc_ctl_inputs": (C.c_int, [C.c_void_p, _dp, _dp]),
+    "llampc_ctl_reference": (C.c_int, [C.c_void_p, _dp, C.c_double, C.c_int32, C.c_int32, C.c_double, C.c_double,
+                                       _dp, C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
+    "llampc_ctl_destroy": (C.c_int, [C.c_void_p]),
     "llampc_dynamics_batch": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                         C.POINTER(Vehicle), C.c_int64, C.c_void_p, C.c_int32,
                                         C.c_int32, C.c_void_p]),

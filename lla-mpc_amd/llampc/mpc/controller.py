@@ -8,11 +8,19 @@ Host logic restated from the reference driver (llampc/mpc/run_nmpc_orca_llampc_r
                              the per-tick IPOPT solve of nmpc.py:161-203 by candidate search)
   * ``LLAMPC.tick``          one tick in rt.py order: look-back on the newest transition,
                              mu-hat, ConstantSpeed reference with mu-hat (rt.py:278-282),
-                             look-ahead of every (model, candidate), chosen control.  While
-                             the window fills (tick <= W) the look-ahead plans with the
-                             NOMINAL model, as the reference's nlp_initial (rt.py:207,
-                             300-301); afterwards with the bank's selected model
-                             (nlp_bank[current_model_idx], rt.py:303).
+                             look-ahead, chosen control.  While the window fills (tick <= W)
+                             the look-ahead plans with the NOMINAL model, as the reference's
+                             nlp_initial (rt.py:207, 300-301); afterwards with the bank's
+                             selected model (nlp_bank[current_model_idx], rt.py:303).
+    mode="device" (default): the whole tick is ONE kernel launch (``DeviceController``,
+                             llampc_ctl_tick): the reference trajectory (projection + the
+                             prefix arc-length table + ConstantSpeed with mu-hat), the
+                             candidates (Philox sampling), look-back + selection, the
+                             look-ahead of the selected model and the top-K, mu-hat and the
+                             controller state all on the GPU; the host passes x_t and reads
+                             the record.
+    mode="host":             the round-3 loop: host ConstantSpeed + host CandidateGenerator
+                             around the fused plan launch, every (model, candidate) rolled out.
 """
 from __future__ import annotations
 
@@ -86,6 +94,17 @@ class MuEstimator:
         self.df_hist.append(self.mu_init * self.mass * 9.8 * self.lf / (self.lf + self.lr))
         self.mu_logged.append(self.mu_init)
 
+    def record(self, dr_mean, df_mean, mu_pred, warm):
+        """The device controller's update of this tick (it computed the same values on the
+        GPU, ctl.hip ctl_complete): the histories, mu-hat and the logged smoothed value."""
+        self.dr_hist.append(dr_mean)
+        self.df_hist.append(df_mean)
+        if warm:
+            self.mu_logged.append(self.mu_init)
+        else:
+            self.mu_pred = mu_pred
+            self.mu_logged.append(self.smoother.update(mu_pred) * .95)
+
     def update(self, topk_Dr, topk_Df) -> float:
         self.dr_hist.append(np.mean(topk_Dr))
         self.df_hist.append(np.mean(topk_Df))
@@ -132,6 +151,96 @@ class CandidateGenerator:
         return np.ascontiguousarray(U)
 
 
+class DeviceController:
+    """Handle of llampc_ctl (include/llampc.h): the control step of rt.py:278-366 as ONE launch
+    on the bank's device, the controller state (x_{t-1}, u_{t-1}, the chosen sequence,
+    projidx, mu-hat histories, current model) resident there between ticks.  The bank must
+    not be ticked by anything else while the controller drives it."""
+
+    def __init__(self, bank: ModelBank, track, H=20, C=64, K=10, Ts=0.02, v_factor=0.9, mu_init=1.0, S=20,
+                 sigma=(0.05, 0.02), seed=2, nominal6=None, cost=None, nan_policy=nat.NAN_FIRST,
+                 debug_inputs=False, lap_projidx=None):
+        if getattr(bank, "raceline", None) is not track:
+            bank.set_raceline(track)
+        self.bank, self.track, self.H, self.C = bank, track, int(H), int(C)
+        cfg = nat.CtlCfg()
+        cfg.C, cfg.H, cfg.K, cfg.nan_policy = int(C), int(H), int(K), int(nan_policy)
+        cfg.Ts, cfg.v_factor, cfg.mu_init, cfg.S = float(Ts), float(v_factor), float(mu_init), int(S)
+        cfg.lap_projidx = int(track.lap_projidx if lap_projidx is None else lap_projidx)
+        cfg.sigma[0], cfg.sigma[1] = float(sigma[0]), float(sigma[1])
+        cfg.seed = int(seed)
+        if nominal6 is None:
+            from llampc.params import ORCA
+            nominal6 = [ORCA(control='pwm')[k] for k in BANK_ORDER]
+        for j, v in enumerate(nominal6):
+            cfg.nominal[j] = float(v)
+        cfg.cost = cost if cost is not None else nat.cost_struct(enforce_bounds=True)
+        cfg.debug_inputs = int(bool(debug_inputs))
+        pts, prefix = track.ctl_table()
+        h = nat.C.c_void_p()
+        nat.check(nat.load().llampc_ctl_create(bank.handle, nat.C.byref(cfg), nat.dptr(pts), pts.shape[1],
+                                               nat.dptr(prefix), nat.C.byref(h)))
+        self._h = h
+        self.cfg = cfg
+        self._x = np.zeros(6)
+
+    def tick(self, x_t, out=None) -> "nat.CtlOut":
+        """One blocking step; ``out`` (a CtlOut) is filled and returned (a new one if None)."""
+        out = nat.CtlOut() if out is None else out
+        x = self._x
+        x[:] = x_t
+        nat.check(nat.load().llampc_ctl_tick(self._h, x.ctypes.data, nat.C.addressof(out)))
+        return out
+
+    def tick_async(self, x_t):
+        x = self._x
+        x[:] = x_t
+        nat.check(nat.load().llampc_ctl_tick_async(self._h, x.ctypes.data))
+
+    def wait(self, out=None) -> "nat.CtlOut":
+        out = nat.CtlOut() if out is None else out
+        nat.check(nat.load().llampc_ctl_wait(self._h, nat.C.addressof(out)))
+        return out
+
+    def inputs(self):
+        """The last tick's reference xref [2, H+1] and candidates U [C, H, 2] (debug_inputs)."""
+        xref = np.empty((2, self.H + 1))
+        U = np.empty((self.C, self.H, 2))
+        nat.check(nat.load().llampc_ctl_inputs(self._h, nat.dptr(xref), nat.dptr(U)))
+        return xref, U
+
+    def reference(self, x0, v0, H, projidx, curr_mu=1., scale=1.):
+        """ConstantSpeed(x0, v0, track, H, Ts, projidx, scale, curr_mu) (planner.py:12-67)
+        evaluated by the device code the controller ticks with -> (xref [2, H+1], projidx, vr)."""
+        xref = np.empty((2, int(H) + 1))
+        pj, vr = nat.C.c_int32(), nat.C.c_double()
+        nat.check(nat.load().llampc_ctl_reference(self._h, nat.dptr(nat.f64(np.asarray(x0)[:2])), float(v0), int(H),
+                                                  int(projidx), float(curr_mu), float(scale), nat.dptr(xref),
+                                                  nat.C.byref(pj), nat.C.byref(vr)))
+        return xref, pj.value, vr.value
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            nat.load().llampc_ctl_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def result_from_ctl(o: "nat.CtlOut", H: int) -> PlanResult:
+    """PlanResult of a controller tick: the record plus the chosen sequence [2, H]."""
+    res = result_from_out(o.plan)
+    res.u_seq = np.ctypeslib.as_array(o.u_seq)[:H].T.copy()
+    res.nominal = bool(o.warm)
+    res.mu_hat = None if np.isnan(o.mu_pred) else float(o.mu_pred)
+    res.raw = o
+    return res
+
+
 class LLAMPC:
     """Stateful LLA-MPC tick loop over a ``ModelBank`` (rt.py:269-366 without IPOPT).
 
@@ -140,13 +249,27 @@ class LLAMPC:
 
     def __init__(self, bank: ModelBank, track, H=20, Ts=0.02, K=10, C=64, v_factor=0.9,
                  mu_init=1.0, S=20, alpha=0.08, cost=None, integrator="rk4", seed=2,
-                 nan_policy=nat.NAN_FIRST, nominal: dict | None = None):
+                 nan_policy=nat.NAN_FIRST, nominal: dict | None = None, mode="device",
+                 sigma=(0.05, 0.02), debug_inputs=False):
         from llampc.params import ORCA
+        if mode not in ("device", "host"):
+            raise ValueError(f"mode={mode!r}: 'device' or 'host'")
+        self.mode = mode
         self.bank, self.track = bank, track
         nominal = ORCA(control='pwm') if nominal is None else nominal
         col = np.array([[float(nominal[k])] for k in BANK_ORDER])
-        # a one-model bank: the warm-up look-ahead runs the same kernel on the nominal model
-        self.nominal_bank = ModelBank(col, shared=bank.shared, W=1, device=bank.device)
+        self.nominal_bank = None
+        self._ctl = None
+        if mode == "device":
+            if integrator != "rk4":
+                raise ValueError("the device controller rolls out with RK4 (use mode='host' for other integrators)")
+            self._ctl = DeviceController(bank, track, H=H, C=C, K=K, Ts=Ts, v_factor=v_factor, mu_init=mu_init,
+                                         S=S, sigma=sigma, seed=seed, nominal6=col[:, 0],
+                                         cost=cost if cost is not None else nat.cost_struct(enforce_bounds=True),
+                                         nan_policy=nan_policy, debug_inputs=debug_inputs)
+        else:
+            # a one-model bank: the warm-up look-ahead runs the same kernel on the nominal model
+            self.nominal_bank = ModelBank(col, shared=bank.shared, W=1, device=bank.device)
         self.H, self.Ts, self.K, self.W = H, Ts, K, bank.W
         self.v_factor = v_factor
         sh = bank.shared
@@ -173,6 +296,8 @@ class LLAMPC:
         Raises NativeError if the selected model is not on this bank (a shard of a larger
         bank: use ShardedBank, whose merged record carries the owner's choice)."""
         x_t = np.asarray(x_t, dtype=np.float64)
+        if self.mode == "device":
+            return self._tick_device(x_t)
         t = self.t
         warm = t <= self.W
         # 1. reference (rt.py:278-282); it uses the mu-hat of the previous tick because
@@ -211,6 +336,9 @@ class LLAMPC:
                                             do_lookahead=True, current_model=self.current_model,
                                             nan_policy=self.nan_policy, cost=self.cost)
             res = result_from_out(o, U)
+            if not res.window_full:
+                raise nat.NativeError(f"tick {t}: the look-back window is not full after the warm-up "
+                                      "(was the bank reset?)")
             if res.u_seq is None:
                 raise nat.NativeError(
                     f"tick {t}: the selected model {res.best_model} is not on this bank "
@@ -230,8 +358,45 @@ class LLAMPC:
         self.t += 1
         return res
 
+    def tick_begin(self, x_t):
+        """Device mode: enqueue the tick (llampc_ctl_tick_async) and return at once, so the
+        controllers of several banks (e.g. two tracks) run concurrently; tick_end() completes it."""
+        if self.mode != "device":
+            raise nat.NativeError("tick_begin/tick_end need mode='device'")
+        self._pending_x = np.asarray(x_t, dtype=np.float64).copy()
+        self._ctl.tick_async(self._pending_x)
+
+    def tick_end(self) -> PlanResult:
+        return self._finish_device(self._ctl.wait(), self._pending_x)
+
+    def _tick_device(self, x_t) -> PlanResult:
+        """ONE launch (llampc_ctl_tick): the device computes the reference, the candidates, the
+        look-back, the look-ahead of the selected and top-K models, mu-hat and its state."""
+        return self._finish_device(self._ctl.tick(x_t), x_t)
+
+    def _finish_device(self, o, x_t) -> PlanResult:
+        res = result_from_ctl(o, self.H)
+        self.mu.record(o.dr_mean, o.df_mean, o.mu_pred, bool(o.warm))
+        res.mu_hat = self.mu.mu_pred
+        if res.window_full:
+            self.last_topk = res.topk
+        self.current_model = res.best_model
+        self.projidx = int(o.projidx)
+        self.u_seq = res.u_seq.T
+        self.x_prev = x_t
+        self.u_prev = res.u_seq[:, 0].copy()
+        self.t += 1
+        return res
+
+    def inputs(self):
+        """Device mode with debug_inputs=True: the last tick's xref [2, H+1] and U [C, H, 2]."""
+        return self._ctl.inputs()
+
     def close(self):
-        self.nominal_bank.close()
+        if self._ctl is not None:
+            self._ctl.close()
+        if self.nominal_bank is not None:
+            self.nominal_bank.close()
 
     def __enter__(self):
         return self

@@ -153,6 +153,20 @@ class Raceline(Track):
         return knots, np.ascontiguousarray(xy), np.ascontiguousarray(speed), np.asarray(self.mus, dtype=np.float64)
 
 
+    def ctl_table(self):
+        """(points [2, np], prefix [np-1]) for llampc_ctl_create: the polyline project_fast
+        projects on (track.py:147-160) and, per projection index p, the start arc length of
+        ConstantSpeed (planner.py:29-36) evaluated with the reference's own expression — so the
+        device controller's lookup equals the host planner's sum bitwise, in O(1) per tick."""
+        cached = getattr(self, "_ctl_table", None)
+        if cached is None:
+            rl = np.ascontiguousarray(self.raceline, dtype=np.float64)
+            prefix = np.array([np.sum(np.linalg.norm(np.diff(rl[:, :p + 2]), 2, axis=0))
+                               for p in range(rl.shape[1] - 1)])
+            cached = self._ctl_table = (rl, prefix)
+        return cached
+
+
 class ETHZTrack(Raceline):
     """ethz.py:15-97: boundary lines from the reference's txt files (packaged) plus the
     raceline chosen by ``reference`` / ``longer``."""

@@ -5,6 +5,10 @@ import sys
 import numpy as np
 import pytest
 
+# device kernel arguments, as bench.py (set before anything initialises HIP; llampc itself
+# leaves the process environment alone)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_ROOT = os.path.join(REPO, "lla-mpc_amd")
 GOLDEN = os.path.join(REPO, "tests", "golden")

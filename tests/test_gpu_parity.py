@@ -476,7 +476,7 @@ def test_closed_loop_lookback_and_mu_vs_golden(nat):
 
 @pytest.mark.parametrize("N", [300, 6])
 def test_llampc_controller_closed_loop_vs_oracle(nat, monkeypatch, N):
-    """The LLAMPC tick loop in closed loop with an RK6 plant (friction dropping): while the
+    """mode="host" (the device mode: tests/test_ctl_gpu.py).  The LLAMPC tick loop in closed loop with an RK6 plant (friction dropping): while the
     window fills (tick <= W) every tick plans with the NOMINAL model (the reference's
     nlp_initial, rt.py:207, 300-301), afterwards with the look-back's selection
     (nlp_bank[current_model_idx], rt.py:303).  Each tick's chosen candidate and cost equal
@@ -499,7 +499,7 @@ def test_llampc_controller_closed_loop_vs_oracle(nat, monkeypatch, N):
     win = O.LookbackWindow(N, W, K)
     x = d["states"][:, 0].copy()
     cur = 0
-    with ModelBank(bank_p, W=W, device=0) as b, LLAMPC(b, ETHZ('optimal', True), H=H, C=C, K=K) as ctl:
+    with ModelBank(bank_p, W=W, device=0) as b, LLAMPC(b, ETHZ('optimal', True), H=H, C=C, K=K, mode="host") as ctl:
         gen = ctl.gen
         ctl.gen = lambda prev, up: (lambda U: (Us.append(U), U)[1])(gen(prev, up))
         x_prev = u_prev = None

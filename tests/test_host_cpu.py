@@ -37,6 +37,9 @@ def test_struct_layouts_match_header():
     assert _native.PLAN_OUT_BYTES == expect
     assert ctypes.sizeof(_native.Cost) == 8 * 18 + 8
     assert ctypes.sizeof(_native.Vehicle) == 8 * 8 + 8
+    # llampc_ctl_cfg / llampc_ctl_out (static_asserts in capi.hip hold the same numbers)
+    assert ctypes.sizeof(_native.CtlCfg) == 280
+    assert ctypes.sizeof(_native.CtlOut) == _native.PLAN_OUT_BYTES + 56 + 16 * _native.HMAX
 
 
 def test_no_device_fails_loudly():
