@@ -369,8 +369,16 @@ def main():
     pins = [sb.make_plan_in(packs[i], C, H, K=K, current_model=0) for i in range(T)]
     lib = nat.load()
 
-    def step(i):
-        sb.launch(pins[i % T], stream)
+    def step(i, ex=None):
+        sb.launch(pins[i % T], stream, exchange_events=ex)
+
+    # with the exchange: the ticks whose plan launch the bank's sampled event pair brackets (one
+    # in TIMING_SAMPLE) run the exchange as its own kernel, bracketed by a second event pair, so
+    # the line splits a tick into plan and exchange (peer: the split form of the same protocol)
+    ex_events = []
+    if sb.exchange and not args.no_timing:
+        ex_events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                     for _ in range(args.steps // TIMING_SAMPLE + 1)]
 
     avg = (ctypes.c_double * 3)()
     cnt = (ctypes.c_int64 * 3)()
@@ -398,7 +406,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(args.warmup + i, ex_events[i // TIMING_SAMPLE] if ex_events and i % TIMING_SAMPLE == 0 else None)
     t_issue = time.perf_counter() - t0       # host time to enqueue the K ticks
     torch.cuda.synchronize()
     if world > 1:
@@ -413,6 +421,10 @@ def main():
         nat.check(lib.llampc_bank_timing_read(sb.bank.handle, avg, cnt))
         nat.check(lib.llampc_bank_timing(sb.bank.handle, 0, 1))
     plan_ms = avg[0]
+    exch_ms = float(np.mean([a.elapsed_time(b) for a, b in ex_events])) if ex_events else None
+    if world > 1 and exch_ms is not None:
+        exch_ms = max_over_ranks(exch_ms)
+        plan_ms = max_over_ranks(plan_ms)
 
     merged = sb.fetch(stream)          # result of the last tick (all ranks identical)
 
@@ -465,9 +477,17 @@ def main():
                      "note": "plain flops only; the 29 fp64 transcendentals per RK4 step are excluded"},
             "issue": issue_roofline(N_local, C, H, lpm_of(N_local, C), plan_ms),
             "kernel_us": {"plan": plan_ms * 1e3, "events": int(cnt[0]),
-                          "bracket": f"one plan launch in every {TIMING_SAMPLE} per event pair" if sb.exchange else
-                                     f"one event pair around all {args.steps} timed plan launches"},
+                          "exchange": exch_ms * 1e3 if exch_ms is not None else None,
+                          "bracket": (f"one tick in every {TIMING_SAMPLE}: its plan launch and its exchange (run as its "
+                                      "own kernel on that tick) each bracketed by an event pair; max over ranks")
+                                     if sb.exchange else
+                                     f"one event pair around all {args.steps} timed plan launches: stream time per "
+                                     "launch (includes any gap between launches; rocprof's kernel average beside it "
+                                     "in profiles/ is the per-dispatch duration)"},
             "exchange": EXCHANGE_DESC[sb.transport] if sb.exchange else None,
+            # the event pair measures stream time: if the host enqueued the launches barely faster
+            # than they ran, gaps between launches would count as kernel time
+            "kernel_time_host_bound_suspect": bool(plan_ms > 0 and t_issue / args.steps * 1e3 > 0.8 * plan_ms),
             "host_issue_us_per_step": t_issue / args.steps * 1e6,
             "lpm": lpm_of(N_local, C),
             "result_check": {"sel_model": merged.best_model, "window_full": merged.window_full,

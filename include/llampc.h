@@ -22,6 +22,7 @@
  *  llampc_merge / _device          (new) cross-shard merge of per-GPU plan results
  *  llampc_exchange_device / _peer  (new) the per-tick gather + merge of the sharded bank
  *                                  (SURVEY.md §8e): RCCL all-gather, or xGMI mailboxes
+ *  llampc_nlp_*                    setupNLP / .solve (nmpc.py:14-203), solved by sampling
  *  llampc_dynamics_batch           Dynamic.calc_forces_batch (llampc/models/dynamic.py:
  *                                  117-154), Dynamic._diffequation_batch (:98-115)
  *  llampc_ctl_*                    the control loop body rt.py:278-366 on the device
@@ -349,6 +350,33 @@ int llampc_ctl_reference(llampc_ctl* ctl, const double* x0, double v0, int32_t H
 /* The last tick's reference xref [2][H+1] and candidates U [C][H][2] (cfg.debug_inputs = 1). */
 int llampc_ctl_inputs(llampc_ctl* ctl, double* xref, double* U);
 int llampc_ctl_destroy(llampc_ctl* ctl);
+
+/* ---- setupNLP.solve drop-in ------------------------------------------------------ */
+/* The selected model's NMPC (nmpc.py:14-203) on the device: the NLP's Euler transcription of
+ * Dynamic.casadi (nmpc.py:58-60, dynamic.py:195-226), its objective (nmpc.py:44-111), the input
+ * bounds and the rate bound (nmpc.py:102-105), minimised by the cross-entropy method: `iters`
+ * rounds of `samples` sequences drawn from a per-(step, input) normal-like distribution (Philox
+ * noise, clipped to the bounds, rate-clipped in order), the `elite` best setting the next mean
+ * and std.  Replaces nlpsol/IPOPT (nmpc.py:146-157, 192), which this platform lacks: the
+ * optimum is NOT IPOPT's (parity unpinned).  The bank holds the ONE model (n = 1). */
+typedef struct llampc_nlp_cfg {
+  int32_t H, samples, iters, elite;  /* samples: power of two in [64, 4096]; 1 <= elite <= samples */
+  double Ts;
+  double sigma0[2];                  /* the first iteration's std per input                     */
+  double std_floor;                  /* added to every elite std                                 */
+  uint64_t seed;
+  llampc_cost cost;                  /* Q, R, P, bounds; rate_max: the symmetric feasibility bound */
+  double rate_lo[2], rate_hi[2];     /* per-step rate bounds already x Ts (min_rates / max_rates x
+                                        Ts); rate_lo > rate_hi: none on that input             */
+} llampc_nlp_cfg;
+typedef struct llampc_nlp llampc_nlp;
+int llampc_nlp_create(llampc_bank* bank, const llampc_nlp_cfg* cfg, llampc_nlp** out);
+/* x0 [6], xref [2][H+1], uprev [2], base [H][2] (the first mean: the previous solution shifted,
+ * or NULL = uprev held); has_hold = 1 adds the held uprev as a candidate of the first round.
+ * -> umpc [H][2], fval, xmpc [H+1][6] (the Euler trajectory of umpc).  Blocking. */
+int llampc_nlp_solve(llampc_nlp* nlp, const double* x0, const double* xref, const double* uprev,
+                     const double* base, int32_t has_hold, double* umpc, double* fval, double* xmpc);
+int llampc_nlp_destroy(llampc_nlp* nlp);
 
 /* ---- raw batched dynamics (Dynamic API parity) ---------------------------------- */
 /* x [n][6], u [n][2]; params [6][P] with P == 1 (one model broadcast) or P == n.

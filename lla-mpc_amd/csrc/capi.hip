@@ -22,6 +22,7 @@
 
 #include "ctl.hpp"
 #include "kernels.hpp"
+#include "nlp.hpp"
 #include "merge.hpp"
 
 using namespace llampc;
@@ -97,7 +98,10 @@ CostK make_cost(const llampc_cost& c, double Ts) {
   for (int i = 0; i < 2; ++i) {
     k.umin[i] = c.umin[i];
     k.umax[i] = c.umax[i];
-    k.dmax[i] = c.rate_max[i] < 0 ? -1.0 : c.rate_max[i] * Ts;   // nmpc.py:104-105
+    // nmpc.py:104-105, tested with a relative tolerance of 1e-9: a sequence rate-clipped to the
+    // bound (u_k = u_{k-1} + rate Ts, the candidate samplers) can exceed it by one rounding
+    // of u_k - u_{k-1}; IPOPT itself accepts violations up to constr_viol_tol (1e-4)
+    k.dmax[i] = c.rate_max[i] < 0 ? -1.0 : c.rate_max[i] * Ts * (1.0 + 1e-9);
   }
   k.enforce = c.enforce_bounds;
   k.pad = 0;
@@ -1122,6 +1126,7 @@ int llampc_mailbox_destroy(llampc_mailbox* mb) {
 // Controller tick (ctl.hip): the control loop body rt.py:278-366 as ONE launch per step, the
 // controller state resident on the device between steps.
 // ------------------------------------------------------------------------------------
+static_assert(sizeof(llampc_nlp_cfg) == 16 + 8 + 16 + 8 + 8 + sizeof(llampc_cost) + 32, "llampc_nlp_cfg layout");
 static_assert(sizeof(llampc_ctl_cfg) == 280, "llampc_ctl_cfg layout (llampc/_native.py CtlCfg)");
 static_assert(sizeof(llampc_ctl_out) == sizeof(llampc_plan_out) + 56 + 16 * LLAMPC_HMAX, "llampc_ctl_out layout");
 
@@ -1455,6 +1460,158 @@ int llampc_ctl_inputs(llampc_ctl* c, double* xref, double* U) {
   const size_t nx = 2 * (size_t)(c->cfg.H + 1), nu = 2 * (size_t)c->cfg.C * c->cfg.H;
   HIP_TRY(hipMemcpy(xref, c->d_dbg, nx * sizeof(double), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(U, c->d_dbg + nx, nu * sizeof(double), hipMemcpyDeviceToHost));
+  return LLAMPC_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------
+// setupNLP.solve drop-in (nlp.hip): CEM iterations enqueued back to back on the bank's
+// stream, the Euler trajectory of the best sequence, one copy back.
+// ------------------------------------------------------------------------------------
+struct llampc_nlp {
+  llampc_bank* b = nullptr;
+  llampc_nlp_cfg cfg{};
+  // device block: NlpState | x0 [6] | xref [2][H+1] | traj [H+1][6] | h [H]  (one H2D, one D2H)
+  unsigned char* d_blk = nullptr;
+  unsigned char* h_blk = nullptr;        // pinned mirror
+  size_t blk_bytes = 0, in_bytes = 0;
+  double* d_cost = nullptr;              // [samples]
+  unsigned* d_ticket = nullptr;
+  uint64_t calls = 0;
+  std::mutex mu;
+};
+
+extern "C" {
+
+int llampc_nlp_destroy(llampc_nlp* p) {
+  if (!p) return LLAMPC_OK;
+  {
+    DeviceGuard g(p->b ? p->b->device : 0);
+    if (p->b && p->b->stream) (void)hipStreamSynchronize(p->b->stream);
+    if (p->d_blk) (void)hipFree(p->d_blk);
+    if (p->d_cost) (void)hipFree(p->d_cost);
+    if (p->d_ticket) (void)hipFree(p->d_ticket);
+    if (p->h_blk) (void)hipHostFree(p->h_blk);
+  }
+  delete p;
+  return LLAMPC_OK;
+}
+
+int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** out) {
+  if (!out) return fail(LLAMPC_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (!b || !cfg) return fail(LLAMPC_E_ARG, "NULL argument");
+  const llampc_nlp_cfg& k = *cfg;
+  if (b->n != 1) return fail(LLAMPC_E_ARG, "the NLP solver's bank holds one model (n=%lld)", (long long)b->n);
+  if (k.H < 1 || k.H > LLAMPC_HMAX) return fail(LLAMPC_E_ARG, "H=%d outside [1, %d]", k.H, LLAMPC_HMAX);
+  if (k.samples < 64 || k.samples > 4096 || (k.samples & (k.samples - 1)))
+    return fail(LLAMPC_E_ARG, "samples=%d: a power of two in [64, 4096]", k.samples);
+  if (k.elite < 1 || k.elite > k.samples || k.iters < 1)
+    return fail(LLAMPC_E_ARG, "elite=%d iters=%d", k.elite, k.iters);
+  if (!(k.Ts > 0) || !std::isfinite(k.Ts)) return fail(LLAMPC_E_ARG, "Ts must be finite > 0");
+  if (nlp_lds_bytes(k.H, k.samples, k.elite) > 160 * 1024) return fail(LLAMPC_E_ARG, "H x elite too large for LDS");
+  DeviceGuard g(b->device);
+  auto* p = new llampc_nlp();
+  p->b = b;
+  p->cfg = k;
+  const size_t H = (size_t)k.H;
+  p->in_bytes = sizeof(NlpState) + 8 * (6 + 2 * (H + 1));
+  p->blk_bytes = p->in_bytes + 8 * (6 * (H + 1) + H);
+  auto cleanup = [&](int code) {
+    llampc_nlp_destroy(p);
+    return code;
+  };
+  int rc;
+  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, (size_t)k.samples)) ||
+      (rc = dev_alloc(&p->d_ticket, 1)))
+    return cleanup(rc);
+  if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(NLP staging) failed"));
+  std::memset(p->h_blk, 0, p->blk_bytes);
+  double* hh = reinterpret_cast<double*>(p->h_blk + p->in_bytes) + 6 * (H + 1);   // h [H] = Ts
+  for (size_t i = 0; i < H; ++i) hh[i] = k.Ts;
+  if (hipMemcpy(p->d_blk, p->h_blk, p->blk_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(p->d_ticket, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return cleanup(fail(LLAMPC_E_HIP, "NLP solver upload failed"));
+  *out = p;
+  return LLAMPC_OK;
+}
+
+int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const double* uprev, const double* base,
+                     int32_t has_hold, double* umpc, double* fval, double* xmpc) {
+  if (!p || !x0 || !xref || !uprev || !umpc) return fail(LLAMPC_E_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lp(p->mu);
+  llampc_bank* b = p->b;
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding on the bank");
+  DeviceGuard g(b->device);
+  const llampc_nlp_cfg& k = p->cfg;
+  const int H = k.H;
+  hipStream_t s = b->stream;
+  // stage: the first mean (base or uprev held), the first std, best = +inf, x0, xref
+  NlpState* hs = reinterpret_cast<NlpState*>(p->h_blk);
+  for (int i = 0; i < H; ++i)
+    for (int j = 0; j < 2; ++j) {
+      hs->mean[i][j] = base ? base[2 * i + j] : uprev[j];
+      hs->std_[i][j] = k.sigma0[j];
+    }
+  hs->best_j = HUGE_VAL;
+  hs->best_it = -1;
+  double* hx = reinterpret_cast<double*>(p->h_blk + sizeof(NlpState));
+  std::memcpy(hx, x0, 6 * sizeof(double));
+  std::memcpy(hx + 6, xref, 2 * (size_t)(H + 1) * sizeof(double));
+  HIP_TRY(hipMemcpyAsync(p->d_blk, p->h_blk, p->in_bytes, hipMemcpyHostToDevice, s));
+  NlpState* ds = reinterpret_cast<NlpState*>(p->d_blk);
+  double* dx = reinterpret_cast<double*>(p->d_blk + sizeof(NlpState));
+  double* dtraj = reinterpret_cast<double*>(p->d_blk + p->in_bytes);
+  double* dh = dtraj + 6 * (H + 1);
+  NlpLaunch a{};
+  a.la.params = b->d_params;
+  a.la.n = 1;
+  a.la.veh = integrator_veh(b->veh, LLAMPC_EULER_NLP);
+  a.la.C = 64;
+  a.la.H = H;
+  a.la.integrator = LLAMPC_EULER_NLP;
+  a.la.Ts = k.Ts;
+  a.la.cost = make_cost(k.cost, k.Ts);
+  a.st = ds;
+  a.x0 = dx;
+  a.xref = dx + 6;
+  a.cost = p->d_cost;
+  a.ticket = p->d_ticket;
+  a.seed = k.seed;
+  a.call = p->calls;
+  a.up0 = uprev[0];
+  a.up1 = uprev[1];
+  a.umin0 = k.cost.umin[0];
+  a.umin1 = k.cost.umin[1];
+  a.umax0 = k.cost.umax[0];
+  a.umax1 = k.cost.umax[1];
+  a.rlo0 = k.rate_lo[0];
+  a.rlo1 = k.rate_lo[1];
+  a.rhi0 = k.rate_hi[0];
+  a.rhi1 = k.rate_hi[1];
+  a.std_floor = k.std_floor;
+  a.H = H;
+  a.samples = k.samples;
+  a.elite = k.elite;
+  a.has_hold = has_hold;
+  for (int it = 0; it < k.iters; ++it) {
+    a.it = it;
+    HIP_TRY(launch_nlp(a, s));
+  }
+  // xmpc: the NLP's Euler trajectory of the best sequence (nmpc.py:58-60)
+  HIP_TRY(launch_integrate(dx, &ds->best_u[0][0], 0, dh, H, b->d_params, 1, a.la.veh, 1, LLAMPC_EULER_NLP, dtraj, 0, s));
+  HIP_TRY(hipMemcpyAsync(p->h_blk, p->d_blk, p->blk_bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  p->calls++;
+  b->launches += k.iters;
+  for (int i = 0; i < H; ++i)
+    for (int j = 0; j < 2; ++j) umpc[2 * i + j] = hs->best_u[i][j];
+  if (fval) *fval = hs->best_j;
+  if (xmpc) std::memcpy(xmpc, reinterpret_cast<double*>(p->h_blk + p->in_bytes), 6 * (size_t)(H + 1) * sizeof(double));
+  if (hs->best_it < 0) return fail(LLAMPC_E_DEVICE, "no finite objective in %d rounds of %d samples", k.iters, k.samples);
   return LLAMPC_OK;
 }
 

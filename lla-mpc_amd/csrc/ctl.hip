@@ -283,7 +283,6 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   const int tid = threadIdx.x;
   const int H = c.la.H, C = c.la.C;
   const RacelineK rl = c.la.rl;
-  const int nseg = rl.n - 1;
   const CtlLds L = ctl_lds(H, C, rl.n);
   double* sx = reinterpret_cast<double*>(smem + L.sx);
   double* Ul = reinterpret_cast<double*>(smem + L.ul);

@@ -1,0 +1,43 @@
+// nlp.hpp — the setupNLP.solve drop-in's launch interface (nlp.hip; llampc_nlp_* in capi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ctl.hpp"
+#include "kernels.hpp"
+#include "llampc.h"
+
+namespace llampc {
+
+// The solver's device state (one per solver handle): the sampling distribution of the
+// current iteration and the best sequence so far.
+struct NlpState {
+  double mean[LLAMPC_HMAX][2];
+  double std_[LLAMPC_HMAX][2];
+  double best_u[LLAMPC_HMAX][2];
+  double best_j;                 // +inf until a finite objective is seen
+  int32_t best_it;
+  int32_t pad;
+};
+
+// One CEM iteration's launch.  Scalars only (no arrays): the kernel never takes the address of
+// its argument (which would copy it to scratch).
+struct NlpLaunch {
+  LookaheadLaunch la;            // params [6][1], veh (NLP form), cost, H, Ts, integrator EULER_NLP
+  NlpState* st;
+  const double* x0;              // [6] device
+  const double* xref;            // [2][H+1] device
+  double* cost;                  // [samples] the iteration's objectives
+  unsigned* ticket;
+  uint64_t seed, call;           // Philox key; counter word 1 = the solve call number
+  double up0, up1;               // uprev (du_0, nmpc.py:65-66)
+  double umin0, umin1, umax0, umax1;
+  double rlo0, rlo1, rhi0, rhi1; // per-step rate bounds (x Ts); lo > hi: none
+  double std_floor;
+  int32_t it, H, samples, elite, has_hold;
+};
+
+size_t nlp_lds_bytes(int H, int samples, int elite);
+hipError_t launch_nlp(const NlpLaunch& a, hipStream_t s);
+
+}  // namespace llampc

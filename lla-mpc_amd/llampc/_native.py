@@ -80,6 +80,13 @@ class CtlCfg(C.Structure):
                 ("nominal", C.c_double * 6), ("cost", Cost), ("debug_inputs", C.c_int32), ("reserved", C.c_int32)]
 
 
+class NlpCfg(C.Structure):
+    """llampc_nlp_cfg: the setupNLP.solve drop-in's cross-entropy search."""
+    _fields_ = [("H", C.c_int32), ("samples", C.c_int32), ("iters", C.c_int32), ("elite", C.c_int32),
+                ("Ts", C.c_double), ("sigma0", C.c_double * 2), ("std_floor", C.c_double), ("seed", C.c_uint64),
+                ("cost", Cost), ("rate_lo", C.c_double * 2), ("rate_hi", C.c_double * 2)]
+
+
 class CtlOut(C.Structure):
     """llampc_ctl_out: the tick record plus the controller's own fields."""
     _fields_ = [("plan", PlanOut), ("tick", C.c_int64), ("projidx", C.c_int32), ("warm", C.c_int32),
@@ -137,6 +144,9 @@ _SIGNATURES = {
     "llampc_ctl_reference": (C.c_int, [C.c_void_p, _dp, C.c_double, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                        _dp, C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
     "llampc_ctl_destroy": (C.c_int, [C.c_void_p]),
+    "llampc_nlp_create": (C.c_int, [C.c_void_p, C.POINTER(NlpCfg), C.POINTER(C.c_void_p)]),
+    "llampc_nlp_solve": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, C.c_int32, _dp, C.POINTER(C.c_double), _dp]),
+    "llampc_nlp_destroy": (C.c_int, [C.c_void_p]),
     "llampc_dynamics_batch": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                         C.POINTER(Vehicle), C.c_int64, C.c_void_p, C.c_int32,
                                         C.c_int32, C.c_void_p]),

@@ -1,22 +1,24 @@
-"""``setupNLP`` drop-in: the selected model's NMPC solved by sampling on the GPU.
+"""``setupNLP`` drop-in: the selected model's NMPC solved on the GPU by a cross-entropy search.
 
 The reference (llampc/mpc/nmpc.py:14-203) transcribes the problem for CasADi/IPOPT:
 states x[6, H+1] with x_{k+1} = x_k + Ts f_nlp(x_k, u_k) (dynamic.py:195-226 +
 nmpc.py:58-60), objective (x_H - xref_H)' P (.) + sum_k [(x_{k+1} - xref_{k+1})' Q (.) +
 du_k' R du_k], du_0 = u_0 - uprev (nmpc.py:44-111), bounds on u and on the steering rate
-(nmpc.py:102-105).  CasADi and IPOPT are not available on this platform (and IPOPT's
-optimum is not reproducible here: parity unpinned), so this ``solve()``
-keeps the interface and the problem but searches it by sampling: ``samples`` control
-sequences per round around the best so far (the warm start first: the previous solution
-shifted one step), every one rolled out with the NLP's own Euler transcription and scored
-with the NLP's objective by the look-ahead kernel (``ModelBank.lookahead``,
-integrator ``euler_nlp``, infeasible sequences cost +inf), ``iters`` rounds with the
-spread shrinking.  Every returned ``umpc`` satisfies the NLP's bounds and rate
-constraints; ``fval`` is the objective of ``umpc`` and ``xmpc`` its Euler trajectory —
-the same triple IPOPT's feasible point would give.
+(nmpc.py:102-105).  CasADi and IPOPT are not available on this platform (and IPOPT's optimum
+is not reproducible here: parity unpinned), so this ``solve()`` keeps the
+interface and the problem and minimises it on the device (llampc_nlp_solve, csrc/nlp.hip):
+``iters`` rounds of ``samples`` control sequences drawn around the current mean (the warm
+start first: the previous solution shifted one step; the held uprev is a candidate of the
+first round) with a per-(step, input) spread, clipped to the bounds and rate-clipped in order,
+every one rolled out with the NLP's own Euler transcription and scored with its objective
+(infeasible: +inf); the ``elite`` best set the next mean and spread (the cross-entropy
+method).  All rounds run back to back on the GPU with one copy back.  Every returned
+``umpc`` satisfies the NLP's bounds and rate constraints; ``fval`` is the objective of
+``umpc`` and ``xmpc`` its Euler trajectory — the same triple IPOPT's feasible point would give.
 
-``track_cons=True`` (rt.py:63 uses False) needs the track-boundary half-planes
-(constraints.py Boundary on the centre line), which are not packaged: it raises.
+``track_cons=True`` (rt.py:63 uses False everywhere) would add the track-boundary half-planes
+of constraints.py; the boundary lines are packaged (llampc.tracks) but the constraint is not
+implemented here (out of scope): it raises.
 """
 from __future__ import annotations
 
@@ -38,16 +40,15 @@ class setupNLP:
     """Same constructor and ``solve`` contract as nmpc.py:14-203 (see module doc)."""
 
     def __init__(self, horizon, Ts, Q, P, R, params, model, track, track_cons=False,
-                 samples=1024, iters=4, sigma=(0.08, 0.04), shrink=0.5, seed=0, device=0):
+                 samples=1024, iters=8, elite=32, sigma=(0.3, 0.15), std_floor=1e-4, seed=0, device=0):
         if track_cons:
-            raise NotImplementedError("track_cons=True needs the track boundary data "
-                                      "(constraints.py Boundary), which is not packaged")
+            raise NotImplementedError("track_cons=True (constraints.py boundary half-planes) is not "
+                                      "implemented: the reference's LLA-MPC runs use TRACK_CONS=False (rt.py:63)")
         self.horizon, self.Ts = int(horizon), float(Ts)
         self.params, self.model, self.track, self.track_cons = params, model, track, track_cons
-        self.samples, self.iters, self.shrink = int(samples), int(iters), float(shrink)
+        self.samples, self.iters, self.elite = int(samples), int(iters), int(elite)
         self.sigma = np.asarray(sigma, dtype=np.float64)
-        self.rng = np.random.RandomState(seed)
-        self.device = device
+        self.std_floor, self.seed, self.device = float(std_floor), int(seed), device
         self.umin = np.asarray(params["min_inputs"], dtype=np.float64)
         self.umax = np.asarray(params["max_inputs"], dtype=np.float64)
         # steering-rate bounds min_rates[1]*Ts <= d delta <= max_rates[1]*Ts (nmpc.py:104-105);
@@ -60,13 +61,14 @@ class setupNLP:
         self.cost = nat.cost_struct(Q=Q, R=R, P=P, umin=self.umin, umax=self.umax,
                                     rate_max=rate_max, enforce_bounds=True)
         self._bank = None
+        self._h = None
         self._dyn = None
         self._last = None            # previous umpc [H, 2] for the warm start
 
     # the device objects are created at the first solve(): rt.py builds one setupNLP per
     # bank model (rt.py:195-202) but solves with one of them per tick
     def _ensure(self):
-        if self._bank is not None:
+        if self._h is not None:
             return
         m = self.model
         p6 = np.array([[float(_attr(m, k))] for k in _PACEJKA])
@@ -76,58 +78,45 @@ class setupNLP:
             p6 = np.nan_to_num(p6)
         self._bank = ModelBank(p6, shared=shared, W=1, device=self.device,
                                input_acc=bool(_attr(m, "input_acc", False)), approx=approx)
-        from llampc.models import Dynamic
-        kw = dict(shared)
-        kw.update({k: (None if approx and k in ("Bf", "Br", "Df", "Dr") else float(p6[i, 0]))
-                   for i, k in enumerate(_PACEJKA)})
-        self._dyn = Dynamic(**kw, input_acc=bool(_attr(m, "input_acc", False)), device=self.device)
-
-    def _sample(self, base, uprev, sigma, extra):
-        """``samples`` sequences [C, H, 2] around ``base`` [H, 2] (row 0 = base itself, then
-        ``extra`` rows), clipped to the input bounds, then to the rate bounds in order."""
-        C, H = self.samples, self.horizon
-        U = np.repeat(base[None], C, axis=0)
-        k = 1 + len(extra)
-        for j, e in enumerate(extra):
-            U[1 + j] = e
-        if C > k:
-            U[k:] += self.rng.randn(C - k, H, 2) * sigma
-        U = np.clip(U, self.umin, self.umax)
+        cfg = nat.NlpCfg()
+        cfg.H, cfg.samples, cfg.iters, cfg.elite = self.horizon, self.samples, self.iters, self.elite
+        cfg.Ts, cfg.std_floor, cfg.seed = self.Ts, self.std_floor, self.seed
+        cfg.sigma0[0], cfg.sigma0[1] = float(self.sigma[0]), float(self.sigma[1])
+        cfg.cost = self.cost
         for j, (lo, hi) in enumerate(self.rate):
-            if lo is None:
-                continue
-            prev = np.full(C, float(uprev[j]))
-            for h in range(H):
-                U[:, h, j] = np.clip(U[:, h, j], prev + lo, prev + hi)
-                prev = U[:, h, j]
-        return np.ascontiguousarray(U)
+            cfg.rate_lo[j], cfg.rate_hi[j] = (1.0, -1.0) if lo is None else (lo, hi)
+        h = nat.C.c_void_p()
+        nat.check(nat.load().llampc_nlp_create(self._bank.handle, nat.C.byref(cfg), nat.C.byref(h)))
+        self._h = h
+        self.cfg = cfg
 
     def solve(self, x0, xref, uprev):
         """-> (umpc [2, H], fval, xmpc [6, H+1], violation in {0, 0.02}) as nmpc.py:161-203."""
         self._ensure()
         H = self.horizon
-        x0 = np.asarray(x0, dtype=np.float64).ravel()
+        x0 = nat.f64(np.asarray(x0, dtype=np.float64).ravel())
         xref = np.ascontiguousarray(np.asarray(xref, dtype=np.float64)[:2, :H + 1])
-        uprev = np.asarray(uprev, dtype=np.float64).ravel()
-        hold = np.tile(uprev, (H, 1))
-        base = hold if self._last is None else np.concatenate([self._last[1:], self._last[-1:]])
-        best_U, best_J = None, np.inf
-        sigma = self.sigma.copy()
-        for it in range(self.iters):
-            extra = [hold] if it == 0 and self._last is not None else []
-            U = self._sample(base, uprev, sigma, extra)
-            r = self._bank.lookahead(x0, U, xref, uprev, Ts=self.Ts, cost=self.cost, integrator="euler_nlp")
-            c, J = r["best_cand"], r["best_cost"]
-            if best_U is None or J < best_J:
-                best_U, best_J = U[c].copy(), J
-            base = best_U
-            sigma = sigma * self.shrink
-        traj = self._dyn._native_integrate(x0[None], best_U[None], np.full(H, self.Ts), nat.EULER_NLP,
-                                           final_only=False)
-        self._last = best_U
-        return best_U.T.copy(), float(best_J), traj[:, 0, :].T.copy(), 0.0
+        uprev = nat.f64(np.asarray(uprev, dtype=np.float64).ravel())
+        base = None if self._last is None else np.ascontiguousarray(np.concatenate([self._last[1:], self._last[-1:]]))
+        umpc = np.empty((H, 2))
+        xmpc = np.empty((H + 1, 6))
+        fval = nat.C.c_double()
+        nat.check(nat.load().llampc_nlp_solve(self._h, nat.dptr(x0), nat.dptr(xref), nat.dptr(uprev), nat.dptr(base),
+                                               int(self._last is not None), nat.dptr(umpc), nat.C.byref(fval),
+                                               nat.dptr(xmpc)))
+        self._last = umpc
+        return umpc.T.copy(), float(fval.value), xmpc.T.copy(), 0.0
 
     def close(self):
+        if self._h is not None:
+            nat.load().llampc_nlp_destroy(self._h)
+            self._h = None
         if self._bank is not None:
             self._bank.close()
             self._bank = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -158,8 +158,13 @@ class ShardedBank:
                 self._setup_peer_exchange(dev, required=mode == "peer")
             if self._mailbox is None and self.backend == "nccl" and mode in ("auto", "rccl"):
                 self._setup_native_exchange(dev)
-            self.transport = ("peer" if self._mailbox is not None else "rccl" if self._comm is not None
-                              else "c10d" if self.backend == "nccl" else "host")
+            self.transport = self._decide_transport()
+
+    def _decide_transport(self) -> str:
+        """The exchange the ticks use, from what the collective setup left: the peer mailboxes,
+        else the native RCCL all-gather, else c10d's (nccl), else the host gather (gloo)."""
+        return ("peer" if self._mailbox is not None else "rccl" if self._comm is not None
+                else "c10d" if self.backend == "nccl" else "host")
 
     def _setup_peer_exchange(self, dev, required=False):
         """Map every rank's mailbox (collective: all ranks take the same decision)."""
@@ -275,19 +280,30 @@ class ShardedBank:
         self._nan_policy = nan_policy
         return pin
 
-    def launch(self, pin: nat.PlanIn, stream=None):
+    def launch(self, pin: nat.PlanIn, stream=None, exchange_events=None):
         """Enqueue one tick on ``tick_stream(stream)``: fused plan on this shard, then (world
         > 1) ONE all-gather of the shard records and the on-device merge, all stream-ordered.
-        The merged record is left in ``self.d_merged``; nothing synchronises."""
+        The merged record is left in ``self.d_merged``; nothing synchronises.
+        exchange_events = (start, stop) torch events: this tick runs the exchange as its own
+        kernel(s) after the plan launch (the peer transport's split form, llampc_plan_device +
+        llampc_exchange_peer: the same protocol and tick number as the fused launch) and the
+        events bracket the exchange alone — the bench's per-tick split of plan and exchange."""
         torch = self._torch
         s = self.tick_stream(stream)
         lib = nat.load()
-        if self._mailbox is not None:        # peer: the plan launch pushes, polls and merges
+        if self._mailbox is not None and exchange_events is None:   # peer: the plan launch pushes, polls, merges
             nat.check(lib.llampc_plan_exchange(self.bank.handle, C.byref(pin), self.d_local.data_ptr(),
                                                self.d_merged.data_ptr(), self._mailbox, s.cuda_stream))
             return s
         nat.check(lib.llampc_plan_device(self.bank.handle, C.byref(pin), self.d_local.data_ptr(),
                                          None, None, None, s.cuda_stream))
+        if exchange_events is not None and self.exchange:
+            exchange_events[0].record(s)
+        if self._mailbox is not None:
+            nat.check(lib.llampc_exchange_peer(self._mailbox, self.d_local.data_ptr(), self.d_merged.data_ptr(),
+                                               pin.nan_policy, s.cuda_stream))
+            exchange_events[1].record(s)
+            return s
         if self._comm is not None:           # native: all-gather + merge on stream s
             nat.check(lib.llampc_exchange_device(self.d_local.data_ptr(), self.d_all.data_ptr(), self.world,
                                                  self.d_merged.data_ptr(), pin.nan_policy, self._comm,
@@ -305,6 +321,8 @@ class ShardedBank:
                     self.d_all.copy_(torch.cat(parts).to(self.d_all.device), non_blocking=False)
             nat.check(lib.llampc_merge_device(self.d_all.data_ptr(), self.world, pin.nan_policy,
                                               self.d_merged.data_ptr(), self.device, s.cuda_stream))
+        if exchange_events is not None and self.exchange:
+            exchange_events[1].record(s)
         return s
 
     def plan_device(self, staged: dict, stream=None, **kw):

@@ -566,6 +566,42 @@ def test_baseline_sizes_properties(nat, N, H, track):
         assert res.global_best[0] == int(np.argmin(np.where(np.isnan(cref), np.inf, cref)))
 
 
+def test_c64_work_queue_full_size_vs_oracle(nat):
+    """The bench's C = 64 throughput shape at full size — N = 10^4, C = 64, H = 20, where
+    launch_plan takes the 8-wave work-queue layout (10^4 units >= 4 per wave slot of 255
+    CUs) — against the oracle: all 640,000 (model, candidate) costs at 1e-7, the selected and
+    top-K models' best candidates and the global argmin exact, the look-back selection exact."""
+    from llampc.mpc import CandidateGenerator, ModelBank, generate_bank, plan
+    from llampc.mpc.planner import ConstantSpeed
+    from llampc.tracks import ETHZ
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    tr = ETHZ('optimal', True)
+    N, C, H, W, K = 10000, 64, 20, 10, 10
+    p = generate_bank(N, seed=0)
+    gen = CandidateGenerator(C, H, seed=2)
+    win = O.LookbackWindow(N, W, K)
+    with ModelBank(p, W=W, device=0) as b:
+        for t in range(1, W + 2):
+            x_t = s[:, t]
+            xref, _, _ = ConstantSpeed(x_t[:2], x_t[3], tr, H, TS, 0, curr_mu=0.9, scale=0.9)
+            U = gen(None, u[:, t])
+            res = plan(b, x_t, u[:, t - 1], s[:, t - 1], xref, U, Ts=TS, K=K, return_costs=(t == W + 1))
+            win.push(O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(p), s[:, t - 1], u[:, t - 1], TS),
+                                       x_t))
+    assert res.window_full and res.best_model == win.current
+    np.testing.assert_array_equal(res.topk, win.best_k)
+    traj = O.rollout_rk4(shared(), tuple(p), s[:, W + 1], U, TS)
+    cref = O.mpc_cost(traj, U, xref, u[:, W], np.eye(2), np.diag([5e-3, 1]), np.zeros((2, 2)))
+    del traj
+    close(res.costs.ravel(), cref, RTOL_ROLL)
+    cm = np.where(np.isnan(cref), np.inf, cref).reshape(N, C)
+    assert res.best_cand == int(np.argmin(cm[win.current]))
+    np.testing.assert_array_equal(res.raw.topk_cand[:K], [int(np.argmin(cm[m])) for m in win.best_k])
+    g = int(np.argmin(cm.ravel()))
+    assert res.global_best[:2] == (g // C, g % C)
+
+
 # ----------------------------------------------------------------- model transcendentals
 def _math(nat, fn, a, b=None):
     a = np.ascontiguousarray(a, dtype=np.float64)
@@ -1106,6 +1142,56 @@ def test_setupnlp_solve_sampling(nat):
         xn, _ = O.sim_continuous(O.Vehicle.from_params(O.orca_params()), x0, umpc[:, :1], [0, Ts])
         x0, uprev = xn[:, -1], umpc[:, 0].copy()
     nlp.close()
+
+
+def _nlp(H=20):
+    from llampc.models import Dynamic
+    from llampc.mpc.nmpc import setupNLP
+    from llampc.params import ORCA
+    from llampc.tracks import ETHZ
+    p = ORCA(control="pwm")
+    return setupNLP(H, TS, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, Dynamic(**p), ETHZ('optimal', True)), p
+
+
+def test_setupnlp_cem_equals_oracle(nat):
+    """The device cross-entropy search (csrc/nlp.hip) against its NumPy restatement
+    (oracle.nlp_cem) over three successive solves (warm start, the held uprev in the first
+    round): the same sequence (the samples are bitwise the oracle's; the elite ranking follows
+    costs equal to 1e-7) and fval at 1e-7."""
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    nlp, p = _nlp()
+    p6 = [p[k] for k in O.BANK_ORDER]
+    try:
+        from llampc.mpc.planner import ConstantSpeed
+        from llampc.tracks import ETHZ
+        tr = ETHZ('optimal', True)
+        last = None
+        for call, t in enumerate((10, 11, 12)):
+            x0, up = s[:, t].copy(), u[:, t - 1].copy()
+            xref, _, _ = ConstantSpeed(x0[:2], x0[3], tr, 20, TS, 0)
+            umpc, fval, xmpc, _ = nlp.solve(x0, xref, up)
+            base = None if last is None else np.concatenate([last[1:], last[-1:]])
+            uo, jo = O.nlp_cem(shared(), p6, x0, xref, up, base, last is not None, 20, TS, call=call)
+            np.testing.assert_array_equal(umpc.T, uo)
+            np.testing.assert_allclose(fval, jo, rtol=RTOL_ROLL)
+            last = umpc.T.copy()
+    finally:
+        nlp.close()
+
+
+def test_setupnlp_within_5pct_of_local_optimum(nat):
+    """Solution quality of the setupNLP drop-in: on three DYN-slice ticks its fval is within
+    5 % of a local optimum of the same restated NLP found by scipy's SLSQP
+    (tests/golden/nlp_optimum.npz, gen_nlp_optimum.py).  IPOPT's own optimum stays unpinned."""
+    g = golden("nlp_optimum.npz")
+    for i in range(len(g["fstar"])):
+        nlp, _ = _nlp()
+        try:
+            umpc, fval, _, _ = nlp.solve(g["x0"][i], g["xref"][i], g["uprev"][i])
+        finally:
+            nlp.close()
+        assert fval <= 1.05 * g["fstar"][i], (int(g["tick"][i]), fval, g["fstar"][i])
 
 
 @pytest.mark.parametrize("track_name,start", [("ETHZ", "projected"), ("ETHZ", "lap_end"), ("ETHZMobil", "projected")])

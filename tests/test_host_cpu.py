@@ -438,3 +438,55 @@ def test_bench_spawn_ranks_environment_and_failure():
         t0 = time.time()
         assert bench.spawn_ranks(3, [sys.executable, "-c", fail]) == 3
         assert time.time() - t0 < 30            # the sleeping ranks were stopped, not waited for
+
+
+def test_native_exchange_fallback_reported(monkeypatch):
+    """The RCCL path's private pieces fail (ProcessGroupNCCL._comm_ptr() missing, or no RCCL in
+    /proc/self/maps): ShardedBank keeps the c10d all-gather, reports transport 'c10d' and says
+    why in transport_fallback (the bench line carries both)."""
+    import torch
+    import torch.distributed as dist
+    from llampc import _native as nat
+    from llampc.mpc import sharded
+
+    class Backend:                                 # a backend without _comm_ptr
+        pass
+
+    class Group:
+        def _get_backend(self, dev):
+            return Backend()
+
+    monkeypatch.setattr(dist, "new_group", lambda **kw: Group())
+    monkeypatch.setattr(dist, "all_gather_into_tensor", lambda *a, **kw: None)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **kw: None)
+
+    def fresh(fallback=None):
+        sb = sharded.ShardedBank.__new__(sharded.ShardedBank)
+        sb._mailbox, sb._comm, sb.backend = None, None, "nccl"
+        sb.fallback_reason = fallback
+        sb.d_all = sb.d_local = None
+        return sb
+
+    sb = fresh("peer: IPC unavailable")
+    sb._setup_native_exchange("cpu")
+    assert sb._comm is None and sb._decide_transport() == "c10d"
+    assert sb.fallback_reason.startswith("peer: IPC unavailable; rccl: ") and "_comm_ptr" in sb.fallback_reason
+
+    class Backend2:
+        def _comm_ptr(self):
+            return 1234
+
+    Group._get_backend = lambda self, dev: Backend2()
+    monkeypatch.setattr(sharded, "_rccl_allgather_addr",
+                        lambda: (_ for _ in ()).throw(nat.NativeError("no RCCL library loaded in this process")))
+    sb = fresh()
+    sb._setup_native_exchange("cpu")
+    assert sb._decide_transport() == "c10d" and sb.fallback_reason == "rccl: no RCCL library loaded in this process"
+    # both present: the native path, nothing to report
+    monkeypatch.setattr(sharded, "_rccl_allgather_addr", lambda: 99)
+    sb = fresh()
+    sb._setup_native_exchange("cpu")
+    assert sb._decide_transport() == "rccl" and sb.fallback_reason is None and sb._allgather == 99
+    sb.backend = "gloo"
+    sb._comm = None
+    assert sb._decide_transport() == "host"
