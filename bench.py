@@ -605,6 +605,7 @@ def extras(args, sb, stream, world, rank=0):
         out["config5"] = concurrent_tracks(args)
         out["config3"] = config3(args)
         out["controller_tick_us"] = controller_ticks(args)
+        out["solve_us"] = solve_latency(args)
     else:
         out["config5"] = concurrent_tracks_sharded(args, world, rank, sb.device)
     return out
@@ -829,6 +830,46 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
             "note": "LLAMPC.tick (device mode, llampc_ctl_tick_async/wait: one launch per track per step) for "
                     "two tracks concurrently, paced at 1 ms; kernel_us_avg = per-launch HIP events of each "
                     "bank's controller launch (these ticks carry the event pairs)"}
+
+
+def solve_latency(args, n=200, warm=10, H=20):
+    """The setupNLP.solve drop-in (llampc_nlp_solve: the selected model's NMPC, nmpc.py:161-203,
+    minimised on the device by the cross-entropy search — 1,024 samples x 8 rounds, elite 32 —
+    with ONE copy back) called from Python per control step on successive DYN-slice states,
+    p50/p99/max; the reference's published figure for its whole control step with IPOPT is
+    0.03 s (results/table1.png)."""
+    from llampc.models import Dynamic
+    from llampc.mpc.nmpc import setupNLP
+    from llampc.mpc.planner import ConstantSpeed
+    from llampc.params import ORCA
+    from llampc.tracks import ETHZ
+    d = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))
+    s, u = d["states"], d["inputs"]
+    tr = ETHZ('optimal', True)
+    p = ORCA(control="pwm")
+    nlp = setupNLP(H, 0.02, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, Dynamic(**p, device=torch_device_index()),
+                   tr, device=torch_device_index())
+    cases, projidx = [], 0
+    for t in range(10, 10 + 40):
+        xref, projidx, _ = ConstantSpeed(s[:2, t], s[3, t], tr, H, 0.02, projidx)
+        cases.append((s[:, t].copy(), xref, u[:, t - 1].copy()))
+    lat, fv = [], []
+    try:
+        for i in range(n + warm):
+            x0, xref, up = cases[i % len(cases)]
+            t0 = time.perf_counter()
+            _, fval, _, _ = nlp.solve(x0, xref, up)
+            lat.append(time.perf_counter() - t0)
+            fv.append(fval)
+    finally:
+        nlp.close()
+    q = pctl(np.array(lat[warm:]) * 1e6)
+    return {"p50": q["p50"], "p99": q["p99"], "max": q["max"], "solves": q["ticks"], "H": H,
+            "samples": nlp.samples, "rounds": nlp.iters, "elite": nlp.elite,
+            "reference_s_per_control_step": 0.03, "fval_p50": float(np.median(fv)),
+            "note": "setupNLP(...).solve from Python: the CEM rounds back to back on the GPU + the Euler "
+                    "trajectory + one copy back; the reference's 0.03 s is its whole tick incl. IPOPT "
+                    "(unstated hardware)"}
 
 
 def issue_roofline(n, C, H, lpm, ms):

@@ -1,7 +1,9 @@
 """Diagnostic (build-time): VALU+SALU instructions per H-step of the fast look-ahead rollout
-loop for each lane split (LPM 1/2/4) of plan_kernel<RK4, staged, LPM, xref shared>, from a
-hipcc -S listing.  bench.py's ISSUE_INSTR_PER_STEP holds these numbers.
+loop for each lane split (LPM 1/2/4) of plan_kernel<RK4, staged, LPM, xref shared> and of the
+controller tick's ctl_kernel<LPM> (unstaged, candidates in LDS), from hipcc -S listings of the
+translation units that hold them.  bench.py's ISSUE_INSTR_PER_STEP holds the plan numbers.
 usage: python tools/diag/isa_counts.py"""
+import collections
 import os
 import re
 import subprocess
@@ -9,15 +11,18 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 tmp = tempfile.mkdtemp()
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm",
-                "-disable-machine-licm", f"-I{REPO}/include", f"-I{REPO}/lla-mpc_amd/csrc", "-c",
-                f"{REPO}/lla-mpc_amd/csrc/kernels.hip", "-save-temps", "-o", f"{tmp}/k.o"],
-               cwd=tmp, check=True, stderr=subprocess.DEVNULL)
-asm = open(f"{tmp}/kernels-hip-amdgcn-amd-amdhsa-gfx950.s").read().split("\n")
-# (lpm, work-queue layout): the headline C = 1 kernel is LPM 4; C >= 64 runs LPM 1 in the
-# work-queue layout (last template flag WQ = 1)
-for lpm, wq in ((4, 0), (2, 0), (1, 0), (1, 1)):
-    s = next(i for i, l in enumerate(asm) if re.match(rf"^_ZN6llampc11plan_kernelILi0ELb1ELi{lpm}ELi0ELb0ELb{wq}E\S+:", l))
+
+
+def listing(tu):
+    out = f"{tmp}/{tu}.s"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm",
+                    "-disable-machine-licm", f"-I{REPO}/include", f"-I{REPO}/lla-mpc_amd/csrc", "--cuda-device-only",
+                    "-S", f"{REPO}/lla-mpc_amd/csrc/{tu}.hip", "-o", out], cwd=tmp, check=True, stderr=subprocess.DEVNULL)
+    return open(out).read().split("\n")
+
+
+def loop_of(asm, pattern):
+    s = next(i for i, l in enumerate(asm) if re.match(pattern, l))
     e = next(i for i in range(s, len(asm)) if "s_endpgm" in asm[i])
     body = asm[s:e]
     labels = {m.group(1): i for i, l in enumerate(body) if (m := re.match(r"^(\.LBB\d+_\d+):", l))}
@@ -27,6 +32,32 @@ for lpm, wq in ((4, 0), (2, 0), (1, 0), (1, 1)):
         if m and m.group(1) in labels and labels[m.group(1)] < i:
             seg = body[labels[m.group(1)]:i + 1]
             n = sum(1 for x in seg if re.match(r"^\s+(v_|s_)", x))
-            if any("v_rcp_f64" in x for x in seg) and 200 < n < 1500 and (best is None or n < best):
-                best = n
-    print(f"LPM {lpm}{' work queue' if wq else ''}: {best} instructions per rollout step")
+            f = sum(1 for x in seg if re.match(r"^\s+v_\w+_f64", x))
+            # the rollout step: the innermost loop with the division and most fp64 work
+            if any("v_rcp_f64" in x for x in seg) and 200 < n < 2000 and f > 150 and (best is None or n < best[0]):
+                best = (n, seg)
+    return best
+
+
+def report(name, best):
+    if best is None:
+        print(f"{name}: no rollout loop found")
+        return
+    n, seg = best
+    ops = collections.Counter(re.match(r"^\s+(\S+)", x).group(1) for x in seg if re.match(r"^\s+(v_|s_|ds_|global_|flat_|buffer_|scratch_)", x))
+    fp64 = sum(v for k, v in ops.items() if k.endswith("_f64"))
+    spill = sum(v for k, v in ops.items() if k.startswith(("v_readlane", "v_writelane", "scratch_")))
+    mem = sum(v for k, v in ops.items() if k.startswith(("ds_", "global_", "flat_", "buffer_")))
+    print(f"{name}: {n} VALU+SALU per step (fp64 {fp64}, lane moves/spill {spill}, memory {mem})")
+
+
+asm4 = listing("plan_rk4_l4")
+report("plan LPM 4 (staged)", loop_of(asm4, r"^_ZN6llampc11plan_kernelILi0ELb1ELi4ELi0ELb0ELi0E\S+:"))
+asm2 = listing("plan_rk4_l2")
+report("plan LPM 2 (staged)", loop_of(asm2, r"^_ZN6llampc11plan_kernelILi0ELb1ELi2ELi0ELb0ELi0E\S+:"))
+asm1 = listing("plan_rk4_l1")
+report("plan LPM 1 (staged)", loop_of(asm1, r"^_ZN6llampc11plan_kernelILi0ELb1ELi1ELi0ELb0ELi0E\S+:"))
+report("plan LPM 1 (work queue, 8 waves)", loop_of(asm1, r"^_ZN6llampc11plan_kernelILi0ELb1ELi1ELi0ELb0ELi2E\S+:"))
+asmc = listing("ctl")
+for lpm in (4, 2, 1):
+    report(f"ctl LPM {lpm} (candidates in LDS)", loop_of(asmc, rf"^_ZN6llampc10ctl_kernelILi{lpm}EEEvNS_9CtlLaunchE:"))
