@@ -791,7 +791,7 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
         else:
             x = np.array([tr.x_init, tr.y_init, tr.psi_init, 1.0, 0.0, 0.0])
         setups.append([b, ctl, plant, x])
-    lat, kern = [], []
+    lat, kern, split = [], [], []
     lib = nat.load()
     try:
         nxt = time.perf_counter() + period
@@ -803,8 +803,11 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
             t0 = time.perf_counter()
             for s in setups:
                 s[1].tick_begin(s[3])
+            t1 = time.perf_counter()
             res = [s[1].tick_end() for s in setups]
-            lat.append(time.perf_counter() - t0)
+            t2 = time.perf_counter()
+            lat.append(t2 - t0)
+            split.append((t1 - t0, t2 - t1))
             for s, r in zip(setups, res):     # the plant (outside the timed step)
                 pl = s[2]
                 pl.Df -= pl.Df / 2600.
@@ -827,6 +830,8 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
             "budget_us": 1000.0, "met": q["p99"] < 1000.0, "tracks": ["ETHZ", "ETHZMobil"],
             "N_per_track": args.n_per_gpu, "H": H, "C": C, "K": args.K, "W": args.W,
             "kernel_us_avg": kern, "sel_models": sel, "projidx": laps,
+            "host_split_us_p50": {"begin": float(np.median([a for a, _ in split[warm:]]) * 1e6),
+                                  "end": float(np.median([b for _, b in split[warm:]]) * 1e6)},
             "note": "LLAMPC.tick (device mode, llampc_ctl_tick_async/wait: one launch per track per step) for "
                     "two tracks concurrently, paced at 1 ms; kernel_us_avg = per-launch HIP events of each "
                     "bank's controller launch (these ticks carry the event pairs)"}

@@ -360,7 +360,7 @@ int llampc_ctl_destroy(llampc_ctl* ctl);
  * and std.  Replaces nlpsol/IPOPT (nmpc.py:146-157, 192), which this platform lacks: the
  * optimum is NOT IPOPT's (parity unpinned).  The bank holds the ONE model (n = 1). */
 typedef struct llampc_nlp_cfg {
-  int32_t H, samples, iters, elite;  /* samples: power of two in [64, 4096]; 1 <= elite <= samples */
+  int32_t H, samples, iters, elite;  /* samples: power of two in [64, 4096]; 1 <= elite <= 64      */
   double Ts;
   double sigma0[2];                  /* the first iteration's std per input                     */
   double std_floor;                  /* added to every elite std                                 */

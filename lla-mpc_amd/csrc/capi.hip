@@ -1476,7 +1476,7 @@ struct llampc_nlp {
   unsigned char* d_blk = nullptr;
   unsigned char* h_blk = nullptr;        // pinned mirror
   size_t blk_bytes = 0, in_bytes = 0;
-  double* d_cost = nullptr;              // [samples]
+  double* d_cost = nullptr;              // the sample blocks' sorted lists (keys, then indices)
   unsigned* d_ticket = nullptr;
   uint64_t calls = 0;
   std::mutex mu;
@@ -1507,8 +1507,8 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
   if (k.H < 1 || k.H > LLAMPC_HMAX) return fail(LLAMPC_E_ARG, "H=%d outside [1, %d]", k.H, LLAMPC_HMAX);
   if (k.samples < 64 || k.samples > 4096 || (k.samples & (k.samples - 1)))
     return fail(LLAMPC_E_ARG, "samples=%d: a power of two in [64, 4096]", k.samples);
-  if (k.elite < 1 || k.elite > k.samples || k.iters < 1)
-    return fail(LLAMPC_E_ARG, "elite=%d iters=%d", k.elite, k.iters);
+  if (k.elite < 1 || k.elite > 64 || k.elite > k.samples || k.iters < 1)
+    return fail(LLAMPC_E_ARG, "elite=%d (1..64, <= samples) iters=%d", k.elite, k.iters);
   if (!(k.Ts > 0) || !std::isfinite(k.Ts)) return fail(LLAMPC_E_ARG, "Ts must be finite > 0");
   if (nlp_lds_bytes(k.H, k.samples, k.elite) > 160 * 1024) return fail(LLAMPC_E_ARG, "H x elite too large for LDS");
   DeviceGuard g(b->device);
@@ -1523,7 +1523,7 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
     return code;
   };
   int rc;
-  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, (size_t)k.samples)) ||
+  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, 2 * (size_t)k.samples)) ||
       (rc = dev_alloc(&p->d_ticket, 1)))
     return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
@@ -1578,7 +1578,8 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.st = ds;
   a.x0 = dx;
   a.xref = dx + 6;
-  a.cost = p->d_cost;
+  a.top_key = reinterpret_cast<uint64_t*>(p->d_cost);
+  a.top_idx = reinterpret_cast<uint32_t*>(a.top_key + (size_t)(k.samples / 64) * nlp_list_len(k.elite));
   a.ticket = p->d_ticket;
   a.seed = k.seed;
   a.call = p->calls;

@@ -27,11 +27,12 @@
 namespace llampc {
 
 // LDS layout of the controller launch (byte offsets; 16-B aligned regions).  Look-ahead
-// blocks: xref [H+1][2] | U [C][H][2] | knots [n + pad] | x/y rows [2][4][n-1] | the two
-// bracketing speed profiles [2][4][n-1] | misc.  The completing block: lb_final's region from
-// kScratchBytes, then its own area at poll_off (CtlPollLds).
+// blocks: xref [H+1][2] | U [C][H][2] | knots [n + pad] | the two speed profiles bracketing mu
+// interleaved per segment [n-1][2][4] (a, b, c, d of lo, then of hi: one segment's values are
+// four 16-B reads) | misc.  The completing block: lb_final's region from kScratchBytes (then
+// the candidates [C][H][2]), its own area at poll_off (CtlPollLds).
 struct CtlLds {
-  size_t sx, ul, kn, xy, spd, misc, end;
+  size_t sx, ul, kn, spd, misc, end;
 };
 __host__ __device__ __forceinline__ size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n) {
@@ -43,8 +44,6 @@ __host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n) {
   o = align16(o + 16 * (size_t)C * H);
   L.kn = o;
   o = align16(o + 8 * (size_t)(n + kKnotPad));
-  L.xy = o;
-  o = align16(o + 64 * (size_t)(n - 1));
   L.spd = o;
   o = align16(o + 64 * (size_t)(n - 1));
   L.misc = o;
@@ -52,6 +51,25 @@ __host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n) {
   return L;
 }
 constexpr size_t kCtlPollBytes = 4096;   // ctl_complete's area (layout there)
+
+#ifdef LLAMPC_STAMPS
+// Diagnostic build only: s_memrealtime (100 MHz) per block and phase of the last launch
+// (tools/diag/ctl_phases.py).  Look-ahead blocks: 0 entry, 1 staged, 10 walk done, 2 walk
+// barrier, 3 selection, 4 rolled out, 5 published; look-back blocks: 0 entry, 6 scored,
+// 7 lb_final done (ticket winner), 8 slots polled, 9 record written.
+static __device__ unsigned long long g_ctl_ph[64][12];
+#define CTL_STAMP(blk, slot)                                                                   \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && (blk) < 64) g_ctl_ph[blk][slot] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+extern "C" int llampc_debug_ctl_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ctl_ph), sizeof(g_ctl_ph)) == hipSuccess ? 0 : -2;
+}
+#else
+#define CTL_STAMP(blk, slot) \
+  do {                       \
+  } while (0)
+#endif
 
 namespace {
 
@@ -71,15 +89,67 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   double* pcost = reinterpret_cast<double*>(pl + 128);            // [kCtlSlotsMax]
   int32_t* pcand = reinterpret_cast<int32_t*>(pl + 448);          // [kCtlSlotsMax]
   int32_t* pnf = reinterpret_cast<int32_t*>(pl + 608);            // [kCtlSlotsMax]
-  double* praw = reinterpret_cast<double*>(pl + 768);             // [HMAX][2]
-  int32_t* pmisc = reinterpret_cast<int32_t*>(pl + 1792);         // sel_cand, pj, late
+  double* pmu = reinterpret_cast<double*>(pl + 768);              // dr, df, mu_pred, mu_used
+  int32_t* pmisc = reinterpret_cast<int32_t*>(pl + 1792);         // projidx
+  double* cu = reinterpret_cast<double*>(smem + kScratchBytes);   // [C][H][2] (lb_final's region, dead)
   unsigned char* late_w = smem + kLateOff;
   CtlState* st = c.st;
+  const bool warm = c.warm != 0;
+  // Before the poll (the look-ahead blocks' rollouts take most of the launch) everything that
+  // does not need their results: the projection, mu-hat and every candidate after its rate
+  // clip (the look-ahead blocks' generator), so the chosen sequence is a copy after the poll.
+  // The state is only read here; it is written after the poll, when no block reads it.
   const int p0 = st->projidx;
   const int segs = ctl_segments(p0, c.np);
   if (tid < kCtlSegs && tid < segs)                                // track.py:155-157
     pdist[tid] = ref_project_dist(c.x_t[0], c.x_t[1], c.pts[p0 + tid], c.pts[c.np + p0 + tid],
                                   c.pts[p0 + tid + 1], c.pts[c.np + p0 + tid + 1]);
+  const double up0 = st->u_prev[0], up1 = st->u_prev[1];
+  {
+    const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
+    for (int e = tid; e < 2 * C * H; e += kBlock) {
+      const int cc = e / (2 * H), r = e - cc * 2 * H, j = r & 1;
+      cu[e] = ctl_cand_raw(cc, r >> 1, j, H, prev_seq, j ? up1 : up0, j ? c.nscale[1] : c.nscale[0],
+                           j ? c.umin[1] : c.umin[0], j ? c.umax[1] : c.umax[0], c.tick, c.seed, 0);
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < 2 * C; t += kBlock) {
+    const int j = t & 1;
+    ctl_rate_chain(cu + 2 * (size_t)(t >> 1) * H + j, H, j ? up1 : up0, j ? c.rate[1] : c.rate[0]);
+  }
+  if (tid == kBlock - 1) {
+    pmisc[0] = segs >= 1 ? p0 + np_argmin(pdist, segs) : p0;      // planner.py:26-27
+    // mu-hat (rt.py:326-344): the warm-up split with g = 9.8, else the top-K means
+    const double mass = c.la.veh.mass, lf = c.la.veh.lf, lr = c.la.veh.lr;
+    double dr, df;
+    if (warm) {
+      dr = c.mu_init * mass * 9.8 * lr / (lf + lr);
+      df = c.mu_init * mass * 9.8 * lf / (lf + lr);
+    } else {
+      int kk = 0;
+      while (kk < c.K && cs.ids[kk] != kNoLocal) ++kk;
+      dr = np_pairwise_ring(cs.dr, 0, kk, LLAMPC_KMAX) / kk;
+      df = np_pairwise_ring(cs.df, 0, kk, LLAMPC_KMAX) / kk;
+    }
+    // the histories are read and written by this block only (the look-ahead blocks read
+    // mu_pred, which is written after the poll)
+    const int cnt = st->hist_count;
+    const int S = c.S;
+    st->dr_hist[cnt % S] = dr;
+    st->df_hist[cnt % S] = df;
+    st->hist_count = cnt + 1;
+    const int tot = cnt + 1, nl = tot < S ? tot : S, first = (tot - nl) % S;
+    const double mu_old = ld_wt(&st->mu_pred);
+    double mu_pred = mu_old;
+    if (!warm)                                                     // rt.py:341
+      mu_pred = (np_pairwise_ring(st->dr_hist, first, nl, S) / nl + np_pairwise_ring(st->df_hist, first, nl, S) / nl) /
+                (9.81 * mass);
+    pmu[0] = dr;
+    pmu[1] = df;
+    pmu[2] = mu_pred;
+    pmu[3] = c.use_mu ? mu_old : c.mu_fixed;                       // the mu this tick's walk used
+  }
   // every slot's result (tagged words of the look-ahead blocks)
   int late = 0;
   if (tid < c.nslots) {
@@ -104,33 +174,13 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   const int wl = __any(late);
   if ((tid & 63) == 0) late_w[tid >> 6] = (unsigned char)wl;
   __syncthreads();
-  if (tid == 0) {
-    const int ss = c.warm ? 0 : c.K;                               // the selected model's slot
-    pmisc[0] = pcand[ss];
-    pmisc[1] = segs >= 1 ? p0 + np_argmin(pdist, segs) : p0;       // planner.py:26-27
-    int anyl = 0;
-    for (int w = 0; w < kWaves; ++w) anyl |= late_w[w];
-    pmisc[2] = anyl;
-  }
-  __syncthreads();
-  // the chosen sequence: candidate sel_cand regenerated (the look-ahead blocks' generator)
-  const int scand = pmisc[0] >= 0 ? pmisc[0] : 0;
-  const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
-  const double up0 = st->u_prev[0], up1 = st->u_prev[1];
-  const double mu_used = c.use_mu ? ld_wt(&st->mu_pred) : c.mu_fixed;   // before the update below
-  if (tid < 2 * H) {
-    const int j = tid & 1;
-    praw[tid] = ctl_cand_raw(scand, tid >> 1, j, H, prev_seq, j ? up1 : up0, j ? c.nscale[1] : c.nscale[0],
-                             j ? c.umin[1] : c.umin[0], j ? c.umax[1] : c.umax[0], c.tick, c.seed, 0);
-  }
-  __syncthreads();
-  if (tid < 2) ctl_rate_chain(praw + tid, H, tid ? up1 : up0, tid ? c.rate[1] : c.rate[0]);
-  __syncthreads();
-  // the record
+  CTL_STAMP(blockIdx.x, 8);
+  // the record and the state
+  const int ss = warm ? 0 : c.K;                                   // the selected model's slot
+  const int scand = pcand[ss] >= 0 ? pcand[ss] : 0;
   llampc_ctl_out* o = c.out;
   llampc_plan_out* po = &o->plan;
   const double nan = __builtin_nan("");
-  const bool warm = c.warm != 0;
   if (tid < LLAMPC_KMAX) {
     const int k = tid;
     const bool have = !warm && k < c.K;
@@ -141,29 +191,30 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     po->topk_cand[k] = have ? pcand[k] : -1;
     po->topk_cost[k] = have ? pcost[k] : nan;
   }
-  if (tid < 2 * H) {
-    const double v = praw[tid];
+  if (tid < 2 * H) {                    // the chosen sequence: candidate sel_cand
+    const double v = cu[2 * (size_t)scand * H + tid];
     (&o->u_seq[0][0])[tid] = v;
     (&st->useq[0][0])[tid] = v;
+    if (tid < 2) st->u_prev[tid] = v;
   }
   if (tid < 6) st->x_prev[tid] = c.x_t[tid];
-  if (tid < 2) st->u_prev[tid] = praw[tid];
   if (tid == 0) {
-    const int ss = warm ? 0 : c.K;
     const int64_t sel = warm ? st->current_model : c.fin.goff + (int64_t)cs.ids[c.K];
     // look-ahead best over the rolled-out slots (flattened (model, candidate) order)
     double lav = nan;
     int64_t lai = kNoIndex;
     int nf = 0;
-    for (int s = 0; s < c.nslots; ++s) {
-      nf += pnf[s];
-      if (warm || pcand[s] < 0 || cs.ids[s] == kNoLocal) continue;
-      const int64_t key = (c.fin.goff + (int64_t)cs.ids[s]) * C + pcand[s];
-      if (less_bf<0>(pcost[s], key, lav, lai)) {
-        lav = pcost[s];
+    for (int q = 0; q < c.nslots; ++q) {
+      nf += pnf[q];
+      if (warm || pcand[q] < 0 || cs.ids[q] == kNoLocal) continue;
+      const int64_t key = (c.fin.goff + (int64_t)cs.ids[q]) * C + pcand[q];
+      if (less_bf<0>(pcost[q], key, lav, lai)) {
+        lav = pcost[q];
         lai = key;
       }
     }
+    int anyl = 0;
+    for (int w = 0; w < kWaves; ++w) anyl |= late_w[w];
     po->window_count = c.fin.window_count;
     po->window_full = c.fin.full;
     po->K = c.K;
@@ -179,31 +230,10 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     po->la_best_model = lai == kNoIndex ? -1 : lai / C;
     po->la_best_cand = lai == kNoIndex ? -1 : (int32_t)(lai % C);
     po->la_best_cost = lai == kNoIndex ? nan : lav;
-    po->status = pmisc[2] ? kPollTimeoutStatus : 0;
-    // mu-hat (rt.py:326-344): the warm-up split with g = 9.8, else the top-K means
-    const double mass = c.la.veh.mass, lf = c.la.veh.lf, lr = c.la.veh.lr;
-    double dr, df;
-    if (warm) {
-      dr = c.mu_init * mass * 9.8 * lr / (lf + lr);
-      df = c.mu_init * mass * 9.8 * lf / (lf + lr);
-    } else {
-      int kk = 0;
-      while (kk < c.K && cs.ids[kk] != kNoLocal) ++kk;
-      dr = np_pairwise_ring(cs.dr, 0, kk, LLAMPC_KMAX) / kk;
-      df = np_pairwise_ring(cs.df, 0, kk, LLAMPC_KMAX) / kk;
-    }
-    const int cnt = st->hist_count;
-    const int S = c.S;
-    st->dr_hist[cnt % S] = dr;
-    st->df_hist[cnt % S] = df;
-    const int tot = cnt + 1, nl = tot < S ? tot : S, first = (tot - nl) % S;
-    double mu_pred = st->mu_pred;
-    if (!warm)                                                     // rt.py:341
-      mu_pred = (np_pairwise_ring(st->dr_hist, first, nl, S) / nl + np_pairwise_ring(st->df_hist, first, nl, S) / nl) /
-                (9.81 * mass);
-    st->hist_count = tot;
+    po->status = anyl ? kPollTimeoutStatus : 0;
+    const double dr = pmu[0], df = pmu[1], mu_pred = pmu[2];
     st->mu_pred = mu_pred;
-    int pj = pmisc[1];
+    int pj = pmisc[0];
     if (pj > c.lap_projidx) pj = 0;                                // rt.py:287-296
     st->projidx = pj;
     st->has_seq = 1;
@@ -211,7 +241,7 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     o->tick = (int64_t)c.tick;
     o->projidx = pj;
     o->warm = c.warm;
-    o->mu_used = mu_used;
+    o->mu_used = pmu[3];
     o->scale_used = c.use_mu ? c.v_factor : c.scale_fixed;
     o->mu_pred = mu_pred;
     o->dr_mean = dr;
@@ -220,6 +250,7 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   }
   __threadfence_system();
   __syncthreads();
+  CTL_STAMP(blockIdx.x, 9);
   if (tid == 0) __hip_atomic_store(c.host_tag, c.host_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -227,16 +258,19 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
 // The device ConstantSpeed (planner.py:12-67), shared by the controller's look-ahead blocks
 // and llampc_ctl_reference: tables -> LDS, the projection, one lane's walk.
 // ------------------------------------------------------------------------------------
-// knots (+inf pad, RaceRef::step), x/y rows [2][4][n-1], the two speed profiles bracketing mu
-// as rows [2][4][n-1] (the walker's whole-lap window)
-__device__ __forceinline__ void cs_stage(const RacelineK& rl, const MuBracket& br, double* kn, double* xy, double* spd) {
+// knots (+inf pad, RaceRef::step) and the two speed profiles bracketing mu, interleaved per
+// segment [n-1][2][4] (consecutive threads write consecutive LDS words; a wave's loads touch 8
+// rows x 8 consecutive segments).  The x/y rows stay in global memory: the walk records each
+// step's (segment, dx) and x/y are evaluated once after it, in parallel.
+__device__ __forceinline__ void cs_stage(const RacelineK& rl, const MuBracket& br, double* kn, double* spd) {
   const int nseg = rl.n - 1;
+  const double* slo = rl.speed + (size_t)br.lo * 4 * nseg;
+  const double* shi = rl.speed + (size_t)br.hi * 4 * nseg;
   copy_lds<4>(kn, rl.n, [&](int e) { return rl.knots[e]; });
-  copy_lds<24>(xy, 8 * nseg, [&](int e) { return rl.xy[e]; });
-  const int q = 4 * nseg;
-  const double* slo = rl.speed + (size_t)br.lo * q;
-  const double* shi = rl.speed + (size_t)br.hi * q;
-  copy_lds<24>(spd, 2 * q, [&](int e) { return e < q ? slo[e] : shi[e - q]; });
+  copy_lds<24>(spd, 8 * nseg, [&](int e) {
+    const int sg = e >> 3, q = e & 3;
+    return ((e >> 2) & 1 ? shi : slo)[(size_t)q * nseg + sg];
+  });
   if ((int)threadIdx.x < kKnotPad) kn[rl.n + threadIdx.x] = __builtin_inf();
 }
 
@@ -250,26 +284,111 @@ __device__ __forceinline__ int cs_project(const double* pts, int np_, int p0, do
   return segs;
 }
 
-// One lane: projidx = p0 + argmin (planner.py:26-27), the start arc length from the prefix
-// table (:29-36), then H steps of :40-62 into sx [H+1][2]; returns projidx, vr (:63-64).
-__device__ __forceinline__ int cs_walk(const RacelineK& rl, const double* kn, const double* xy, const double* spd,
-                                       const double* prefix, const double* dist, int segs, int p0, double px,
-                                       double py, double v0, double mu, double scale, double Ts, int H, double* sx,
-                                       double* vr) {
+// x / den rounded as the IEEE division, by den's correctly rounded reciprocal rden = 1 / den:
+// q0 = x rden, then one FMA residual step (Markstein; checked against x / den on 10^8 pairs
+// of normal operands) — 3 dependent instructions instead of the division's ~10
+__device__ __forceinline__ double div_by(double x, double den, double rden) {
+  const double q0 = x * rden;
+  const double e = __builtin_fma(-q0, den, x);
+  return __builtin_fma(e, rden, q0);
+}
+
+// One speed profile's cubic at dx from its interleaved coefficients (spline_at's expression,
+// so the same roundings): two 16-B LDS reads.
+__device__ __forceinline__ double spline4(const double* c, double dx) {
+  const double2 ab = *reinterpret_cast<const double2*>(c);
+  const double2 cd = *reinterpret_cast<const double2*>(c + 2);
+  const double dx2 = dx * dx;
+  return ab.x + ab.y * dx + cd.x * dx2 + cd.y * (dx2 * dx);
+}
+
+// ConstantSpeed's walk (planner.py:24-65) by ONE WAVE (all 64 lanes call it, uniform control
+// flow): projidx = p0 + argmin (:26-27), the start arc length from the prefix table (:29-36),
+// then H <= 64 steps of :40-62 into sx [H+1][2]; returns projidx and, in lane 0, vr (:63-64).
+// RaceRef::step's walk with the step's candidate segments evaluated speculatively: lane
+// l <= kAhead reads knot seg + l and that segment's two speed cubics (five LDS reads, all
+// addressed by the step's start segment) and evaluates v there; the count of knots <= t over
+// lanes 1..kAhead (a ballot: RaceRef::step's advance) picks the lane whose v holds.  So the
+// chain of a step is one LDS round trip, the cubic and one division chain; x/y are not on it:
+// lane k keeps step k's (segment, dx) and evaluates :43 after the walk.  (The serial walker
+// read the knots, then the chosen segment's coefficients, ~0.7 us a step; a first wave version
+// with x/y in the loop 0.45 us.)  v = (v_lo wa) / den + (v_hi wb) / den (:58-60), the
+// divisions by div_by.
+__device__ __forceinline__ int cs_walk_wave(const RacelineK& rl, const MuBracket& br, const double* kn,
+                                            const double* spd, const double* prefix, const double* dist, int segs,
+                                            int p0, double px, double py, double v0, double scale, double Ts, int H,
+                                            double* sx, double* vr) {
+  const int lane = (int)threadIdx.x & 63;
+  const int m = rl.n - 1;
   const int pj = segs >= 1 ? p0 + np_argmin(dist, segs) : p0;
-  RaceRef rr;
-  rr.init(rl, kn, rl.mus, mu, prefix[pj], v0, scale, Ts, -1);
-  rr.lo = 0;                            // the LDS window holds the bracketing profiles as rows 0, 1
-  rr.hi = rr.single ? 0 : 1;
-  const SpeedWin sw{spd, 0, rl.n - 1};
-  sx[0] = px;                           // planner.py:33 xref[:, 0] = x0
-  sx[1] = py;
+  const double L = kn[m];
+  double s = prefix[pj];
+  double v = fmax(v0, 0.01);                                        // planner.py:34
+  // the start segment: bisect-right on the knots clamped to [0, m - 1] = the count of
+  // knots[i] <= s over i in [1, m - 1] (ascending knots)
+  int cnt = 0;
+  for (int i = 1 + lane; i <= m - 1; i += 64) cnt += (int)(kn[i] <= s);
+  int seg = wave_sum(cnt);
+  double kseg = kn[seg];
+  // a single profile (mu outside the table) has wa = 1, wb = 0, den = 1: v = v_lo exactly
+  // (both rows hold it), so no branch keeps the second cubic's reads behind the first
+  const double wa = br.wa, wb = br.wb, den = br.den, rden = 1.0 / den;
+  const int l = lane < kAhead ? lane : kAhead;                      // lanes > kAhead repeat kAhead
+  int myseg = 0;                                                    // lane k: step k's segment, dx
+  double mydx = 0.0, v1 = 0.0;
   for (int k = 0; k < H; ++k) {
-    double xr, yr;
-    rr.step(rl, kn, xy, sw, xr, yr);
-    sx[2 * (k + 1)] = xr;
-    sx[2 * (k + 1) + 1] = yr;
-    if (k == 0) *vr = rr.v * scale;
+    double t = s + scale * v * Ts;                                  // :41
+    if (!(t >= 0.0 && t < L)) {                                     // :42 Python float %
+      double r = fmod(t, L);
+      if (r != 0.0 && r < 0.0) r += L;
+      t = (r == 0.0) ? 0.0 : r;
+    }
+    s = t;
+    if (t < kseg) {                                                 // wrapped past the lap end
+      seg = 0;
+      kseg = kn[0];
+    }
+    // lane l: knot seg + l (+inf past the last: never counted, since t < L = kn[m]) and the
+    // segment's cubics at t (coefficient reads clamped into the table; unused lanes discard)
+    const int sl = seg + l < m - 1 ? seg + l : m - 1;
+    const double kl = kn[seg + l];
+    const double* cl = spd + 8 * (size_t)sl;
+    const int adv = __popcll(__ballot(lane >= 1 && lane <= kAhead && kl <= t));
+    const double dl = t - kl;
+    const double vb = spline4(cl, dl);
+    const double va = spline4(cl + 4, dl);
+    const double vl = div_by(vb * wa, den, rden) + div_by(va * wb, den, rden);
+    double dx;
+    if (__builtin_expect(adv < kAhead, 1)) {                        // wave-uniform
+      v = readlane_d(vl, adv);
+      kseg = readlane_d(kl, adv);
+      dx = readlane_d(dl, adv);
+      seg += adv;
+    } else {                                                        // past a full window: serial
+      int sg = seg + kAhead;
+      while (sg < m - 1 && kn[sg + 1] <= t) ++sg;
+      kseg = kn[sg];
+      dx = t - kseg;
+      const double* c = spd + 8 * (size_t)sg;
+      const double b = spline4(c, dx);
+      const double a = spline4(c + 4, dx);
+      v = div_by(b * wa, den, rden) + div_by(a * wb, den, rden);
+      seg = sg;
+    }
+    if (lane == k) {
+      myseg = seg;
+      mydx = dx;
+    }
+    if (k == 0) v1 = v;
+  }
+  if (lane == 0) {
+    sx[0] = px;                                                     // planner.py:33
+    sx[1] = py;
+    *vr = v1 * scale;
+  }
+  if (lane < H) {                                                   // :43 calc_position
+    sx[2 * (lane + 1)] = spline_at(rl.xy, m, myseg, mydx);
+    sx[2 * (lane + 1) + 1] = spline_at(rl.xy + 4 * (size_t)m, m, myseg, mydx);
   }
   return pj;
 }
@@ -287,12 +406,12 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   double* sx = reinterpret_cast<double*>(smem + L.sx);
   double* Ul = reinterpret_cast<double*>(smem + L.ul);
   double* kn = reinterpret_cast<double*>(smem + L.kn);
-  double* xy = reinterpret_cast<double*>(smem + L.xy);
   double* spd = reinterpret_cast<double*>(smem + L.spd);
   double* dist = reinterpret_cast<double*>(smem + L.misc);              // [16]
   uint32_t* slot_id = reinterpret_cast<uint32_t*>(smem + L.misc + 128);   // [mpb] (<= 64)
   int32_t* sel_late = reinterpret_cast<int32_t*>(smem + L.misc + 384);    // [mpb]
   double* x0 = reinterpret_cast<double*>(smem + L.misc + 640);            // [6] x_t (no kernarg address taken)
+  CTL_STAMP(blockIdx.x, 0);
   if (tid < 6) x0[tid] = c.x_t[0 + tid];
   const CtlState* st = c.st;
   const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
@@ -302,44 +421,39 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   const double mu = c.use_mu ? ld_wt(&st->mu_pred) : c.mu_fixed;
   const double scale = c.use_mu ? c.v_factor : c.scale_fixed;
   const MuBracket br = mu_bracket(rl.mus, rl.M, mu);
-  // (a) tables: knots, x/y rows, the two speed profiles bracketing mu (cs_stage)
-  cs_stage(rl, br, kn, xy, spd);
-  // (b) project_fast of x_t on raceline[:, p0 : p0 + 10] (track.py:147-160)
+  // (a) tables: knots, x/y rows, the two speed profiles bracketing mu (cs_stage); (b)
+  //     project_fast of x_t on raceline[:, p0 : p0 + 10] (track.py:147-160)
+  cs_stage(rl, br, kn, spd);
   const int segs = cs_project(c.pts, c.np, p0, c.x_t[0], c.x_t[1], dist);
-  // (c) the candidates before the rate clip, every (c, k, j)
-  {
-    const double up0 = st->u_prev[0], up1 = st->u_prev[1];
-    for (int e = tid; e < 2 * C * H; e += kBlock) {
+  __syncthreads();
+  CTL_STAMP(blockIdx.x, 1);
+  // (c) wave 0 walks ConstantSpeed from the projection (planner.py:24-65) while waves 1-3
+  //     draw the candidates before the rate clip, every (c, k, j)
+  const double up0 = st->u_prev[0], up1 = st->u_prev[1];
+  if (tid < 64) {
+    double vr;
+    (void)cs_walk_wave(rl, br, kn, spd, c.prefix, dist, segs, p0, c.x_t[0], c.x_t[1], c.x_t[3], scale, c.la.Ts, H,
+                       sx, &vr);
+    CTL_STAMP(blockIdx.x, 10);
+  } else {
+    for (int e = tid - 64; e < 2 * C * H; e += kBlock - 64) {
       const int cc = e / (2 * H), r = e - cc * 2 * H, j = r & 1;
       Ul[e] = ctl_cand_raw(cc, r >> 1, j, H, prev_seq, j ? up1 : up0, j ? c.nscale[1] : c.nscale[0],
                            j ? c.umin[1] : c.umin[0], j ? c.umax[1] : c.umax[0], c.tick, c.seed, 0);
     }
   }
   __syncthreads();
-  // (d) lane 0 walks ConstantSpeed from the projection (planner.py:24-65); waves 1-3 run the
-  //     candidates' rate-clip chains meanwhile
-  if (tid == 0) {
-    double vr;
-    (void)cs_walk(rl, kn, xy, spd, c.prefix, dist, segs, p0, c.x_t[0], c.x_t[1], c.x_t[3], mu, scale, c.la.Ts, H, sx,
-                  &vr);
-  } else if (tid >= 64) {
+  CTL_STAMP(blockIdx.x, 2);
+  // (d) waves 1-3 clip the candidates' rates; meanwhile (e) wave 0 takes this block's slots:
+  //     the selection (tagged words of the look-back ticket winner), or the nominal model
+  //     while the window fills
+  const int mpb = c.mpb;
+  if (tid >= 64) {
     for (int t = tid - 64; t < 2 * C; t += kBlock - 64) {
       const int j = t & 1;
-      ctl_rate_chain(Ul + 2 * (size_t)(t >> 1) * H + j, H, st->u_prev[j], j ? c.rate[1] : c.rate[0]);
+      ctl_rate_chain(Ul + 2 * (size_t)(t >> 1) * H + j, H, j ? up1 : up0, j ? c.rate[1] : c.rate[0]);
     }
-  }
-  __syncthreads();
-  if (c.dbg && blk == 0) {              // tests: this tick's reference and candidates
-    for (int e = tid; e < 2 * (H + 1); e += kBlock) {
-      const int row = e / (H + 1), k = e - row * (H + 1);
-      c.dbg[e] = sx[2 * k + row];
-    }
-    for (int e = tid; e < 2 * C * H; e += kBlock) c.dbg[2 * (H + 1) + e] = Ul[e];
-  }
-  // (e) this block's slots: the selection (tagged words of the look-back ticket winner), or
-  //     the nominal model while the window fills
-  const int mpb = c.mpb;
-  if (tid < mpb) {
+  } else if (tid < mpb) {
     const int slot = blk * mpb + tid;
     uint32_t id = kNoLocal;
     int late = 0;
@@ -366,6 +480,14 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
     sel_late[tid] = late;
   }
   __syncthreads();
+  CTL_STAMP(blockIdx.x, 3);
+  if (c.dbg && blk == 0) {              // tests: this tick's reference and candidates
+    for (int e = tid; e < 2 * (H + 1); e += kBlock) {
+      const int row = e / (H + 1), k = e - row * (H + 1);
+      c.dbg[e] = sx[2 * k + row];
+    }
+    for (int e = tid; e < 2 * C * H; e += kBlock) c.dbg[2 * (H + 1) + e] = Ul[e];
+  }
   // (f) rollouts: lane layout of the plan kernel's look-ahead (G candidate lanes per model,
   //     LPM lanes per rollout)
   const int G = c.G, cpl = c.cpl;
@@ -409,7 +531,6 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   pin_vgpr(veh.Cr0);
   pin_vgpr(veh.Cr2);
   pin_vgpr(Ts);
-  const double up0 = st->u_prev[0], up1 = st->u_prev[1];
   double bv = __builtin_nan("");
   int64_t bc = kNoIndex;
   int nf = 0;
@@ -461,6 +582,7 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
       }
     }
   }
+  CTL_STAMP(blockIdx.x, 4);
   // (g) per-slot argmin over its candidates and non-finite count: xor shuffles inside a wave,
   //     then across the slot's waves in LDS (a slot of 2 or 4 waves: G LPM in {128, 256})
   const int span = G * LPM;
@@ -502,6 +624,7 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
     st_wt(&w[2], tag_word(c.seq, (uint32_t)(int32_t)bc));
     st_wt(&w[3], tag_word(c.seq, nfw));
   }
+  CTL_STAMP(blockIdx.x, 5);
 }
 
 }  // namespace
@@ -527,37 +650,41 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
     __syncthreads();
     LookbackLaunch lb = c.lb;           // x_prev / u_prev: the state
     lb.x_now = xl;
+    CTL_STAMP(blk, 0);
     lookback_block(lb, blk, sc);
+    CTL_STAMP(blk, 6);
     if (!ticket_last(&c.tickets[0], (unsigned)c.nb_lb, flag)) return;
     if (c.full) {
       lb_final<true>(c.fin, smem, &cs);
       __threadfence_system();           // the record's look-back half (pinned host memory)
     }
+    CTL_STAMP(blk, 7);
     __syncthreads();
   }
   ctl_complete(c, smem, cs);
 }
 
 // llampc_ctl_reference: ConstantSpeed alone (one block), into out = xref [2][H+1], projidx,
-// vr.  LDS: xref | knots | x/y | two profiles | dists (the controller's layout with C = 0).
+// vr.  LDS: xref | knots | two profiles | dists (the controller's layout with C = 0).
 __global__ __launch_bounds__(kBlock) void cs_kernel(CsLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const CtlLds L = ctl_lds(a.H, 0, a.rl.n);
   double* sx = reinterpret_cast<double*>(smem + L.sx);
   double* kn = reinterpret_cast<double*>(smem + L.kn);
-  double* xy = reinterpret_cast<double*>(smem + L.xy);
   double* spd = reinterpret_cast<double*>(smem + L.spd);
   double* dist = reinterpret_cast<double*>(smem + L.misc);
   const MuBracket br = mu_bracket(a.rl.mus, a.rl.M, a.mu);
-  cs_stage(a.rl, br, kn, xy, spd);
+  cs_stage(a.rl, br, kn, spd);
   const int segs = cs_project(a.pts, a.np, a.p0, a.x0, a.y0, dist);
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {                // wave 0 walks (the controller tick's walker)
     double vr = 0.0;
-    const int pj = cs_walk(a.rl, kn, xy, spd, a.prefix, dist, segs, a.p0, a.x0, a.y0, a.v0, a.mu, a.scale, a.Ts, a.H,
-                           sx, &vr);
-    a.out[2 * (a.H + 1)] = (double)pj;
-    a.out[2 * (a.H + 1) + 1] = vr;
+    const int pj = cs_walk_wave(a.rl, br, kn, spd, a.prefix, dist, segs, a.p0, a.x0, a.y0, a.v0, a.scale, a.Ts,
+                                a.H, sx, &vr);
+    if (threadIdx.x == 0) {
+      a.out[2 * (a.H + 1)] = (double)pj;
+      a.out[2 * (a.H + 1) + 1] = vr;
+    }
   }
   __syncthreads();
   for (int e = threadIdx.x; e < 2 * (a.H + 1); e += kBlock) {

@@ -10,14 +10,38 @@
 //                   the mean itself, sample 1 of the first iteration holds uprev — and rolls
 //                   them out (the plan kernel's rollout, NLP-Euler, four lanes per rollout,
 //                   candidates in LDS), writing each sample's objective (+inf if infeasible);
-//   the last block  (ticket) sorts the samples' objectives (bitonic in LDS, NaN last, ties to
-//                   the lower index), regenerates the E elite sequences and sets the next mean /
-//                   std to their mean / standard deviation (NumPy's axis-0 order), keeping the
-//                   best sequence seen so far.
+//                   Each block then sorts its 64 (objective, index) keys in one wave (a bitonic
+//                   network of DPP / shuffle exchanges: NaN last, ties to the lower index) and
+//                   publishes its best len = next_pow2(E) sorted;
+//   the last block  (ticket) merges the blocks' lists pairwise up a tree — the lower len of two
+//                   sorted lists is min(a_i, b_(len-1-i)), bitonic, then one half-cleaner
+//                   network in registers per level — to the E best overall in order,
+//                   regenerates the E elite sequences and sets the next mean / std to their mean
+//                   / standard deviation (NumPy's axis-0 order), keeping the best sequence seen
+//                   so far.  (A bitonic sort of all samples in LDS took 36 us of the 62 us
+//                   round: 55 barrier-separated passes.)
 #include "plan_dev.hpp"
 #include "nlp.hpp"
 
 namespace llampc {
+
+#ifdef LLAMPC_STAMPS
+// Diagnostic build only: s_memrealtime per block and phase of the last launch
+// (tools/diag/nlp_phases.py): 0 entry, 1 drawn, 2 rate-clipped, 3 rolled out; the completing
+// block: 4 keyed, 5 sorted, 6 elite drawn, 7 elite clipped, 8 done.
+static __device__ unsigned long long g_nlp_ph[32][12];
+#define NLP_STAMP(slot)                                                                               \
+  do {                                                                                                \
+    if (threadIdx.x == 0 && blockIdx.x < 32) g_nlp_ph[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+extern "C" int llampc_debug_nlp_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nlp_ph), sizeof(g_nlp_ph)) == hipSuccess ? 0 : -2;
+}
+#else
+#define NLP_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
 
 namespace {
 
@@ -58,52 +82,81 @@ __device__ __forceinline__ uint64_t nlp_key(double v) {
   const uint64_t b = (uint64_t)__double_as_longlong(w);
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
+__device__ __forceinline__ double nlp_unkey(uint64_t k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
+}
+
+// (key, index) exchange step of a bitonic network across lanes lane ^ j: the lane keeps the
+// smaller pair when `low`, else the larger (indices are distinct, so the order is total)
+__device__ __forceinline__ void nlp_cx(uint64_t& k, uint32_t& i, int j, bool low) {
+  const uint64_t pk = __shfl_xor(k, j, 64);
+  const uint32_t pi = __shfl_xor(i, j, 64);
+  const bool pless = pk < k || (pk == k && pi < i);
+  if (low == pless) {
+    k = pk;
+    i = pi;
+  }
+}
 
 __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem) {
 #pragma clang fp contract(off)
-  const int tid = threadIdx.x, H = a.H, S = a.samples, E = a.elite;
+  const int tid = threadIdx.x, H = a.H, E = a.elite;
+  const int len = nlp_list_len(E), nl = (int)gridDim.x;
   NlpState* st = a.st;
-  uint64_t* key = reinterpret_cast<uint64_t*>(smem + kScratchBytes);      // [S]
-  uint32_t* idx = reinterpret_cast<uint32_t*>(key + S);                    // [S]
-  double* eu = reinterpret_cast<double*>(idx + S + (S & 1));                // [E][H][2]
-  for (int i = tid; i < S; i += kBlock) {
-    key[i] = nlp_key(ld_wt(&a.cost[i]));
-    idx[i] = (uint32_t)i;
+  uint64_t* kA = reinterpret_cast<uint64_t*>(smem + kScratchBytes);       // [nl * len] x 2
+  uint64_t* kB = kA + (size_t)nl * len;
+  uint32_t* iA = reinterpret_cast<uint32_t*>(kB + (size_t)nl * len);
+  uint32_t* iB = iA + (size_t)nl * len;
+  double* eu = reinterpret_cast<double*>(smem + kScratchBytes + 24 * (size_t)nl * len);   // [E][H][2]
+  for (int e = tid; e < nl * len; e += kBlock) {
+    kA[e] = ld_wt(&a.top_key[e]);
+    iA[e] = ld_wt(&a.top_idx[e]);
   }
   __syncthreads();
-  // bitonic sort of (key, index) ascending
-  for (int k = 2; k <= S; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < S; i += kBlock) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint64_t ki = key[i], kl = key[l];
-          const uint32_t ii = idx[i], il = idx[l];
-          const bool l_less = (kl < ki) || (kl == ki && il < ii);
-          const bool up = (i & k) == 0;
-          if (up ? l_less : !l_less) {
-            key[i] = kl;
-            key[l] = ki;
-            idx[i] = il;
-            idx[l] = ii;
-          }
+  NLP_STAMP(4);
+  // merge tree: lists 2g, 2g + 1 -> list g; a group of len lanes (inside one wave) per pair
+  for (int n = nl; n > 1; n >>= 1) {
+    const int pairs = n >> 1, gpp = kBlock / len, i = tid & (len - 1);
+    for (int g0 = 0; g0 < pairs; g0 += gpp) {                      // block-uniform
+      const int g = g0 + tid / len;
+      if (g < pairs) {
+        uint64_t k = kA[(size_t)(2 * g) * len + i];
+        uint32_t x = iA[(size_t)(2 * g) * len + i];
+        const uint64_t kb = kA[(size_t)(2 * g + 1) * len + (len - 1 - i)];
+        const uint32_t xb = iA[(size_t)(2 * g + 1) * len + (len - 1 - i)];
+        if (kb < k || (kb == k && xb < x)) {
+          k = kb;
+          x = xb;
         }
+        for (int j = len >> 1; j > 0; j >>= 1) nlp_cx(k, x, j, (i & j) == 0);
+        kB[(size_t)g * len + i] = k;
+        iB[(size_t)g * len + i] = x;
       }
-      __syncthreads();
     }
+    __syncthreads();
+    uint64_t* tk = kA;
+    kA = kB;
+    kB = tk;
+    uint32_t* ti = iA;
+    iA = iB;
+    iB = ti;
   }
+  NLP_STAMP(5);
+  const uint32_t* idx = iA;                                        // the E best, in order
   // the elite sequences, regenerated (the sample blocks' generator), then their rate chains
   for (int e = tid; e < E * H * 2; e += kBlock) {
     const int r = e / (2 * H), q = e - r * 2 * H;
     eu[e] = nlp_raw(a, st, (int)idx[r], q >> 1, q & 1);
   }
   __syncthreads();
+  NLP_STAMP(6);
   if (tid < 2 * E) {
     const int r = tid >> 1, j = tid & 1;
     nlp_rate_chain(eu + 2 * (size_t)r * H + j, H, j ? a.up1 : a.up0, j ? a.rlo1 : a.rlo0, j ? a.rhi1 : a.rhi0);
   }
   __syncthreads();
-  const double c0 = ld_wt(&a.cost[idx[0]]);
+  NLP_STAMP(7);
+  const double c0 = nlp_unkey(kA[0]);
   const bool better = c0 < st->best_j;              // the best sequence so far (NaN never)
   __syncthreads();                                  // every thread has read best_j
   if (tid < 2 * H) {
@@ -130,6 +183,7 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
     }
     __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  NLP_STAMP(8);
 }
 
 }  // namespace
@@ -143,7 +197,9 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);            // xref [H+1][2]
   double* Ul = sx + 2 * (H + 1);                                            // [64][H][2]
   double* x0 = Ul + 2 * (size_t)kPerBlock * H;                              // [6]
+  uint64_t* ks = reinterpret_cast<uint64_t*>(x0 + 6);                       // [64] the samples' keys
   const NlpState* st = a.st;
+  NLP_STAMP(0);
   for (int e = tid; e <= H; e += kBlock) {
     sx[2 * e] = a.xref[e];
     sx[2 * e + 1] = a.xref[(H + 1) + e];
@@ -154,11 +210,13 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     Ul[e] = nlp_raw(a, st, blk * kPerBlock + r, q >> 1, q & 1);
   }
   __syncthreads();
+  NLP_STAMP(1);
   if (tid < 2 * kPerBlock) {
     const int r = tid >> 1, j = tid & 1;
     nlp_rate_chain(Ul + 2 * (size_t)r * H + j, H, j ? a.up1 : a.up0, j ? a.rlo1 : a.rlo0, j ? a.rhi1 : a.rhi0);
   }
   __syncthreads();
+  NLP_STAMP(2);
   // rollouts: a quad per sample (the plan kernel's NLP-Euler fast stage + the general re-run)
   const int sub = tid % LPM, c = tid / LPM;
   const Tire t = load_tire(a.la.params, 1, 0);
@@ -190,14 +248,28 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     if (bi) J = rollout<1, false, LPM, 0, false, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K,
                                                               fq, unused);
   }
-  if (sub == 0) st_wt(&a.cost[blk * kPerBlock + c], J);
+  NLP_STAMP(3);
+  if (sub == 0) ks[c] = nlp_key(J);
+  __syncthreads();
+  if (tid < 64) {                       // wave 0: the block's 64 keys sorted (bitonic, in registers)
+    uint64_t k = ks[tid];
+    uint32_t x = (uint32_t)(blk * kPerBlock + tid);
+    for (int w = 2; w <= 64; w <<= 1)
+      for (int j = w >> 1; j > 0; j >>= 1) nlp_cx(k, x, j, ((tid & j) == 0) == ((tid & w) == 0));
+    const int len = nlp_list_len(a.elite);
+    if (tid < len) {
+      st_wt(&a.top_key[(size_t)blk * len + tid], k);
+      st_wt(&a.top_idx[(size_t)blk * len + tid], x);
+    }
+  }
   if (!ticket_last(a.ticket, gridDim.x, flag)) return;
   nlp_complete(a, smem);
 }
 
 size_t nlp_lds_bytes(int H, int samples, int elite) {
-  const size_t blocks = kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 64;
-  const size_t last = kScratchBytes + 12 * (size_t)samples + 8 + 16 * (size_t)elite * H;
+  const size_t blocks = kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 48 + 8 * 64;
+  const size_t nll = (size_t)(samples / 64) * nlp_list_len(elite);
+  const size_t last = kScratchBytes + 24 * nll + 16 * (size_t)elite * H;
   return std::max(blocks, last);
 }
 

@@ -27,7 +27,8 @@ struct NlpLaunch {
   NlpState* st;
   const double* x0;              // [6] device
   const double* xref;            // [2][H+1] device
-  double* cost;                  // [samples] the iteration's objectives
+  uint64_t* top_key;             // [samples / 64][len] each sample block's best (sorted keys),
+  uint32_t* top_idx;             //   then their sample indices (len = nlp_list_len(elite))
   unsigned* ticket;
   uint64_t seed, call;           // Philox key; counter word 1 = the solve call number
   double up0, up1;               // uprev (du_0, nmpc.py:65-66)
@@ -37,6 +38,12 @@ struct NlpLaunch {
   int32_t it, H, samples, elite, has_hold;
 };
 
+// the length of each sample block's sorted list: next power of two >= elite (elite <= 64)
+__host__ __device__ __forceinline__ int nlp_list_len(int elite) {
+  int l = 1;
+  while (l < elite) l <<= 1;
+  return l;
+}
 size_t nlp_lds_bytes(int H, int samples, int elite);
 hipError_t launch_nlp(const NlpLaunch& a, hipStream_t s);
 

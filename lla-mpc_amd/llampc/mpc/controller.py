@@ -183,6 +183,9 @@ class DeviceController:
         self._h = h
         self.cfg = cfg
         self._x = np.zeros(6)
+        lib = nat.load()
+        self._xp = self._x.ctypes.data
+        self._f_async, self._f_wait = lib.llampc_ctl_tick_async, lib.llampc_ctl_wait
 
     def tick(self, x_t, out=None) -> "nat.CtlOut":
         """One blocking step; ``out`` (a CtlOut) is filled and returned (a new one if None)."""
@@ -193,13 +196,16 @@ class DeviceController:
         return out
 
     def tick_async(self, x_t):
-        x = self._x
-        x[:] = x_t
-        nat.check(nat.load().llampc_ctl_tick_async(self._h, x.ctypes.data))
+        self._x[:] = x_t
+        rc = self._f_async(self._h, self._xp)
+        if rc:
+            nat.check(rc)
 
     def wait(self, out=None) -> "nat.CtlOut":
         out = nat.CtlOut() if out is None else out
-        nat.check(nat.load().llampc_ctl_wait(self._h, nat.C.addressof(out)))
+        rc = self._f_wait(self._h, nat.C.addressof(out))
+        if rc:
+            nat.check(rc)
         return out
 
     def inputs(self):
@@ -231,14 +237,66 @@ class DeviceController:
             pass
 
 
-def result_from_ctl(o: "nat.CtlOut", H: int) -> PlanResult:
-    """PlanResult of a controller tick: the record plus the chosen sequence [2, H]."""
-    res = result_from_out(o.plan)
-    res.u_seq = np.ctypeslib.as_array(o.u_seq)[:H].T.copy()
-    res.nominal = bool(o.warm)
-    res.mu_hat = None if np.isnan(o.mu_pred) else float(o.mu_pred)
-    res.raw = o
-    return res
+_PLAN_DT = np.dtype(nat.PlanOut)
+
+
+class CtlResult:
+    """A controller tick's result: PlanResult's fields over the llampc_ctl_out record, the
+    arrays (top-K, u_seq) views of the record built on first use — a 1 kHz loop that reads
+    only the first control does not pay for NumPy arrays it never touches."""
+    __slots__ = ("raw", "H", "best_model", "window_full", "window_count", "best_cand", "cost",
+                 "n_nonfinite", "nominal", "mu_hat", "_kk", "_rec", "_u")
+    lookback_err = window_mean = costs = None
+
+    def __init__(self, o: "nat.CtlOut", H: int):
+        p = o.plan
+        if p.status:
+            raise nat.NativeError(f"tick record status {p.status}: the in-launch completion timed out")
+        self.raw, self.H = o, int(H)
+        self.best_model, self.best_cand, self.cost = p.sel_model, p.sel_cand, p.sel_cost
+        self.window_full = bool(p.window_full) and p.lb_best >= 0
+        self.window_count, self.n_nonfinite = p.window_count, p.n_nonfinite
+        self.nominal = bool(o.warm)
+        mu = o.mu_pred
+        self.mu_hat = None if mu != mu else mu
+        self._kk = -1
+        self._rec = self._u = None
+
+    def _field(self, name):
+        if self._rec is None:
+            self._rec = np.frombuffer(self.raw, np.uint8, count=_PLAN_DT.itemsize).view(_PLAN_DT)[0]
+            # the record pads top-K with -1 when the bank holds fewer than K models
+            # (argsort()[:K], rt.py:360, returns only those entries)
+            self._kk = int(np.count_nonzero(self._rec["topk"][:self.raw.plan.K] >= 0))
+        return self._rec[name][:self._kk]
+
+    topk = property(lambda self: self._field("topk") if self.window_full else None)
+    topk_err = property(lambda self: self._field("topk_val") if self.window_full else None)
+    topk_Df = property(lambda self: self._field("topk_Df") if self.window_full else None)
+    topk_Dr = property(lambda self: self._field("topk_Dr") if self.window_full else None)
+
+    @property
+    def u_seq(self):
+        """[2, H] the chosen control sequence (a view of the record)."""
+        if self._u is None:
+            self._u = np.frombuffer(self.raw.u_seq, np.float64, count=2 * self.H).reshape(self.H, 2).T
+        return self._u
+
+    @property
+    def u0(self):
+        """The control applied this tick, (u_seq[0, 0], u_seq[1, 0])."""
+        r = self.raw.u_seq[0]
+        return (r[0], r[1])
+
+    @property
+    def global_best(self):
+        p = self.raw.plan
+        return (p.la_best_model, p.la_best_cand, p.la_best_cost)
+
+
+def result_from_ctl(o: "nat.CtlOut", H: int) -> CtlResult:
+    """The result of a controller tick: the record plus the chosen sequence [2, H]."""
+    return CtlResult(o, H)
 
 
 class LLAMPC:
@@ -278,6 +336,8 @@ class LLAMPC:
         self.integrator = integrator
         self.gen = CandidateGenerator(C, H, Ts, seed=seed)
         self.nan_policy = nan_policy
+        self._last = self._last_full = None
+        self._u_seq_host = self._u_prev_host = self._topk_host = None
         self.current_model = 0          # rt.py:264
         self.projidx = 0
         self.t = 0
@@ -363,8 +423,8 @@ class LLAMPC:
         controllers of several banks (e.g. two tracks) run concurrently; tick_end() completes it."""
         if self.mode != "device":
             raise nat.NativeError("tick_begin/tick_end need mode='device'")
-        self._pending_x = np.asarray(x_t, dtype=np.float64).copy()
-        self._ctl.tick_async(self._pending_x)
+        self._pending_x = x = np.array(x_t, dtype=np.float64)
+        self._ctl.tick_async(x)
 
     def tick_end(self) -> PlanResult:
         return self._finish_device(self._ctl.wait(), self._pending_x)
@@ -374,19 +434,26 @@ class LLAMPC:
         look-back, the look-ahead of the selected and top-K models, mu-hat and its state."""
         return self._finish_device(self._ctl.tick(x_t), x_t)
 
-    def _finish_device(self, o, x_t) -> PlanResult:
-        res = result_from_ctl(o, self.H)
-        self.mu.record(o.dr_mean, o.df_mean, o.mu_pred, bool(o.warm))
+    def _finish_device(self, o, x_t) -> CtlResult:
+        res = CtlResult(o, self.H)
+        self.mu.record(o.dr_mean, o.df_mean, o.mu_pred, res.nominal)
         res.mu_hat = self.mu.mu_pred
         if res.window_full:
-            self.last_topk = res.topk
+            self._last_full = res
         self.current_model = res.best_model
-        self.projidx = int(o.projidx)
-        self.u_seq = res.u_seq.T
+        self.projidx = o.projidx
+        self._last = res
         self.x_prev = x_t
-        self.u_prev = res.u_seq[:, 0].copy()
         self.t += 1
         return res
+
+    # device mode keeps the last result; these read it on demand
+    last_topk = property(lambda self: self._last_full.topk if self._last_full is not None else self._topk_host,
+                         lambda self, v: setattr(self, "_topk_host", v))
+    u_seq = property(lambda self: self._last.u_seq.T if self._last is not None else self._u_seq_host,
+                     lambda self, v: setattr(self, "_u_seq_host", v))
+    u_prev = property(lambda self: self._last.u_seq[:, 0].copy() if self._last is not None else self._u_prev_host,
+                      lambda self, v: setattr(self, "_u_prev_host", v))
 
     def inputs(self):
         """Device mode with debug_inputs=True: the last tick's xref [2, H+1] and U [C, H, 2]."""

@@ -1,0 +1,44 @@
+"""Diagnostic (stamps build): phases of the setupNLP.solve CEM round launches — per block
+(µs from the first block's entry, s_memrealtime): drawn, rate-clipped, rolled out; the
+completing block: keyed, sorted, elite drawn, elite clipped, done — for the last round of a
+few solves.  usage: python tools/diag/nlp_phases.py"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("LLAMPC_HIP_LIB", os.path.join(REPO, "lla-mpc_amd/llampc/_lib/libllampc_hip_stamps.so"))
+sys.path[:0] = [REPO, os.path.join(REPO, "lla-mpc_amd")]
+from llampc import _native as nat  # noqa: E402
+from llampc.models import Dynamic  # noqa: E402
+from llampc.mpc.nmpc import setupNLP  # noqa: E402
+from llampc.mpc.planner import ConstantSpeed  # noqa: E402
+from llampc.params import ORCA  # noqa: E402
+from llampc.tracks import ETHZ  # noqa: E402
+
+lib = nat.load()
+lib.llampc_debug_nlp_stamps.argtypes = [ctypes.c_void_p]
+H = 20
+d = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))
+s, u = d["states"], d["inputs"]
+tr = ETHZ('optimal', True)
+p = ORCA(control="pwm")
+nlp = setupNLP(H, 0.02, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, Dynamic(**p, device=0), tr, device=0)
+buf = (ctypes.c_ulonglong * (32 * 12))()
+projidx = 0
+for t in range(10, 16):
+    xref, projidx, _ = ConstantSpeed(s[:2, t], s[3, t], tr, H, 0.02, projidx)
+    nlp.solve(s[:, t].copy(), xref, u[:, t - 1].copy())
+    lib.llampc_debug_nlp_stamps(buf)
+    Z = np.frombuffer(buf, dtype=np.uint64).reshape(32, 12).astype(np.int64)
+    nb = nlp.samples // 64
+    base = Z[:nb, 0].min()
+    us = lambda v: (v - base) / 100.0  # noqa: E731
+    win = int(np.argmax(Z[:nb, 8]))
+    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (1, 2, 3)]
+    comp = [f"{k}: {us(Z[win, k]):.1f}" for k in (4, 5, 6, 7, 8)]
+    print(f"solve {t}: blocks drawn/clipped/rolled (min/max) {' '.join(row)} | completion (block {win}) {' '.join(comp)}",
+          flush=True)
+nlp.close()
