@@ -1476,7 +1476,8 @@ struct llampc_nlp {
   unsigned char* d_blk = nullptr;
   unsigned char* h_blk = nullptr;        // pinned mirror
   size_t blk_bytes = 0, in_bytes = 0;
-  double* d_cost = nullptr;              // the sample blocks' sorted lists (keys, then indices)
+  double* d_cost = nullptr;              // the sample blocks' sorted lists (keys, then indices), then
+                                         // the round's rate-clipped sequences [samples][H][2]
   unsigned* d_ticket = nullptr;
   uint64_t calls = 0;
   std::mutex mu;
@@ -1523,7 +1524,7 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
     return code;
   };
   int rc;
-  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, 2 * (size_t)k.samples)) ||
+  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, 2 * (size_t)k.samples * (1 + (size_t)H))) ||
       (rc = dev_alloc(&p->d_ticket, 1)))
     return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
@@ -1565,7 +1566,6 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   NlpState* ds = reinterpret_cast<NlpState*>(p->d_blk);
   double* dx = reinterpret_cast<double*>(p->d_blk + sizeof(NlpState));
   double* dtraj = reinterpret_cast<double*>(p->d_blk + p->in_bytes);
-  double* dh = dtraj + 6 * (H + 1);
   NlpLaunch a{};
   a.la.params = b->d_params;
   a.la.n = 1;
@@ -1580,6 +1580,8 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.xref = dx + 6;
   a.top_key = reinterpret_cast<uint64_t*>(p->d_cost);
   a.top_idx = reinterpret_cast<uint32_t*>(a.top_key + (size_t)(k.samples / 64) * nlp_list_len(k.elite));
+  a.cand = p->d_cost + 2 * (size_t)k.samples;
+  a.traj = dtraj;
   a.ticket = p->d_ticket;
   a.seed = k.seed;
   a.call = p->calls;
@@ -1600,10 +1602,9 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.has_hold = has_hold;
   for (int it = 0; it < k.iters; ++it) {
     a.it = it;
+    a.last = it == k.iters - 1;         // its completion writes xmpc (nmpc.py:58-60)
     HIP_TRY(launch_nlp(a, s));
   }
-  // xmpc: the NLP's Euler trajectory of the best sequence (nmpc.py:58-60)
-  HIP_TRY(launch_integrate(dx, &ds->best_u[0][0], 0, dh, H, b->d_params, 1, a.la.veh, 1, LLAMPC_EULER_NLP, dtraj, 0, s));
   HIP_TRY(hipMemcpyAsync(p->h_blk, p->d_blk, p->blk_bytes, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   p->calls++;

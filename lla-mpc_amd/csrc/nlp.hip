@@ -98,6 +98,48 @@ __device__ __forceinline__ void nlp_cx(uint64_t& k, uint32_t& i, int j, bool low
   }
 }
 
+// xmpc (nmpc.py:58-60): the NLP's Euler trajectory of the best sequence over all rounds, by
+// one quad of the completing block (the sample blocks' fast rollout, the general re-run when
+// its domain check fails) — it was a separate one-lane launch of the general evaluation, 32 us.
+__device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, unsigned char* smem, double* ub, bool better) {
+  const int tid = threadIdx.x, H = a.H;
+  const NlpState* st = a.st;
+  __syncthreads();                      // the elite rows are read; best_u is final
+  double* sx = ub + 2 * (size_t)H;      // after the sequence: xref [H+1][2], x0 [6]
+  double* x0 = sx + 2 * (size_t)(H + 1);
+  for (int e = tid; e < 2 * H; e += kBlock) ub[e] = better ? ub[e] : (&st->best_u[0][0])[e];
+  for (int e = tid; e <= H; e += kBlock) {
+    sx[2 * e] = a.xref[e];
+    sx[2 * e + 1] = a.xref[(H + 1) + e];
+  }
+  if (tid < 6) x0[tid] = a.x0[tid];
+  __syncthreads();
+  if (tid >= 4) return;
+  constexpr int LPM = 4;
+  const int sub = tid;
+  const Tire t = load_tire(a.la.params, 1, 0);
+  const CostK q = a.la.cost;
+  const VehK veh = a.la.veh;
+  const double Ts = a.la.Ts;
+  const StageK sk = make_stage<LPM>(veh, t, sub, 1.0);
+  const FusedK fq = make_fused(veh, sk, Ts, false);
+  const fm::FmK K = fm::FmK::load();
+  double* out = sub == 0 ? a.traj : nullptr;
+  if (sub == 0)
+    for (int m = 0; m < 6; ++m) a.traj[m] = x0[m];
+  bool bad = false;
+  (void)rollout<1, false, LPM, 0, true, false, true, true>(a.la, 0, 0, x0, sx, ub, veh, t, sk, q, Ts, a.up0, a.up1, K, fq,
+                                                           bad, out);
+  int bi = bad;
+  bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX1, 0xF, 0xF, false);
+  bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX2, 0xF, 0xF, false);
+  if (bi) {
+    bool unused = false;
+    (void)rollout<1, false, LPM, 0, false, false, true, true>(a.la, 0, 0, x0, sx, ub, veh, t, sk, q, Ts, a.up0, a.up1, K,
+                                                              fq, unused, out);
+  }
+}
+
 __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem) {
 #pragma clang fp contract(off)
   const int tid = threadIdx.x, H = a.H, E = a.elite;
@@ -143,19 +185,13 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   }
   NLP_STAMP(5);
   const uint32_t* idx = iA;                                        // the E best, in order
-  // the elite sequences, regenerated (the sample blocks' generator), then their rate chains
+  // the elite sequences (the sample blocks' rate-clipped candidates)
   for (int e = tid; e < E * H * 2; e += kBlock) {
     const int r = e / (2 * H), q = e - r * 2 * H;
-    eu[e] = nlp_raw(a, st, (int)idx[r], q >> 1, q & 1);
+    eu[e] = ld_wt(&a.cand[2 * (size_t)idx[r] * H + q]);
   }
   __syncthreads();
   NLP_STAMP(6);
-  if (tid < 2 * E) {
-    const int r = tid >> 1, j = tid & 1;
-    nlp_rate_chain(eu + 2 * (size_t)r * H + j, H, j ? a.up1 : a.up0, j ? a.rlo1 : a.rlo0, j ? a.rhi1 : a.rhi0);
-  }
-  __syncthreads();
-  NLP_STAMP(7);
   const double c0 = nlp_unkey(kA[0]);
   const bool better = c0 < st->best_j;              // the best sequence so far (NaN never)
   __syncthreads();                                  // every thread has read best_j
@@ -184,6 +220,7 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
     __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   NLP_STAMP(8);
+  if (a.last) nlp_trajectory(a, smem, eu, better);
 }
 
 }  // namespace
@@ -217,6 +254,7 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   }
   __syncthreads();
   NLP_STAMP(2);
+  for (int e = tid; e < kPerBlock * H * 2; e += kBlock) st_wt(&a.cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
   // rollouts: a quad per sample (the plan kernel's NLP-Euler fast stage + the general re-run)
   const int sub = tid % LPM, c = tid / LPM;
   const Tire t = load_tire(a.la.params, 1, 0);
@@ -269,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
 size_t nlp_lds_bytes(int H, int samples, int elite) {
   const size_t blocks = kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 48 + 8 * 64;
   const size_t nll = (size_t)(samples / 64) * nlp_list_len(elite);
-  const size_t last = kScratchBytes + 24 * nll + 16 * (size_t)elite * H;
+  const size_t last = kScratchBytes + 24 * nll + 16 * (size_t)elite * H + 16 * (size_t)(H + 1) + 48;
   return std::max(blocks, last);
 }
 

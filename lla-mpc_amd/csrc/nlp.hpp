@@ -29,13 +29,15 @@ struct NlpLaunch {
   const double* xref;            // [2][H+1] device
   uint64_t* top_key;             // [samples / 64][len] each sample block's best (sorted keys),
   uint32_t* top_idx;             //   then their sample indices (len = nlp_list_len(elite))
+  double* cand;                  // [samples][H][2] the round's sequences after the rate clip
+  double* traj;                  // [H+1][6] the last round: the best sequence's trajectory
   unsigned* ticket;
   uint64_t seed, call;           // Philox key; counter word 1 = the solve call number
   double up0, up1;               // uprev (du_0, nmpc.py:65-66)
   double umin0, umin1, umax0, umax1;
   double rlo0, rlo1, rhi0, rhi1; // per-step rate bounds (x Ts); lo > hi: none
   double std_floor;
-  int32_t it, H, samples, elite, has_hold;
+  int32_t it, H, samples, elite, has_hold, last;
 };
 
 // the length of each sample block's sorted list: next power of two >= elite (elite <= 64)

@@ -571,12 +571,13 @@ __device__ __forceinline__ bool input_feasible(const CostK& q, double ua, double
 // (J_X + J_Y) + act by two DPP broadcasts at the end.
 // ULDS (the controller tick, ctl.hip): the raw candidates U [C][H][2] are at `su` (LDS)
 // instead of a.U; only with STAGE = false.
-template <int INTEG, bool STAGE, int LPM, int XM, bool FAST, bool SPLIT = false, bool ULDS = false>
+template <int INTEG, bool STAGE, int LPM, int XM, bool FAST, bool SPLIT = false, bool ULDS = false, bool TRAJ = false>
 __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64_t n,
                                           const double* x0, const double* sx, const double* su, const VehK& veh,
                                           const Tire& t, const StageK& sk, const CostK& q,
                                           double Ts, double up0, double up1, const fm::FmK& K,
-                                          const FusedK& fq, bool& bad) {
+                                          const FusedK& fq, bool& bad, double* traj = nullptr) {
+  static_assert(!TRAJ || (INTEG != 0 && !SPLIT), "trajectory output: unscaled, unsplit state");
   static_assert(!SPLIT || (FAST && INTEG == 0 && LPM == 4), "position split: fused RK4 quads only");
   static_assert(!ULDS || !STAGE, "candidates in LDS: unstaged rollout");
   const int H = a.H, C = a.C;
@@ -652,6 +653,10 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     if (!STAGE) act = act + act_term(q, d0, d1);
     p0 = ua;
     p1 = ud;
+    if (TRAJ && traj != nullptr) {      // the state after step k (every lane of a quad holds it)
+#pragma unroll
+      for (int m = 0; m < 6; ++m) traj[6 * (k + 1) + m] = x[m];
+    }
   }
   double J;
   if (SPLIT) {                                                    // nmpc.py:48, :111
@@ -1365,6 +1370,16 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
     kv = val[e];
   }
   STAMP(2);
+  if constexpr (SEL) {                     // the controller's selection first: the look-ahead
+    if (lane < K) {                        // blocks wait on it (the record's stores below wait
+      cs->ids[lane] = kl;                  // on the Pacejka loads of the top-K rows)
+      st_wt(&cs->tag[lane], tag_word(cs->seq, kl));
+    }
+    if (lane == 0) {
+      cs->ids[K] = li;
+      st_wt(&cs->tag[K], tag_word(cs->seq, li));
+    }
+  }
   // Every record field is stored write-through (sc1): on the ticket path another block —
   // possibly on another XCD — completes the record, and peer_finish reads all of it back
   // with sc1 loads (MI355X_MICROARCH.md "Valid forms": sc1 stores AND sc1 loads).
@@ -1391,14 +1406,8 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
   if constexpr (SEL) {
     if (lane < K) {
       const bool have = kl != kNoLocal;
-      cs->ids[lane] = kl;
       cs->dr[lane] = have ? f.params[5 * f.n + kl] : __builtin_nan("");
       cs->df[lane] = have ? f.params[2 * f.n + kl] : __builtin_nan("");
-      st_wt(&cs->tag[lane], tag_word(cs->seq, kl));
-    }
-    if (lane == 0) {
-      cs->ids[K] = li;
-      st_wt(&cs->tag[K], tag_word(cs->seq, li));
     }
   }
 }
