@@ -539,6 +539,28 @@ int wait_host_tag(llampc_bank* b, uint64_t seq, llampc_plan_out* out) {
 
 }  // namespace
 
+namespace {
+// A bank's stream.  HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4 by
+// default, least-used first), so two banks ticked concurrently — the two controllers of
+// config 5 — can land on one queue and run one after the other: the two-track controller
+// step measured 172 us instead of 98 us whenever two other streams were in use first
+// (tools/diag/bench_extra.py).  A stream with a CU mask gets a hardware queue of its own;
+// the mask holds every CU, so nothing else changes.  LLAMPC_SHARED_QUEUES=1 keeps the plain
+// stream; the plain stream is also the fallback.
+hipError_t bank_stream(int device, hipStream_t* s) {
+  if (!std::getenv("LLAMPC_SHARED_QUEUES")) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
+      std::vector<uint32_t> mask((cus + 31) / 32, 0xFFFFFFFFu);
+      if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
+      if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return hipSuccess;
+      (void)hipGetLastError();
+    }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+}  // namespace
+
 extern "C" {
 
 int32_t llampc_abi_version(void) { return LLAMPC_ABI_VERSION; }
@@ -584,8 +606,7 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
     llampc_bank_destroy(b);
     return code;
   };
-  if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess)
-    return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
+  if (bank_stream(device, &b->stream) != hipSuccess) return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
   b->own_stream = true;
   const int64_t lbl = (int64_t)lookback_blocks(n) * (kBlock / 64);   // look-back lists (waves)
   const int64_t lab = n;                 // worst case: one model per block (wave-role, G=64)
@@ -708,7 +729,7 @@ int llampc_bank_set_stream(llampc_bank* b, void* stream) {
     b->stream = (hipStream_t)stream;
     b->own_stream = false;
   } else {
-    HIP_TRY(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    HIP_TRY(bank_stream(b->device, &b->stream));
     b->own_stream = true;
   }
   return LLAMPC_OK;
