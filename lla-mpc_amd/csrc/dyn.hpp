@@ -541,9 +541,10 @@ __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::F
 // roundings, which the look-back keeps (its errors are ranked, rt.py:359-360).
 // The look-ahead's fused stages use the lean cores (fastmath.hpp kAtanRL / kSinWQL, the
 // division without its residual step; the FmK of those rollouts is loaded with
-// FmK::load<kLeanLA>()): ~1e-14 relative on the tire forces; 467 instructions per step at
-// LPM 4 (494 with the precise 10-term cores, 507 in round 2), A/B 28.8 -> 27.2 us per tick
-// (profiles/r03/ab_lean).  -DLLAMPC_PRECISE_LA
+// FmK::load<kLeanLA>()): ~1e-13 relative on the tire forces (8 terms, round 4; ~1e-14 with 9);
+// 456 instructions per step at LPM 4 (467 with 9 terms, 494 with the precise 10-term cores,
+// 507 in round 2), A/B 28.8 -> 27.2 us per tick with 9 terms (profiles/r03/ab_lean), 26.6
+// with 8 (profiles/r04/ab_lean8.log).  -DLLAMPC_PRECISE_LA
 // builds the precise (<= 4 ulp) cores into the look-ahead too, for A/B runs.
 #ifdef LLAMPC_PRECISE_LA
 constexpr bool kLeanLA = false;

@@ -180,14 +180,16 @@ constexpr double kAtanR[10] = {
     -0.06649613695291669,  0.05736332165907643,  -0.04483334622272886,
     0.02275052699336167};
 constexpr double kTanPi8 = 0.41421356237309503;
-// Lean cores of the look-ahead rollouts (kLeanLA): 9-term atan (3.8e-15 relative on |t| <=
-// tan(pi/8)) and 9-term sin_wide (2.3e-15 absolute to |a| = 3, <= 4 ulp to 2), and the
-// division without its residual correction (<= 18 ulp): ~1e-14 relative on the tire forces
-// against the <= 4 ulp of the precise cores, which the look-back keeps (its errors are ranked).
-// -DLLAMPC_LEAN_TERMS=8 (A/B): 8-term lean cores (atan 1.1e-13 relative, sin_wide 2.6e-13
-// absolute to |a| = 3, tools/fit_fastmath.py), 12 fewer instructions per LPM-4 step.
+// Lean cores of the look-ahead rollouts (kLeanLA): 8-term atan (1.1e-13 relative on |t| <=
+// tan(pi/8)) and 8-term sin_wide (5e-14 absolute to |a| = 2, 2.6e-13 to 3), and the division
+// without its residual correction (<= 18 ulp): ~1e-13 relative on the tire forces against the
+// <= 4 ulp of the precise cores, which the look-back keeps (its errors are ranked).  Round 4
+// went from 9 to 8 terms (tools/fit_fastmath.py): 12 fewer instructions per LPM-4 step, 24 per
+// LPM-1 step; alternating A/B (profiles/r04/ab_lean8.log) 26.8-27.2 -> 26.6-26.7 us per tick at
+// C = 1 and 394-404 -> 383-390 us at C = 64 — the rollouts stay within 1e-7 of the NumPy
+// restatement (north star: 1e-5).  -DLLAMPC_LEAN_TERMS=9 builds the round-3 cores.
 #ifndef LLAMPC_LEAN_TERMS
-#define LLAMPC_LEAN_TERMS 9
+#define LLAMPC_LEAN_TERMS 8
 #endif
 constexpr int kLeanTerms = LLAMPC_LEAN_TERMS;
 #if LLAMPC_LEAN_TERMS == 8
@@ -224,7 +226,7 @@ struct FmK {
   double inv_pi, inv_3pi;                 // (2/pi)/2, (2/pi)/6: the scaled yaw's RK4 weights
 
   __device__ __forceinline__ static void pin(double& x) { asm volatile("" : "+v"(x)); }
-  // LEAN: the 9-term coefficient sets in ar[0..8] / sw[0..8] (the lean cores read no more)
+  // LEAN: the kLeanTerms-term coefficient sets in ar / sw (the lean cores read no more)
   template <bool LEAN = false>
   __device__ __forceinline__ static FmK load() {
     FmK k;

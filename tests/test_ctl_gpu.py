@@ -74,6 +74,31 @@ def test_ctl_reference_matches_reference_planner(nat, name):
             ctl.close()
 
 
+@pytest.mark.parametrize("name", ["ETHZ", "ETHZMobil"])
+def test_ctl_reference_fast_starts_and_lap_end(nat, name):
+    """The walk's branches off the common path: a first step past kAhead segments (v0 up to
+    25 m/s: the serial continuation after the wave's window), and starts just before the lap
+    end (the mod-L wrap, then the restart at segment 0) — against host ConstantSpeed, 1e-10."""
+    from llampc.mpc import DeviceController, ModelBank, generate_bank
+    from llampc.mpc.planner import ConstantSpeed
+    tr, _ = tracks(name)
+    pts = np.asarray(tr.raceline)
+    npnt = pts.shape[1]
+    with ModelBank(generate_bank(16, seed=0), W=2, device=0) as b:
+        ctl = DeviceController(b, tr, H=40, C=1, K=1)
+        try:
+            for pi in (0, npnt // 3, npnt - 12, npnt - 3):
+                for v0, mu, scale in ((25.0, 0.9, 1.0), (8.0, 0.6, 1.5), (0.5, 1.2, 0.9)):
+                    px, py = pts[0, pi] + 0.01, pts[1, pi] - 0.02
+                    out, oidx, ovr = ctl.reference([px, py], v0, 40, pi, mu, scale)
+                    host, hidx, hvr = ConstantSpeed(np.array([px, py]), v0, tr, 40, TS, pi, scale=scale, curr_mu=mu)
+                    np.testing.assert_allclose(out, host, rtol=1e-10, atol=1e-12, err_msg=f"{pi} {v0} {mu} {scale}")
+                    assert oidx == hidx
+                    np.testing.assert_allclose(ovr, hvr, rtol=1e-10)
+        finally:
+            ctl.close()
+
+
 @pytest.mark.parametrize("N,C,H,W,K,name,ticks", [
     (200, 8, 20, 4, 10, "ETHZ", 14),
     (6, 8, 20, 4, 10, "ETHZ", 10),            # N < K: top-K padded with -1, never in mu-hat

@@ -668,11 +668,11 @@ def test_fast_cores_ulp_on_domain(nat):
 
 
 def test_lean_cores_accuracy_on_domain(nat):
-    """The look-ahead's lean cores (math fn 10-12: 9-term atan and sin_wide, division without
-    its residual step) on the same domains vs NumPy: atan2 / atan within 128 ulp (~3e-14
-    relative), sin_wide within 16 ulp for |a| <= 2 and 2^-47 absolute up to 3 — far inside
-    the 1e-7 rollout tolerance and the north star's 1e-5, the rollouts' own fused-RK4
-    roundings being of the same order."""
+    """The look-ahead's lean cores (math fn 10-12: 8-term atan and sin_wide, division without
+    its residual step) on the same domains vs NumPy: atan2 / atan within 1024 ulp (~2.3e-13
+    relative; the fit's own error is 1.05e-13), sin_wide within 512 ulp for |a| <= 2 (5e-14
+    absolute) and 2^-41 absolute up to 3 — far inside the 1e-7 rollout tolerance and the
+    north star's 1e-5."""
     rng = np.random.RandomState(2)
     n = 1 << 20
     y = np.concatenate([rng.uniform(-3, 3, n), rng.standard_cauchy(n), [0.0, -0.0, 1.0, -1.0, 1e-300, 5.0]])
@@ -684,10 +684,10 @@ def test_lean_cores_accuracy_on_domain(nat):
     a = rng.uniform(-2, 2, n)
     u_s = _ulp(_math(nat, 12, a), np.sin(a))
     print(f"lean cores: atan2 {u_a2:.1f} ulp, atan {u_a:.1f} ulp, sin_wide |a|<=2 {u_s:.1f} ulp")
-    assert u_a2 <= 128 and u_a <= 128 and u_s <= 16
+    assert u_a2 <= 1024 and u_a <= 1024 and u_s <= 512
     a = np.concatenate([rng.uniform(-3, 3, n), [3.0, -3.0, 0.0, -0.0, 1e-300]])
     err = np.abs(_math(nat, 12, a) - np.sin(a))
-    assert np.all(err <= 16 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -47), err.max()
+    assert np.all(err <= 16 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -41), err.max()
     # the paired cores of the LPM-1 look-ahead lane (math fn 13/14: front and rear division
     # through one reciprocal, partner = element n-1-i) on their domain (Dom::ok_paired:
     # atan2 divisors max(|y|, x) in [2^-500, 2^499], atan divisor products <= 2^499)
@@ -699,7 +699,7 @@ def test_lean_cores_accuracy_on_domain(nat):
     zz = z[np.abs(z) <= 2.0 ** 240]
     u_p = _ulp(_math(nat, 14, zz), np.arctan(zz))
     print(f"paired cores: atan2 {u_p2:.1f} ulp, atan {u_p:.1f} ulp")
-    assert u_p2 <= 128 and u_p <= 128
+    assert u_p2 <= 1024 and u_p <= 1024
 
 
 def test_lookahead_out_of_domain_fallback(nat):
