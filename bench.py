@@ -631,6 +631,7 @@ def concurrent_tracks_sharded(args, world, rank, dev_index, ticks=1000, warm=50)
             a.track, a.H, a.C, a.scenario = track, H, 1, None
             t = make_ticks(a, 8)
             sb = ShardedBank(generate_bank(args.n_per_gpu * world, seed=seed), rank, world, dev_index, W=args.W)
+            sb.bank.set_concurrency(2)    # the two tracks' launches share each GPU
             sbs.append(sb)
             packs = torch.from_numpy(t).to(dev)
             torch.cuda.synchronize(dev)
@@ -690,6 +691,7 @@ def concurrent_tracks(args, ticks=1000, warm=50, period=1e-3):
         a.track, a.H, a.C = track, H, 1
         t = make_ticks(a, 8)
         banks.append(ModelBank(generate_bank(args.n_per_gpu, seed=seed), W=W, device=torch_device_index()))
+        banks[-1].set_concurrency(2)      # two launches share the chip (llampc_bank_set_concurrency)
         inputs.append(t)
 
     def step(i):
@@ -721,7 +723,8 @@ def concurrent_tracks(args, ticks=1000, warm=50, period=1e-3):
             "back_to_back": q,
             "sel_models": [int(o.sel_model) for o in outs],
             "note": "two independent plan() instances per control step (ETHZ + ETHZMobil), async on two streams, "
-                    "host pointers in and the record read back; paced: one step per 1 ms period (busy-wait)"}
+                    "host pointers in and the record read back, each bank sized for half the chip "
+                    "(set_concurrency(2)); paced: one step per 1 ms period (busy-wait)"}
 
 
 def config3(args, steps=200, warmup=20):

@@ -141,6 +141,7 @@ struct llampc_bank {
   VehK veh{};
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  int32_t share = 1;                     // banks ticked concurrently (llampc_bank_set_concurrency)
   double* d_params = nullptr;
   double* d_ring = nullptr;
   double* d_am_val = nullptr;
@@ -446,7 +447,7 @@ int plan_launch(llampc_bank* b, const llampc_plan_in& in, llampc_plan_out* d_out
   f.wq = b->d_wq;
   {
     TimedLaunch tl(b, 0, s);
-    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s, pk));
+    HIP_TRY(launch_plan(lb ? &lbl : nullptr, la ? &lal : nullptr, f, s, pk, b->share));
   }
   b->seq = seq;
   if (px) px->seq = px_seq;
@@ -716,6 +717,14 @@ int llampc_bank_window(llampc_bank* b, double* ring, int32_t* window_count) {
     }
   }
   if (window_count) *window_count = cnt;
+  return LLAMPC_OK;
+}
+
+int llampc_bank_set_concurrency(llampc_bank* b, int32_t banks) {
+  if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
+  if (banks < 1 || banks > 64) return fail(LLAMPC_E_ARG, "banks=%d outside [1, 64]", banks);
+  std::lock_guard<std::mutex> lk(b->mu);
+  b->share = banks;
   return LLAMPC_OK;
 }
 

@@ -195,14 +195,18 @@ int lookahead_group(int32_t C) {
 // chain, sin psi, cos psi in one stream) up to 16k rollouts, a lane pair (front / rear
 // chain) up to 32k; one lane per rollout once the chip fills (fewest instructions per
 // rollout).
-int lookahead_lpm(int64_t n, int32_t C, int32_t integrator) {
+// share: the number of banks the caller ticks concurrently on the device (llampc_bank_set_
+// concurrency): each launch is sized for 1/share of the SIMDs (BASELINE config 5, two tracks
+// at N = 10^4, H = 40: LPM 2 instead of 4, so both launches are resident together — 111 ->
+// 86 us per paced step, profiles/r04/config5_lpm.log).
+int lookahead_lpm(int64_t n, int32_t C, int32_t integrator, int32_t share) {
   if (integrator == LLAMPC_RK6) return 1;
   const int G = lookahead_group(C);
   if (const char* e = getenv("LLAMPC_LPM")) {     // benchmarking override
     const int v = atoi(e);
     if (v == 1 || ((v == 2 || v == 4) && v * G <= kBlock)) return v;
   }
-  const int64_t lanes = n * G;
+  const int64_t lanes = n * G * std::max(share, 1);
   if (lanes <= 16384 && 4 * G <= kBlock) return 4;
   return (lanes <= 32768 && 2 * G <= kBlock) ? 2 : 1;
 }
@@ -273,7 +277,7 @@ static int device_cus() {
 }
 
 hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
-                       hipStream_t s, const InlinePack* pk) {
+                       hipStream_t s, const InlinePack* pk, int32_t share) {
   LookbackLaunch lbv{};
   LookaheadLaunch lav{};
   int G = 1, cpl = 1, lpm = 1, integ = LLAMPC_RK4;
@@ -300,7 +304,7 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
     G = lookahead_group(la->C);
     cpl = (la->C + G - 1) / G;
     integ = la->integrator;
-    lpm = lookahead_lpm(la->n, la->C, integ);
+    lpm = lookahead_lpm(la->n, la->C, integ, share);
     f.nb_la = lookahead_blocks(la->n, la->C, lpm);
     if (la->xref_mode == LLAMPC_XREF_RACELINE) {
       // knots + x/y rows in LDS, the staged inputs when they fit beside them, and the rest

@@ -125,7 +125,7 @@ struct InlinePack {
 
 int lookback_blocks(int64_t n);
 int lookahead_group(int32_t C);
-int lookahead_lpm(int64_t n, int32_t C, int32_t integrator);
+int lookahead_lpm(int64_t n, int32_t C, int32_t integrator, int32_t share = 1);
 int lookahead_blocks(int64_t n, int32_t C, int lpm);
 int lookback_r(int64_t n, int32_t K);               // models per look-back lane
 int lookback_blocks_r(int64_t n, int R);
@@ -137,7 +137,7 @@ size_t raceline_lds_bytes(int32_t n, int32_t M);
 // pk != null: the inputs are in *pk (see InlinePack); needs a look-ahead with RK4, the
 // given xref and U staged in LDS (plan_inline_ok), else hipErrorInvalidValue.
 hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, FinalLaunch f,
-                       hipStream_t s, const InlinePack* pk = nullptr);
+                       hipStream_t s, const InlinePack* pk = nullptr, int32_t share = 1);
 bool plan_inline_ok(int32_t C, int32_t H, int32_t integrator, int32_t xref_mode);
 // The plan-kernel variant groups (plan_dev.hpp; one translation unit per group, plan_*.hip):
 // (integrator, lanes per rollout) with the staged / unstaged inputs and, for RK4 at LPM 1, the

@@ -127,6 +127,12 @@ class ModelBank:
     def set_stream(self, stream_ptr: int | None):
         nat.check(nat.load().llampc_bank_set_stream(self.handle, stream_ptr))
 
+    def set_concurrency(self, banks: int):
+        """The number of banks ticked concurrently on this device (default 1; two tracks
+        ticked together: 2): each look-ahead launch is sized for 1/banks of the chip, so the
+        concurrent launches are resident together (llampc_bank_set_concurrency)."""
+        nat.check(nat.load().llampc_bank_set_concurrency(self.handle, int(banks)))
+
     @property
     def window_count(self) -> int:
         c = nat.C.c_int32()

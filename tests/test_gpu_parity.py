@@ -926,6 +926,41 @@ def test_polled_completion_equals_ticket_completion(nat):
             b_bank.close()
 
 
+def test_bank_concurrency_lane_split_equals_default(nat):
+    """llampc_bank_set_concurrency(2) (BASELINE config 5: two tracks share the chip) sizes the
+    look-ahead for half the SIMDs — at N = 10^4, H = 40, C = 1 the lane pair (LPM 2) instead of
+    the quad — with the same selections and top-K as the default bank and costs within 1e-9,
+    tick after tick; 0 and 65 are rejected."""
+    from llampc import _native
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    N, H, W = 10000, 40, 3
+    a_bank = ModelBank(generate_bank(N, seed=1), W=W, device=0)
+    b_bank = ModelBank(generate_bank(N, seed=1), W=W, device=0)
+    try:
+        b_bank.set_concurrency(2)
+        for bad in (0, 65):
+            with pytest.raises(_native.NativeError):
+                b_bank.set_concurrency(bad)
+        for t in range(1, W + 3):
+            U = u[:, t:t + H].T[None].copy()
+            xref = s[:2, t:t + H + 1] + 0.01
+            args = (s[:, t - 1], u[:, t - 1], s[:, t], U, xref, u[:, t - 1])
+            A = _native.plan_out_to_dict(a_bank.plan_raw(*args, K=10)[0])
+            B = _native.plan_out_to_dict(b_bank.plan_raw(*args, K=10)[0])
+            for k in ("window_full", "lb_best", "sel_model", "sel_cand", "la_best_model", "la_best_cand", "n_nonfinite",
+                      "status"):
+                assert A[k] == B[k], (t, k, A[k], B[k])
+            np.testing.assert_array_equal(A["topk"], B["topk"])
+            np.testing.assert_array_equal(A["topk_cand"], B["topk_cand"])
+            np.testing.assert_allclose(B["sel_cost"], A["sel_cost"], rtol=1e-9)
+            np.testing.assert_allclose(B["la_best_cost"], A["la_best_cost"], rtol=1e-9)
+    finally:
+        a_bank.close()
+        b_bank.close()
+
+
 def test_work_queue_layout_equals_static_and_oracle(nat, monkeypatch):
     """The throughput layout (launch_plan's work queue: one look-ahead block per CU, waves
     taking units of models from the bank's counter) at N = 3000, C = 64 (750 static blocks >
