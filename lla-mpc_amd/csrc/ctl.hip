@@ -353,11 +353,14 @@ __device__ __forceinline__ int cs_walk_wave(const RacelineK& rl, const MuBracket
     const int sl = seg + l < m - 1 ? seg + l : m - 1;
     const double kl = kn[seg + l];
     const double* cl = spd + 8 * (size_t)sl;
-    const int adv = __popcll(__ballot(lane >= 1 && lane <= kAhead && kl <= t));
-    const double dl = t - kl;
+    double dl = t - kl;
     const double vb = spline4(cl, dl);
     const double va = spline4(cl + 4, dl);
-    const double vl = div_by(vb * wa, den, rden) + div_by(va * wb, den, rden);
+    double vl = div_by(vb * wa, den, rden) + div_by(va * wb, den, rden);
+    // every lane's v before the advance is known: the compiler would otherwise sink the
+    // cubics' reads below the ballot's branch — a second LDS round trip on the chain
+    asm volatile("" : "+v"(vl), "+v"(dl));
+    const int adv = __popcll(__ballot(lane >= 1 && lane <= kAhead && kl <= t));
     double dx;
     if (__builtin_expect(adv < kAhead, 1)) {                        // wave-uniform
       v = readlane_d(vl, adv);

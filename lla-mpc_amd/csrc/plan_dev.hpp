@@ -1324,6 +1324,7 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
     }
     __syncthreads();
   }
+  STAMP(6);
   const uint64_t tk = thr[0];
   const uint32_t ti = (uint32_t)thr[1];
   for (int e = tid; e < M; e += kBlock) {
@@ -1337,6 +1338,7 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
     }
   }
   __syncthreads();
+  STAMP(7);
   const int c = *cnt;                      // >= K (the K smallest heads, or all M >= K)
   for (int q = tid; q < c; q += kBlock) {
     const uint64_t mk = ck[q];

@@ -62,7 +62,9 @@ print(f"all {nla} look-ahead blocks (min/median/max): start {q(us(Z[:,0,1]))}, s
 cyc = Z[:, 2, 0] - Z[:, 1, 0]
 rt = (Z[:, 2, 1] - Z[:, 1, 1]) / 100.0
 print(f"rollout per block: {q(rt)} us, {q(cyc)} shader cycles, clock {np.median(cyc / rt) / 1e3:.2f} GHz")
-print(f"lb_final: {us(R[0]):.2f} -> {us(R[1]):.2f} -> {us(R[2]):.2f}")
+R8 = F[l, :8, 1]
+print(f"lb_final: {us(R[0]):.2f} (loads) -> {us(R[1]):.2f} (head ranks) -> {us(R8[6]):.2f} (candidates) -> "
+      f"{us(R8[7]):.2f} (ranks, argmin) -> {us(R[2]):.2f}")
 print(f"final_select: {us(R[3]):.2f} -> {us(R[4]):.2f} -> {us(R[5]):.2f}")
 
 WV = (ctypes.c_ulonglong * (1024 * 4))()
