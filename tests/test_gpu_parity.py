@@ -1215,8 +1215,9 @@ def test_setupnlp_cem_equals_oracle(nat):
         nlp.close()
 
 
-@pytest.mark.parametrize("samples,elite,iters", [(64, 5, 3), (256, 17, 3), (4096, 64, 2), (1024, 1, 2)])
-def test_setupnlp_cem_shapes_equal_oracle(nat, samples, elite, iters):
+@pytest.mark.parametrize("samples,elite,iters,H", [(64, 5, 3, 20), (256, 17, 3, 20), (4096, 64, 2, 20), (1024, 1, 2, 20),
+                                                   (512, 32, 3, 40)])
+def test_setupnlp_cem_shapes_equal_oracle(nat, samples, elite, iters, H):
     """The CEM's selection (each sample block's in-wave sort, the merge tree of the blocks'
     lists) at other sizes: one block (64 samples), a non-power-of-two elite, the largest
     search (4,096 samples, 64 elite) and elite 1 — the same sequence and fval as oracle.nlp_cem."""
@@ -1229,16 +1230,19 @@ def test_setupnlp_cem_shapes_equal_oracle(nat, samples, elite, iters):
     s, u = d["states"], d["inputs"]
     p = ORCA(control="pwm")
     tr = ETHZ('optimal', True)
-    nlp = setupNLP(20, TS, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, Dynamic(**p), tr,
+    nlp = setupNLP(H, TS, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, Dynamic(**p), tr,
                    samples=samples, elite=elite, iters=iters)
     p6 = [p[k] for k in O.BANK_ORDER]
     try:
         x0, up = s[:, 20].copy(), u[:, 19].copy()
-        xref, _, _ = ConstantSpeed(x0[:2], x0[3], tr, 20, TS, 0)
-        umpc, fval, _, _ = nlp.solve(x0, xref, up)
-        uo, jo = O.nlp_cem(shared(), p6, x0, xref, up, None, False, 20, TS, samples=samples, iters=iters, elite=elite)
+        xref, _, _ = ConstantSpeed(x0[:2], x0[3], tr, H, TS, 0)
+        umpc, fval, xmpc, _ = nlp.solve(x0, xref, up)
+        uo, jo = O.nlp_cem(shared(), p6, x0, xref, up, None, False, H, TS, samples=samples, iters=iters, elite=elite)
         np.testing.assert_array_equal(umpc.T, uo)
         np.testing.assert_allclose(fval, jo, rtol=RTOL_ROLL)
+        bank6 = tuple(np.array([p[k]]) for k in O.BANK_ORDER)
+        traj = O.rollout_euler_nlp(shared(), bank6, x0, uo[None], TS)   # xmpc: the last round's quad
+        np.testing.assert_allclose(xmpc, traj[:, 0, :].T, rtol=RTOL_STEP * 10, atol=1e-12)
     finally:
         nlp.close()
 
