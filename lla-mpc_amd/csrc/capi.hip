@@ -1509,6 +1509,10 @@ struct llampc_nlp {
   double* d_cost = nullptr;              // the sample blocks' sorted lists (keys, then indices), then
                                          // the round's rate-clipped sequences [samples][H][2]
   unsigned* d_ticket = nullptr;
+  NlpResult* h_res = nullptr;            // pinned, coherent, mapped: the last round writes it
+  NlpResult* d_res = nullptr;            //   (device alias), then the solve's number into h_tag
+  uint64_t* h_tag = nullptr;
+  uint64_t* d_tag = nullptr;
   uint64_t calls = 0;
   std::mutex mu;
 };
@@ -1524,6 +1528,8 @@ int llampc_nlp_destroy(llampc_nlp* p) {
     if (p->d_cost) (void)hipFree(p->d_cost);
     if (p->d_ticket) (void)hipFree(p->d_ticket);
     if (p->h_blk) (void)hipHostFree(p->h_blk);
+    if (p->h_res) (void)hipHostFree(p->h_res);
+    if (p->h_tag) (void)hipHostFree(p->h_tag);
   }
   delete p;
   return LLAMPC_OK;
@@ -1548,7 +1554,7 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
   p->cfg = k;
   const size_t H = (size_t)k.H;
   p->in_bytes = sizeof(NlpState) + 8 * (6 + 2 * (H + 1));
-  p->blk_bytes = p->in_bytes + 8 * (6 * (H + 1) + H);
+  p->blk_bytes = p->in_bytes;
   auto cleanup = [&](int code) {
     llampc_nlp_destroy(p);
     return code;
@@ -1560,8 +1566,14 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(NLP staging) failed"));
   std::memset(p->h_blk, 0, p->blk_bytes);
-  double* hh = reinterpret_cast<double*>(p->h_blk + p->in_bytes) + 6 * (H + 1);   // h [H] = Ts
-  for (size_t i = 0; i < H; ++i) hh[i] = k.Ts;
+  if (hipHostMalloc(reinterpret_cast<void**>(&p->h_res), sizeof(NlpResult), hipHostMallocCoherent | hipHostMallocMapped) !=
+          hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&p->h_tag), 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(NLP result) failed"));
+  *p->h_tag = 0;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_res), p->h_res, 0) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_tag), p->h_tag, 0) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_HIP, "hipHostGetDevicePointer(NLP result) failed"));
   if (hipMemcpy(p->d_blk, p->h_blk, p->blk_bytes, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(p->d_ticket, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "NLP solver upload failed"));
@@ -1595,7 +1607,6 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   HIP_TRY(hipMemcpyAsync(p->d_blk, p->h_blk, p->in_bytes, hipMemcpyHostToDevice, s));
   NlpState* ds = reinterpret_cast<NlpState*>(p->d_blk);
   double* dx = reinterpret_cast<double*>(p->d_blk + sizeof(NlpState));
-  double* dtraj = reinterpret_cast<double*>(p->d_blk + p->in_bytes);
   NlpLaunch a{};
   a.la.params = b->d_params;
   a.la.n = 1;
@@ -1611,7 +1622,9 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.top_key = reinterpret_cast<uint64_t*>(p->d_cost);
   a.top_idx = reinterpret_cast<uint32_t*>(a.top_key + (size_t)(k.samples / 64) * nlp_list_len(k.elite));
   a.cand = p->d_cost + 2 * (size_t)k.samples;
-  a.traj = dtraj;
+  a.res = p->d_res;
+  a.host_tag = p->d_tag;
+  a.host_seq = p->calls + 1;
   a.ticket = p->d_ticket;
   a.seed = k.seed;
   a.call = p->calls;
@@ -1635,15 +1648,26 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
     a.last = it == k.iters - 1;         // its completion writes xmpc (nmpc.py:58-60)
     HIP_TRY(launch_nlp(a, s));
   }
-  HIP_TRY(hipMemcpyAsync(p->h_blk, p->d_blk, p->blk_bytes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  // the last round's completion writes the result into pinned memory and then the tag
+  const uint64_t want = p->calls + 1;
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t spins = 0;
+  while (__atomic_load_n(p->h_tag, __ATOMIC_ACQUIRE) != want) {
+    __builtin_ia32_pause();
+    if ((++spins & 0xFFF) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      HIP_TRY(hipStreamSynchronize(s));
+      if (__atomic_load_n(p->h_tag, __ATOMIC_ACQUIRE) == want) break;
+      return fail(LLAMPC_E_DEVICE, "NLP solve %llu: completion tag never arrived", (unsigned long long)want);
+    }
+  }
   p->calls++;
   b->launches += k.iters;
+  const NlpResult* r = const_cast<const NlpResult*>(p->h_res);
   for (int i = 0; i < H; ++i)
-    for (int j = 0; j < 2; ++j) umpc[2 * i + j] = hs->best_u[i][j];
-  if (fval) *fval = hs->best_j;
-  if (xmpc) std::memcpy(xmpc, reinterpret_cast<double*>(p->h_blk + p->in_bytes), 6 * (size_t)(H + 1) * sizeof(double));
-  if (hs->best_it < 0) return fail(LLAMPC_E_DEVICE, "no finite objective in %d rounds of %d samples", k.iters, k.samples);
+    for (int j = 0; j < 2; ++j) umpc[2 * i + j] = r->best_u[i][j];
+  if (fval) *fval = r->best_j;
+  if (xmpc) std::memcpy(xmpc, &r->traj[0][0], 6 * (size_t)(H + 1) * sizeof(double));
+  if (r->best_it < 0) return fail(LLAMPC_E_DEVICE, "no finite objective in %d rounds of %d samples", k.iters, k.samples);
   return LLAMPC_OK;
 }
 

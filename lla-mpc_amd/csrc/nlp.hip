@@ -28,7 +28,7 @@ namespace llampc {
 #ifdef LLAMPC_STAMPS
 // Diagnostic build only: s_memrealtime per block and phase of the last launch
 // (tools/diag/nlp_phases.py): 0 entry, 1 drawn, 2 rate-clipped, 3 rolled out; the completing
-// block: 4 keyed, 5 sorted, 6 elite drawn, 7 elite clipped, 8 done.
+// block: 4 keyed, 5 sorted, 6 elite drawn, 7 elite clipped, 8 done; 9 staged (sample blocks).
 static __device__ unsigned long long g_nlp_ph[32][12];
 #define NLP_STAMP(slot)                                                                               \
   do {                                                                                                \
@@ -98,23 +98,43 @@ __device__ __forceinline__ void nlp_cx(uint64_t& k, uint32_t& i, int j, bool low
   }
 }
 
+__device__ __forceinline__ void nlp_traj_quad(const NlpLaunch& a, const double* sx, const double* ub, const double* x0);
+
 // xmpc (nmpc.py:58-60): the NLP's Euler trajectory of the best sequence over all rounds, by
 // one quad of the completing block (the sample blocks' fast rollout, the general re-run when
 // its domain check fails) — it was a separate one-lane launch of the general evaluation, 32 us.
-__device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, unsigned char* smem, double* ub, bool better) {
+__device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, unsigned char* smem, double* ub, bool better,
+                                               double bj, int bit) {
   const int tid = threadIdx.x, H = a.H;
   const NlpState* st = a.st;
+  NlpResult* res = a.res;
   __syncthreads();                      // the elite rows are read; best_u is final
   double* sx = ub + 2 * (size_t)H;      // after the sequence: xref [H+1][2], x0 [6]
   double* x0 = sx + 2 * (size_t)(H + 1);
-  for (int e = tid; e < 2 * H; e += kBlock) ub[e] = better ? ub[e] : (&st->best_u[0][0])[e];
+  for (int e = tid; e < 2 * H; e += kBlock) {
+    const double v = better ? ub[e] : (&st->best_u[0][0])[e];
+    ub[e] = v;
+    (&res->best_u[0][0])[e] = v;
+  }
+  if (tid == 0) {
+    res->best_j = bj;
+    res->best_it = bit;
+  }
   for (int e = tid; e <= H; e += kBlock) {
     sx[2 * e] = a.xref[e];
     sx[2 * e + 1] = a.xref[(H + 1) + e];
   }
   if (tid < 6) x0[tid] = a.x0[tid];
   __syncthreads();
-  if (tid >= 4) return;
+  if (tid < 4) nlp_traj_quad(a, sx, ub, x0);
+  __threadfence_system();               // the result's host-memory stores, then the tag
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(a.host_tag, a.host_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// one quad: the rollout with the trajectory written (lane 0) into the host result
+__device__ __forceinline__ void nlp_traj_quad(const NlpLaunch& a, const double* sx, const double* ub, const double* x0) {
+  const int tid = threadIdx.x;
   constexpr int LPM = 4;
   const int sub = tid;
   const Tire t = load_tire(a.la.params, 1, 0);
@@ -124,9 +144,9 @@ __device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, unsigned char
   const StageK sk = make_stage<LPM>(veh, t, sub, 1.0);
   const FusedK fq = make_fused(veh, sk, Ts, false);
   const fm::FmK K = fm::FmK::load();
-  double* out = sub == 0 ? a.traj : nullptr;
+  double* out = sub == 0 ? &a.res->traj[0][0] : nullptr;
   if (sub == 0)
-    for (int m = 0; m < 6; ++m) a.traj[m] = x0[m];
+    for (int m = 0; m < 6; ++m) out[m] = x0[m];
   bool bad = false;
   (void)rollout<1, false, LPM, 0, true, false, true, true>(a.la, 0, 0, x0, sx, ub, veh, t, sk, q, Ts, a.up0, a.up1, K, fq,
                                                            bad, out);
@@ -212,6 +232,10 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
     st->std_[k][j] = sqrt(s / E) + a.std_floor;
     if (better) st->best_u[k][j] = eu[2 * k + j];
   }
+  // the result (the last round): best objective and round, before this round's update
+  const double bj = better ? c0 : st->best_j;
+  const int bit = better ? a.it : st->best_it;
+  __syncthreads();                                  // read before thread 0 updates them
   if (tid == 0) {
     if (better) {
       st->best_j = c0;
@@ -220,11 +244,18 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
     __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   NLP_STAMP(8);
-  if (a.last) nlp_trajectory(a, smem, eu, better);
+  if (a.last) nlp_trajectory(a, smem, eu, better, bj, bit);
 }
 
 }  // namespace
 
+// ST: the candidates' per-step input terms staged in LDS once per block (pwm, delta, sin /
+// cos delta, the input-rate cost term, feasibility: the plan kernel's staged Euler layout,
+// [k][c][kStageW]), so the rollout loop reads them instead of forming them per step; when
+// 64 x H x 64 B fit beside the rest (H <= kNlpStageH).
+constexpr int kNlpStageH = 28;
+
+template <bool ST>
 __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Scratch sc(smem);
@@ -235,6 +266,7 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   double* Ul = sx + 2 * (H + 1);                                            // [64][H][2]
   double* x0 = Ul + 2 * (size_t)kPerBlock * H;                              // [6]
   uint64_t* ks = reinterpret_cast<uint64_t*>(x0 + 6);                       // [64] the samples' keys
+  double* su = reinterpret_cast<double*>(ks + 64);                          // ST: [H][64][kStageW]
   const NlpState* st = a.st;
   NLP_STAMP(0);
   for (int e = tid; e <= H; e += kBlock) {
@@ -255,6 +287,30 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   __syncthreads();
   NLP_STAMP(2);
   for (int e = tid; e < kPerBlock * H * 2; e += kBlock) st_wt(&a.cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
+  const fm::FmK K = fm::FmK::load();
+  if constexpr (ST) {
+    const CostK& q0 = a.la.cost;
+    // consecutive threads take consecutive candidates of one step: their 64-B records are
+    // adjacent in LDS (one step per thread-row was a 4 KB stride: every write one bank)
+    for (int f = tid; f < kPerBlock * H; f += kBlock) {
+      const int k = f >> 6, c = f & (kPerBlock - 1), e = c * H + k;
+      const double ua = Ul[2 * e], dl = Ul[2 * e + 1];
+      double sd, cd;
+      if (fm::sincos_fast_ok(dl)) fm::sincos_fast(dl, &sd, &cd, K);
+      else LL_SINCOS(dl, &sd, &cd);
+      const double p0 = k ? Ul[2 * e - 2] : a.up0, p1 = k ? Ul[2 * e - 1] : a.up1;
+      const double d0 = ua - p0, d1 = dl - p1;
+      double* o = su + kStageW * (k * kPerBlock + c);
+      o[0] = ua;
+      o[1] = dl;
+      o[2] = sd;
+      o[3] = cd;
+      o[6] = act_term(q0, d0, d1);
+      o[7] = (!q0.enforce || input_feasible(q0, ua, dl, d0, d1)) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    NLP_STAMP(9);
+  }
   // rollouts: a quad per sample (the plan kernel's NLP-Euler fast stage + the general re-run)
   const int sub = tid % LPM, c = tid / LPM;
   const Tire t = load_tire(a.la.params, 1, 0);
@@ -274,17 +330,24 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   pin_vgpr(Ts);
   const StageK sk = make_stage<LPM>(veh, t, sub, 1.0);
   const FusedK fq = make_fused(veh, sk, Ts, false);
-  const fm::FmK K = fm::FmK::load();
   bool bad = false;
-  double J = rollout<1, false, LPM, 0, true, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K,
-                                                          fq, bad);
+  double J;
+  if constexpr (ST)
+    J = rollout<1, true, LPM, 0, true>(a.la, c, 0, x0, sx, su, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, bad);
+  else
+    J = rollout<1, false, LPM, 0, true, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, bad);
   int bi = bad;
   bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX1, 0xF, 0xF, false);
   bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX2, 0xF, 0xF, false);
   if (__builtin_expect(__any(bi), 0)) {
     bool unused = false;
-    if (bi) J = rollout<1, false, LPM, 0, false, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K,
-                                                              fq, unused);
+    if (bi) {
+      if constexpr (ST)
+        J = rollout<1, true, LPM, 0, false>(a.la, c, 0, x0, sx, su, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, unused);
+      else
+        J = rollout<1, false, LPM, 0, false, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K, fq,
+                                                          unused);
+    }
   }
   NLP_STAMP(3);
   if (sub == 0) ks[c] = nlp_key(J);
@@ -305,7 +368,8 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
 }
 
 size_t nlp_lds_bytes(int H, int samples, int elite) {
-  const size_t blocks = kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 48 + 8 * 64;
+  const size_t blocks = kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 48 + 8 * 64 +
+                        (H <= kNlpStageH ? 8 * kStageW * 64 * (size_t)H : 0);
   const size_t nll = (size_t)(samples / 64) * nlp_list_len(elite);
   const size_t last = kScratchBytes + 24 * nll + 16 * (size_t)elite * H + 16 * (size_t)(H + 1) + 48;
   return std::max(blocks, last);
@@ -313,8 +377,13 @@ size_t nlp_lds_bytes(int H, int samples, int elite) {
 
 hipError_t launch_nlp(const NlpLaunch& a, hipStream_t s) {
   const size_t lds = std::max<size_t>(nlp_lds_bytes(a.H, a.samples, a.elite), 82 * 1024);
-  allow_lds(nlp_kernel);
-  hipLaunchKernelGGL(nlp_kernel, dim3(a.samples / 64), dim3(kBlock), lds, s, a);
+  if (a.H <= kNlpStageH) {
+    allow_lds(nlp_kernel<true>);
+    hipLaunchKernelGGL(nlp_kernel<true>, dim3(a.samples / 64), dim3(kBlock), lds, s, a);
+  } else {
+    allow_lds(nlp_kernel<false>);
+    hipLaunchKernelGGL(nlp_kernel<false>, dim3(a.samples / 64), dim3(kBlock), lds, s, a);
+  }
   return hipGetLastError();
 }
 

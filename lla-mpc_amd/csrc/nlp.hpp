@@ -22,6 +22,15 @@ struct NlpState {
 
 // One CEM iteration's launch.  Scalars only (no arrays): the kernel never takes the address of
 // its argument (which would copy it to scratch).
+// The solve's result as the last round's completion writes it into pinned host memory (then
+// a system-scope fence and the host tag): no D2H copy, no stream synchronisation.
+struct NlpResult {
+  double best_u[LLAMPC_HMAX][2];
+  double traj[LLAMPC_HMAX + 1][6];     // xmpc: the NLP's Euler trajectory of best_u
+  double best_j;
+  int32_t best_it, pad;
+};
+
 struct NlpLaunch {
   LookaheadLaunch la;            // params [6][1], veh (NLP form), cost, H, Ts, integrator EULER_NLP
   NlpState* st;
@@ -30,7 +39,9 @@ struct NlpLaunch {
   uint64_t* top_key;             // [samples / 64][len] each sample block's best (sorted keys),
   uint32_t* top_idx;             //   then their sample indices (len = nlp_list_len(elite))
   double* cand;                  // [samples][H][2] the round's sequences after the rate clip
-  double* traj;                  // [H+1][6] the last round: the best sequence's trajectory
+  NlpResult* res;                // the last round: the result, in pinned host memory (device alias)
+  uint64_t* host_tag;            //   then this solve's number (host alias spun on by the caller)
+  uint64_t host_seq;
   unsigned* ticket;
   uint64_t seed, call;           // Philox key; counter word 1 = the solve call number
   double up0, up1;               // uprev (du_0, nmpc.py:65-66)

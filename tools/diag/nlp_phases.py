@@ -37,7 +37,7 @@ for t in range(10, 16):
     base = Z[:nb, 0].min()
     us = lambda v: (v - base) / 100.0  # noqa: E731
     win = int(np.argmax(Z[:nb, 8]))
-    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (1, 2, 3)]
+    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (1, 2, 9, 3)]
     comp = [f"{k}: {us(Z[win, k]):.1f}" for k in (4, 5, 6, 7, 8)]
     print(f"solve {t}: blocks drawn/clipped/rolled (min/max) {' '.join(row)} | completion (block {win}) {' '.join(comp)}",
           flush=True)
