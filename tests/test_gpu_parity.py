@@ -961,6 +961,35 @@ def test_bank_concurrency_lane_split_equals_default(nat):
         b_bank.close()
 
 
+def test_shared_queue_stream_equals_dedicated(nat, monkeypatch):
+    """A bank on a plain stream (LLAMPC_SHARED_QUEUES=1, shared hardware queues) and one on its
+    own full-CU-mask stream (the default) tick to identical records."""
+    from llampc import _native
+    from llampc.mpc import ModelBank, generate_bank
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    N, H, W = 2000, 20, 3
+    a_bank = ModelBank(generate_bank(N, seed=4), W=W, device=0)
+    monkeypatch.setenv("LLAMPC_SHARED_QUEUES", "1")
+    b_bank = ModelBank(generate_bank(N, seed=4), W=W, device=0)
+    monkeypatch.delenv("LLAMPC_SHARED_QUEUES")
+    try:
+        for t in range(1, W + 3):
+            U = np.repeat(u[:, t:t + H].T[None], 3, axis=0)
+            U[1:, :, 1] += 0.01
+            args = (s[:, t - 1], u[:, t - 1], s[:, t], U, s[:2, t:t + H + 1], u[:, t - 1])
+            A = _native.plan_out_to_dict(a_bank.plan_raw(*args, K=5)[0])
+            B = _native.plan_out_to_dict(b_bank.plan_raw(*args, K=5)[0])
+            for k in A:
+                if isinstance(A[k], np.ndarray):
+                    np.testing.assert_array_equal(A[k], B[k], err_msg=k)
+                else:
+                    assert A[k] == B[k] or (A[k] != A[k] and B[k] != B[k]), (k, A[k], B[k])
+    finally:
+        a_bank.close()
+        b_bank.close()
+
+
 def test_work_queue_layout_equals_static_and_oracle(nat, monkeypatch):
     """The throughput layout (launch_plan's work queue: one look-ahead block per CU, waves
     taking units of models from the bank's counter) at N = 3000, C = 64 (750 static blocks >
