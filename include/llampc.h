@@ -170,6 +170,9 @@ int llampc_bank_launches(const llampc_bank* bank, int64_t* launches);
 int llampc_bank_window(llampc_bank* bank, double* ring, int32_t* window_count);
 /* stream the bank launches on (hipStream_t as void*); NULL = its own stream */
 int llampc_bank_set_stream(llampc_bank* bank, void* stream);
+/* the stream the bank launches on now (its own — a hardware queue of its own, see
+ * INTEGRATION.md — or the one set above), for callers that enqueue their own work with it */
+int llampc_bank_stream(const llampc_bank* bank, void** stream);
 /* the number of banks the caller ticks concurrently on this device (default 1; BASELINE
  * config 5 ticks two tracks together: 2).  The look-ahead sizes its launch for 1/banks of the
  * chip (its lane split), so the concurrent launches are resident together — replaces nothing

@@ -720,6 +720,12 @@ int llampc_bank_window(llampc_bank* b, double* ring, int32_t* window_count) {
   return LLAMPC_OK;
 }
 
+int llampc_bank_stream(const llampc_bank* b, void** stream) {
+  if (!b || !stream) return fail(LLAMPC_E_ARG, "NULL argument");
+  *stream = (void*)b->stream;
+  return LLAMPC_OK;
+}
+
 int llampc_bank_set_concurrency(llampc_bank* b, int32_t banks) {
   if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
   if (banks < 1 || banks > 64) return fail(LLAMPC_E_ARG, "banks=%d outside [1, 64]", banks);

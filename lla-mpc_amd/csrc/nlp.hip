@@ -45,8 +45,23 @@ extern "C" int llampc_debug_nlp_stamps(unsigned long long* out) {
 
 namespace {
 
-// sample s of iteration `it` before the rate chain (the bounds applied)
-__device__ __forceinline__ double nlp_raw(const NlpLaunch& a, const NlpState* st, int s, int k, int j) {
+// The search's noise: one Philox4x32-10 call per PAIR of values, the counter (i / 2, call lo,
+// call hi, round + 1): value i takes the 16-bit halves (low for even i, high for odd) of the
+// four words, z = (h0 + h1 + h2 + h3 + 2) 2^-16 - 2 — the 4-term Irwin-Hall variate of the
+// controller's candidates (ctl_z) on 16-bit cells (centred: mean 0, variance 1/3 - 1/(3 2^32)),
+// at half the Philox calls (the sample blocks' draw was 4.3 of a 26 us round).
+__device__ __forceinline__ void nlp_z2(uint32_t pair, uint64_t call, uint64_t seed, uint32_t stream, double& z0,
+                                       double& z1) {
+  const Philox4 w = philox4x32_10(Philox4{pair, (uint32_t)call, (uint32_t)(call >> 32), stream}, (uint32_t)seed,
+                                  (uint32_t)(seed >> 32));
+  const uint32_t lo = (w.x & 0xFFFFu) + (w.y & 0xFFFFu) + (w.z & 0xFFFFu) + (w.w & 0xFFFFu) + 2u;
+  const uint32_t hi = (w.x >> 16) + (w.y >> 16) + (w.z >> 16) + (w.w >> 16) + 2u;
+  z0 = (double)lo * 0x1p-16 - 2.0;      // exact: integers < 2^19 and a power-of-two scale
+  z1 = (double)hi * 0x1p-16 - 2.0;
+}
+
+// sample s of iteration `it` before the rate chain (the bounds applied), given its variate z
+__device__ __forceinline__ double nlp_raw_z(const NlpLaunch& a, const NlpState* st, int s, int k, int j, double z) {
 #pragma clang fp contract(off)
   const double m = st->mean[k][j];
   double u;
@@ -55,7 +70,6 @@ __device__ __forceinline__ double nlp_raw(const NlpLaunch& a, const NlpState* st
   } else if (s == 1 && a.it == 0 && a.has_hold) {
     u = j ? a.up1 : a.up0;
   } else {
-    const double z = ctl_z((uint32_t)((s * a.H + k) * 2 + j), a.call, a.seed, (uint32_t)(a.it + 1));
     const double zu = z * 1.7320508075688772;       // unit variance (sqrt(3), as np.sqrt(3.0))
     const double d = zu * st->std_[k][j];
     u = m + d;
@@ -274,9 +288,14 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     sx[2 * e + 1] = a.xref[(H + 1) + e];
   }
   if (tid < 6) x0[tid] = a.x0[tid];
-  for (int e = tid; e < kPerBlock * H * 2; e += kBlock) {
-    const int r = e / (2 * H), q = e - r * 2 * H;
-    Ul[e] = nlp_raw(a, st, blk * kPerBlock + r, q >> 1, q & 1);
+  // value i = (s H + k) 2 + j of the round; pair i / 2 = (s H + k): the (j = 0, 1) values of
+  // one (sample, step) share a Philox call
+  for (int e = tid; e < kPerBlock * H; e += kBlock) {
+    const int r = e / H, k = e - r * H, s = blk * kPerBlock + r;
+    double z0, z1;
+    nlp_z2((uint32_t)(s * H + k), a.call, a.seed, (uint32_t)(a.it + 1), z0, z1);
+    Ul[2 * e] = nlp_raw_z(a, st, s, k, 0, z0);
+    Ul[2 * e + 1] = nlp_raw_z(a, st, s, k, 1, z1);
   }
   __syncthreads();
   NLP_STAMP(1);

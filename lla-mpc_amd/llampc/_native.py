@@ -108,6 +108,7 @@ _SIGNATURES = {
     "llampc_bank_window": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int32)]),
     "llampc_bank_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "llampc_bank_set_concurrency": (C.c_int, [C.c_void_p, C.c_int32]),
+    "llampc_bank_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "llampc_bank_set_raceline": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, _dp, _dp, C.c_int32]),
     "llampc_plan_async": (C.c_int, [C.c_void_p, C.c_void_p]),
     "llampc_plan_wait": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -127,6 +127,12 @@ class ModelBank:
     def set_stream(self, stream_ptr: int | None):
         nat.check(nat.load().llampc_bank_set_stream(self.handle, stream_ptr))
 
+    def stream_handle(self) -> int:
+        """The hipStream_t the bank launches on (its own stream: a hardware queue of its own)."""
+        h = nat.C.c_void_p()
+        nat.check(nat.load().llampc_bank_stream(self.handle, nat.C.byref(h)))
+        return int(h.value or 0)
+
     def set_concurrency(self, banks: int):
         """The number of banks ticked concurrently on this device (default 1; two tracks
         ticked together: 2): each look-ahead launch is sized for 1/banks of the chip, so the
