@@ -141,10 +141,13 @@ class ShardedBank:
         self.h_merged = torch.empty(B, dtype=torch.uint8).pin_memory()
         self._inputs = None
         # every stage of the tick (input upload, plan, all-gather, merge, read-back) runs on
-        # ONE stream, the bank's own — a hardware queue of its own, so two shards ticked
-        # together (config 5) never serialise on a shared queue — wrapped for torch
-        # (torch's default stream has handle 0, which the C ABI reads as "the bank's stream")
-        self.stream = torch.cuda.ExternalStream(self.bank.stream_handle(), device=dev)
+        # ONE stream, which is also the bank's: torch's default stream has handle 0, which the
+        # C ABI reads as "the bank's own stream", so it is never used to launch a tick.  A
+        # torch stream, not the bank's own wrapped as an ExternalStream: torch's caching
+        # allocator keeps using the streams its blocks were used on after the shard is closed
+        # (the self-spawned 2-rank bench crashed at the end with the bank's stream destroyed)
+        self.stream = torch.cuda.Stream(device=dev)
+        self.bank.set_stream(self.stream.cuda_stream)
         # native exchange (nccl): the all-gather is issued by llampc_exchange_device straight
         # on the tick's stream, over the communicator of a group of its own — no c10d stream
         # hand-off, ~1 us of host time per tick.  LLAMPC_C10D_EXCHANGE=1 keeps the c10d call.
