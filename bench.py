@@ -409,9 +409,9 @@ def main():
         step(args.warmup + i, ex_events[i // TIMING_SAMPLE] if ex_events and i % TIMING_SAMPLE == 0 else None)
     t_issue = time.perf_counter() - t0       # host time to enqueue the K ticks
     torch.cuda.synchronize()
-    if world > 1:
+    if world > 1:                            # (at world 1 there is no barrier to re-synchronise after)
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
         el = max_over_ranks(el)
