@@ -99,12 +99,13 @@ def test_ctl_reference_fast_starts_and_lap_end(nat, name):
             ctl.close()
 
 
-@pytest.mark.parametrize("N,C,H,W,K,name,ticks", [
-    (200, 8, 20, 4, 10, "ETHZ", 14),
-    (6, 8, 20, 4, 10, "ETHZ", 10),            # N < K: top-K padded with -1, never in mu-hat
-    (1000, 64, 40, 10, 10, "ETHZMobil", 16),  # the bench shape of the controller (C = 64, H = 40)
+@pytest.mark.parametrize("N,C,H,W,K,name,ticks,lap", [
+    (200, 8, 20, 4, 10, "ETHZ", 14, None),
+    (6, 8, 20, 4, 10, "ETHZ", 10, None),            # N < K: top-K padded with -1, never in mu-hat
+    (1000, 64, 40, 10, 10, "ETHZMobil", 16, None),  # the bench shape of the controller (C = 64, H = 40)
+    (200, 8, 20, 4, 10, "ETHZ", 16, 3),             # lap_projidx = 3: the lap wrap (rt.py:287-296) every few ticks
 ])
-def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks):
+def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks, lap):
     """LLAMPC.tick in device mode (ONE launch per tick) against ControllerOracle in closed
     loop with the RK6 plant (friction dropping 1/260 per tick): every tick's reference (and the
     host ConstantSpeed on the same mu / scale / projidx), candidates, look-back top-K,
@@ -113,8 +114,11 @@ def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks):
     from llampc.mpc import LLAMPC, ModelBank, generate_bank
     from llampc.mpc.planner import ConstantSpeed
     tr, ref = tracks(name)
+    if lap is not None:
+        tr.lap_projidx = lap
     bank_p = generate_bank(N, seed=21)
     orc = O.ControllerOracle(shared(), bank_p, ref, tr.lap_projidx, H=H, C=C, K=K, W=W, Ts=TS)
+    wraps = 0
     plant = O.Vehicle.from_params(O.orca_params())
     x = start_state(name, tr)
     with ModelBank(bank_p, W=W, device=0) as b, LLAMPC(b, tr, H=H, C=C, K=K, debug_inputs=True) as ctl:
@@ -132,6 +136,7 @@ def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks):
             host, hidx, _ = ConstantSpeed(x[:2], x[3], tr, H, TS, projidx, scale=raw.scale_used, curr_mu=raw.mu_used)
             np.testing.assert_allclose(xref, host, rtol=1e-10, atol=1e-12, err_msg=f"tick {t}")
             assert raw.projidx == (0 if hidx > tr.lap_projidx else hidx) == o["projidx"], t
+            wraps += int(hidx > tr.lap_projidx)
             projidx = raw.projidx
             assert res.nominal == o["warm"] == (t <= W)
             assert res.best_cand == o["best_cand"], (t, res.best_cand, o["best_cand"])
@@ -154,6 +159,8 @@ def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks):
             plant.Dr *= 1 - 1 / 260.0
             xn, _ = O.sim_continuous(plant, x, u.reshape(2, 1), [0, TS])
             x = xn[:, -1]
+    if lap is not None:
+        assert wraps >= 2, wraps                    # the case exercised the wrap
 
 
 def test_ctl_two_tracks_async_equal_sequential(nat):
