@@ -47,7 +47,7 @@ FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation
 # Issue roofline: instructions per rollout step of the fast look-ahead loop, per lane, by lane
 # split (tools/diag/isa_counts.py on the current sources), and the chip's fp64 VALU issue
 # capacity: 1,024 SIMDs x 16 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md max clock).
-ISSUE_INSTR_PER_STEP = {4: 456, 2: 568, 1: 814}   # tools/diag/isa_counts.py (LPM 1: work queue)
+ISSUE_INSTR_PER_STEP = {4: 444, 2: 556, 1: 777}   # tools/diag/isa_counts.py (LPM 1: work queue)
 ISSUE_PEAK_LANE_INSTR = 1024 * 16 * 2.4e9
 
 

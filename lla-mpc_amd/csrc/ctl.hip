@@ -56,7 +56,7 @@ constexpr size_t kCtlPollBytes = 4096;   // ctl_complete's area (layout there)
 // Diagnostic build only: s_memrealtime (100 MHz) per block and phase of the last launch
 // (tools/diag/ctl_phases.py).  Look-ahead blocks: 0 entry, 1 staged, 10 walk done, 2 walk
 // barrier, 3 selection, 4 rolled out, 5 published; look-back blocks: 0 entry, 6 scored,
-// 7 lb_final done (ticket winner), 8 slots polled, 9 record written.
+// 7 lb_final done (ticket winner), 8 slots polled, 11 record stores issued, 9 record written.
 static __device__ unsigned long long g_ctl_ph[64][12];
 #define CTL_STAMP(blk, slot)                                                                   \
   do {                                                                                         \
@@ -248,7 +248,12 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     o->df_mean = df;
     __hip_atomic_store(&c.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  CTL_STAMP(blockIdx.x, 11);
+#ifdef LLAMPC_CTL_WAITCNT   // diagnostic A/B: this wave's stores complete, no L2 write-back
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+#else
   __threadfence_system();
+#endif
   __syncthreads();
   CTL_STAMP(blockIdx.x, 9);
   if (tid == 0) __hip_atomic_store(c.host_tag, c.host_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

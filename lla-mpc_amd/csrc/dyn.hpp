@@ -312,8 +312,11 @@ constexpr bool kPairLA = false;
 
 // F = D sin(C atan(B slip)) with slip = dsel - atan2(yy, den) for the front tire
 // (dsel = delta) and atan2(yy, den) for the rear (dsel = 0); yy = lf om + vy | lr om - vy
-// (dynamic.py:149-152 / :215-220).  The divisors go to the lane's Dom.
-template <bool LEAN = false>
+// (dynamic.py:149-152 / :215-220).  The divisors go to the lane's Dom.  LO = false: the
+// caller records the lower bound itself (the LPM-1 lane: |den| once for both chains — the
+// divisor max(|yy|, |den|) is at least |den|, so min |den| >= 2^-1000 is a sufficient test,
+// stricter only at a standstill, which then takes the general path).
+template <bool LEAN = false, bool LO = true>
 __device__ __forceinline__ double chain_fast(const Chain& c, double den, double vy, double om,
                                              double dsel, Dom& dm, const fm::FmK& K) {
   const double yy = fma(c.lw, om, c.sg * vy);
@@ -321,7 +324,7 @@ __device__ __forceinline__ double chain_fast(const Chain& c, double den, double 
   const double a2 = fm::atan2_fast<LEAN>(yy, den, K, h2);
   const double z = c.B * fma(-c.sg, a2, dsel);
   const double at = fm::atan_fast<LEAN>(z, K);
-  dm.lo = fm::vmin(dm.lo, h2);
+  if constexpr (LO) dm.lo = fm::vmin(dm.lo, h2);
   dm.hi = fm::vmax(dm.hi, h2);
   return c.D * fm::sin_wide<LEAN>(c.C * at, K);
 }
@@ -472,8 +475,9 @@ __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, doub
   } else if constexpr (LEAN && kPairLA) {
     chain_pair(sk.ch[0], sk.ch[1], den, vy, om, d, dm, K, f.Ffy, f.Fry);
   } else {
-    f.Ffy = chain_fast<LEAN>(sk.ch[0], den, vy, om, d, dm, K);
-    f.Fry = chain_fast<LEAN>(sk.ch[1], den, vy, om, 0.0, dm, K);
+    f.Ffy = chain_fast<LEAN, false>(sk.ch[0], den, vy, om, d, dm, K);
+    f.Fry = chain_fast<LEAN, false>(sk.ch[1], den, vy, om, 0.0, dm, K);
+    dm.lo = fm::vmin_abs(den, dm.lo);
   }
   if constexpr (SCALED && LPM == 1) {
     // LPM = 1 with the scaled yaw Psi = (2/pi) psi (k_fused): the quad's fold in one lane —

@@ -180,19 +180,29 @@ constexpr double kAtanR[10] = {
     -0.06649613695291669,  0.05736332165907643,  -0.04483334622272886,
     0.02275052699336167};
 constexpr double kTanPi8 = 0.41421356237309503;
-// Lean cores of the look-ahead rollouts (kLeanLA): 8-term atan (1.1e-13 relative on |t| <=
-// tan(pi/8)) and 8-term sin_wide (5e-14 absolute to |a| = 2, 2.6e-13 to 3), and the division
-// without its residual correction (<= 18 ulp): ~1e-13 relative on the tire forces against the
-// <= 4 ulp of the precise cores, which the look-back keeps (its errors are ranked).  Round 4
-// went from 9 to 8 terms (tools/fit_fastmath.py): 12 fewer instructions per LPM-4 step, 24 per
-// LPM-1 step; alternating A/B (profiles/r04/ab_lean8.log) 26.8-27.2 -> 26.6-26.7 us per tick at
-// C = 1 and 394-404 -> 383-390 us at C = 64 — the rollouts stay within 1e-7 of the NumPy
-// restatement (north star: 1e-5).  -DLLAMPC_LEAN_TERMS=9 builds the round-3 cores.
+// Lean cores of the look-ahead rollouts (kLeanLA): 7-term atan (3.0e-12 relative on |t| <=
+// tan(pi/8)) and 7-term sin_wide (1.0e-11 absolute to |a| = 2, 3.9e-11 to 3), and the division
+// without its residual correction (<= 18 ulp): ~1e-11 relative on the tire forces against the
+// <= 4 ulp of the precise cores, which the look-back keeps (its errors are ranked).  Round 3
+// shipped 9 terms; round 4 went to 8 (12 fewer instructions per LPM-4 step, 24 per LPM-1 step;
+// profiles/r04/ab_lean8.log) and then 7 (another 12 / 32 with the LPM-1 lane's single
+// lower-bound record, dyn.hpp forces_fast): alternating A/B (profiles/r04/ab_lean7.log)
+// 26.75-26.91 -> 26.07-26.35 us per tick at C = 1 and 390-394 -> 372-373 us at C = 64.  The
+// rollout costs stay within 1e-6 of the NumPy restatement (the worst of the GPU tests' 10^6
+// costs: 1.2e-7, a tracking term's cancellation x - xref; north star: 1e-5).
+// -DLLAMPC_LEAN_TERMS=8 / 9 build the earlier cores (tools/fit_fastmath.py fits them).
 #ifndef LLAMPC_LEAN_TERMS
-#define LLAMPC_LEAN_TERMS 8
+#define LLAMPC_LEAN_TERMS 7
 #endif
 constexpr int kLeanTerms = LLAMPC_LEAN_TERMS;
-#if LLAMPC_LEAN_TERMS == 8
+#if LLAMPC_LEAN_TERMS == 7
+constexpr double kAtanRL[7] = {-0.3333333333144073, 0.1999999891728858, -0.14285612511387016,
+                               0.11107495135714474, -0.09028983500350463, 0.07135325122330678,
+                               -0.04043224825887161};
+constexpr double kSinWQL[7] = {-0.1666666666651697, 0.008333333317028357, -0.00019841266938549256,
+                               2.755712516942648e-06, -2.5045917650344973e-08, 1.5957259420467993e-10,
+                               -6.809345001958508e-13};
+#elif LLAMPC_LEAN_TERMS == 8
 constexpr double kAtanRL[8] = {-0.33333333333266196, 0.19999999949854794, -0.142857081103604,
                                0.11110819716745676, -0.09084101895346429, 0.07604800046078292,
                                -0.06027307460946675, 0.03295679541870136};

@@ -4,7 +4,7 @@ restatement: ConstantSpeed with mu-hat, the Philox candidates, the look-back win
 look-ahead of the selected and top-K models, mu-hat) tick by tick in closed loop with the RK6
 plant, and the device ConstantSpeed against the reference's own planner vectors.
 Tolerances: candidates and indices exact; the reference trajectory 1e-10 (the device walks the
-banded-solve spline coefficients, the oracle the reference's dense solve); costs 1e-7
+banded-solve spline coefficients, the oracle the reference's dense solve); costs 1e-6
 (rollouts, as the plan kernel's tests); mu-hat 1e-12."""
 import os
 
@@ -17,7 +17,7 @@ from oracle import llampc_oracle as O
 pytestmark = pytest.mark.gpu
 
 TS = 0.02
-RTOL_ROLL = 1e-7
+RTOL_ROLL = 1e-6
 
 
 @pytest.fixture(scope="module")

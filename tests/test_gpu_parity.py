@@ -1,7 +1,7 @@
 """GPU parity tests: the HIP path (through the C ABI) against the pinned oracle and the
 reference-generated golden vectors.  Tolerances: fp64 values 1e-9 relative for one
-integration step (ocml vs NumPy transcendentals differ by ulps), 1e-7 for H-step rollouts
-and their costs (north star bound: 1e-5); indices exact (tie-tolerant only where stated)."""
+integration step (ocml vs NumPy transcendentals differ by ulps), 1e-6 for H-step rollouts
+and their costs (the look-ahead's 7-term lean cores; north star bound: 1e-5); indices exact (tie-tolerant only where stated)."""
 import os
 
 import numpy as np
@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 TS = 0.02
 RTOL_STEP = 1e-9
-RTOL_ROLL = 1e-7
+RTOL_ROLL = 1e-6
 
 
 @pytest.fixture(scope="module")
@@ -569,7 +569,7 @@ def test_baseline_sizes_properties(nat, N, H, track):
 def test_c64_work_queue_full_size_vs_oracle(nat):
     """The bench's C = 64 throughput shape at full size — N = 10^4, C = 64, H = 20, where
     launch_plan takes the 8-wave work-queue layout (10^4 units >= 4 per wave slot of 255
-    CUs) — against the oracle: all 640,000 (model, candidate) costs at 1e-7, the selected and
+    CUs) — against the oracle: all 640,000 (model, candidate) costs at 1e-6, the selected and
     top-K models' best candidates and the global argmin exact, the look-back selection exact."""
     from llampc.mpc import CandidateGenerator, ModelBank, generate_bank, plan
     from llampc.mpc.planner import ConstantSpeed
@@ -668,11 +668,11 @@ def test_fast_cores_ulp_on_domain(nat):
 
 
 def test_lean_cores_accuracy_on_domain(nat):
-    """The look-ahead's lean cores (math fn 10-12: 8-term atan and sin_wide, division without
-    its residual step) on the same domains vs NumPy: atan2 / atan within 1024 ulp (~2.3e-13
-    relative; the fit's own error is 1.05e-13), sin_wide within 512 ulp for |a| <= 2 (5e-14
-    absolute) and 2^-41 absolute up to 3 — far inside the 1e-7 rollout tolerance and the
-    north star's 1e-5."""
+    """The look-ahead's lean cores (math fn 10-12: 7-term atan and sin_wide, division without
+    its residual step) on the same domains vs NumPy: atan2 / atan within 2^16 ulp (~7e-12
+    relative; the fit's own error is 3.0e-12), sin_wide within 2^18 ulp for |a| <= 2 (1e-11
+    absolute) and 2^-33 absolute up to 3 (the fit: 3.9e-11) — far inside the 1e-6 rollout
+    tolerance and the north star's 1e-5."""
     rng = np.random.RandomState(2)
     n = 1 << 20
     y = np.concatenate([rng.uniform(-3, 3, n), rng.standard_cauchy(n), [0.0, -0.0, 1.0, -1.0, 1e-300, 5.0]])
@@ -684,10 +684,10 @@ def test_lean_cores_accuracy_on_domain(nat):
     a = rng.uniform(-2, 2, n)
     u_s = _ulp(_math(nat, 12, a), np.sin(a))
     print(f"lean cores: atan2 {u_a2:.1f} ulp, atan {u_a:.1f} ulp, sin_wide |a|<=2 {u_s:.1f} ulp")
-    assert u_a2 <= 1024 and u_a <= 1024 and u_s <= 512
+    assert u_a2 <= 2 ** 16 and u_a <= 2 ** 16 and u_s <= 2 ** 18
     a = np.concatenate([rng.uniform(-3, 3, n), [3.0, -3.0, 0.0, -0.0, 1e-300]])
     err = np.abs(_math(nat, 12, a) - np.sin(a))
-    assert np.all(err <= 16 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -41), err.max()
+    assert np.all(err <= 16 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -33), err.max()
     # the paired cores of the LPM-1 look-ahead lane (math fn 13/14: front and rear division
     # through one reciprocal, partner = element n-1-i) on their domain (Dom::ok_paired:
     # atan2 divisors max(|y|, x) in [2^-500, 2^499], atan divisor products <= 2^499)
@@ -699,7 +699,7 @@ def test_lean_cores_accuracy_on_domain(nat):
     zz = z[np.abs(z) <= 2.0 ** 240]
     u_p = _ulp(_math(nat, 14, zz), np.arctan(zz))
     print(f"paired cores: atan2 {u_p2:.1f} ulp, atan {u_p:.1f} ulp")
-    assert u_p2 <= 1024 and u_p <= 1024
+    assert u_p2 <= 2 ** 16 and u_p <= 2 ** 16
 
 
 def test_lookahead_out_of_domain_fallback(nat):
@@ -832,7 +832,7 @@ def test_config5_concurrent_tracks_vs_oracle(nat):
     llampc_plan_async / llampc_plan_wait (two streams in flight), over W + 2 ticks, against
     the oracle (rt.py:347-366 look-back + H x _integrate_batch + nmpc.py cost per track):
     selection, top-K and the look-ahead argmin exact; every cost in the record (selected
-    model's, top-K models', global best) within 1e-7; top-K Df/Dr bitwise."""
+    model's, top-K models', global best) within 1e-6; top-K Df/Dr bitwise."""
     from llampc import _native
     from llampc.mpc import ConstantSpeed, ModelBank, generate_bank
     from llampc.tracks import ETHZ, ETHZMobil
@@ -996,7 +996,7 @@ def test_work_queue_layout_equals_static_and_oracle(nat, monkeypatch):
     the CUs) and C = 40 (G = 64, ragged candidates), with 4-wave and (forced) 8-wave blocks:
     every record field equal to the static
     block-per-models layout (LLAMPC_NO_WQ=1) tick after tick — polled and ticket completion —
-    costs equal to the oracle's at 1e-7, and the counter's base carried correctly across
+    costs equal to the oracle's at 1e-6, and the counter's base carried correctly across
     ticks, a reset and a second bank."""
     from llampc import _native
     from llampc.mpc import ModelBank, generate_bank
@@ -1221,7 +1221,7 @@ def test_setupnlp_cem_equals_oracle(nat):
     """The device cross-entropy search (csrc/nlp.hip) against its NumPy restatement
     (oracle.nlp_cem) over three successive solves (warm start, the held uprev in the first
     round): the same sequence (the samples are bitwise the oracle's; the elite ranking follows
-    costs equal to 1e-7) and fval at 1e-7."""
+    costs equal to 1e-6) and fval at 1e-6."""
     d = golden("dyn_slice.npz")
     s, u = d["states"], d["inputs"]
     nlp, p = _nlp()

@@ -3,7 +3,8 @@ mode, ETHZ, H = 40, C = 64, K = 10, W = 10) on an N-model bank and prints, per t
 phase boundaries of every block of the launch relative to the first block's entry (µs,
 s_memrealtime at 100 MHz): look-ahead blocks — staged (tables + candidates), walk done
 (thread 0), walk barrier, selection known, rolled out, published; the look-back ticket winner
-— scored, lb_final done, slots polled, record written — plus the host's own split of the
+— scored, lb_final done, slots polled, record stores issued (thread 0), record
+written (after the system fence) — plus the host's own split of the
 tick (tick_begin, the wait, the result).  Paced at 1 ms and back to back.
 usage: python tools/diag/ctl_phases.py [N] [ticks]"""
 import ctypes
@@ -69,7 +70,7 @@ for mode in ("paced", "back-to-back"):
         la = [k for k in range(64) if live[k] and Z[k, 5] >= base and Z[k, 1] >= base]
         parts = [f"{mode} tick: host begin {hb:.1f} wait {hw:.1f} result {hr:.1f} us |"]
         parts.append(f"lb(block {win}): scored {us(Z[win, 6]):.1f} lb_final {us(Z[win, 7]):.1f} "
-                     f"polled {us(Z[win, 8]):.1f} record {us(Z[win, 9]):.1f} |")
+                     f"polled {us(Z[win, 8]):.1f} stored {us(Z[win, 11]):.1f} record {us(Z[win, 9]):.1f} |")
         for slot in (1, 10, 2, 3, 4, 5):
             v = np.array([us(Z[k, slot]) for k in la])
             parts.append(f"{NAMES[slot]} {v.min():.1f}/{v.max():.1f}")

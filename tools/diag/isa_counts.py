@@ -2,11 +2,12 @@
 loop for each lane split (LPM 1/2/4) of plan_kernel<RK4, staged, LPM, xref shared> and of the
 controller tick's ctl_kernel<LPM> (unstaged, candidates in LDS), from hipcc -S listings of the
 translation units that hold them.  bench.py's ISSUE_INSTR_PER_STEP holds the plan numbers.
-usage: python tools/diag/isa_counts.py"""
+usage: python tools/diag/isa_counts.py [extra hipcc flags, e.g. -DLLAMPC_LEAN_TERMS=7]"""
 import collections
 import os
 import re
 import subprocess
+import sys
 import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -16,7 +17,7 @@ tmp = tempfile.mkdtemp()
 def listing(tu):
     out = f"{tmp}/{tu}.s"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm",
-                    "-disable-machine-licm", f"-I{REPO}/include", f"-I{REPO}/lla-mpc_amd/csrc", "--cuda-device-only",
+                    "-disable-machine-licm", *sys.argv[1:], f"-I{REPO}/include", f"-I{REPO}/lla-mpc_amd/csrc", "--cuda-device-only",
                     "-S", f"{REPO}/lla-mpc_amd/csrc/{tu}.hip", "-o", out], cwd=tmp, check=True, stderr=subprocess.DEVNULL)
     return open(out).read().split("\n")
 

@@ -1,7 +1,7 @@
 """Diagnostic (stamps build): phases of the setupNLP.solve CEM round launches — per block
 (µs from the first block's entry, s_memrealtime): drawn, rate-clipped, rolled out; the
-completing block: keyed, sorted, elite drawn, elite clipped, done — for the last round of a
-few solves.  usage: python tools/diag/nlp_phases.py"""
+completing block: 4 lists loaded, 5 merged, 6 elite loaded, 8 mean/std done — for the last
+round of a few solves.  usage: python tools/diag/nlp_phases.py"""
 import ctypes
 import os
 import sys
@@ -38,7 +38,7 @@ for t in range(10, 16):
     us = lambda v: (v - base) / 100.0  # noqa: E731
     win = int(np.argmax(Z[:nb, 8]))
     row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (1, 2, 9, 3)]
-    comp = [f"{k}: {us(Z[win, k]):.1f}" for k in (4, 5, 6, 7, 8)]
+    comp = [f"{k}: {us(Z[win, k]):.1f}" for k in (4, 5, 6, 8)]
     print(f"solve {t}: blocks drawn/clipped/rolled (min/max) {' '.join(row)} | completion (block {win}) {' '.join(comp)}",
           flush=True)
 nlp.close()
