@@ -1514,7 +1514,8 @@ struct llampc_nlp {
   size_t blk_bytes = 0, in_bytes = 0;
   double* d_cost = nullptr;              // the sample blocks' sorted lists (keys, then indices), then
                                          // the round's rate-clipped sequences [samples][H][2]
-  unsigned* d_ticket = nullptr;
+  unsigned* d_ticket = nullptr;          // [4]: the round ticket, pad, then the round tag (u64)
+  bool per_round = false;                // one launch per round (LLAMPC_NLP_ROUND_LAUNCHES=1: A/B)
   NlpResult* h_res = nullptr;            // pinned, coherent, mapped: the last round writes it
   NlpResult* d_res = nullptr;            //   (device alias), then the solve's number into h_tag
   uint64_t* h_tag = nullptr;
@@ -1567,8 +1568,12 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
   };
   int rc;
   if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, 2 * (size_t)k.samples * (1 + (size_t)H))) ||
-      (rc = dev_alloc(&p->d_ticket, 1)))
+      (rc = dev_alloc(&p->d_ticket, 4)))
     return cleanup(rc);
+  {
+    const char* e = std::getenv("LLAMPC_NLP_ROUND_LAUNCHES");
+    p->per_round = !nlp_persistent(k.samples) || (e && e[0] == '1');
+  }
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(NLP staging) failed"));
   std::memset(p->h_blk, 0, p->blk_bytes);
@@ -1581,7 +1586,7 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
       hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_tag), p->h_tag, 0) != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "hipHostGetDevicePointer(NLP result) failed"));
   if (hipMemcpy(p->d_blk, p->h_blk, p->blk_bytes, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(p->d_ticket, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      hipMemset(p->d_ticket, 0, 4 * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "NLP solver upload failed"));
   *out = p;
   return LLAMPC_OK;
@@ -1632,6 +1637,7 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.host_tag = p->d_tag;
   a.host_seq = p->calls + 1;
   a.ticket = p->d_ticket;
+  a.round_tag = reinterpret_cast<uint64_t*>(p->d_ticket + 2);
   a.seed = k.seed;
   a.call = p->calls;
   a.up0 = uprev[0];
@@ -1649,9 +1655,16 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.samples = k.samples;
   a.elite = k.elite;
   a.has_hold = has_hold;
-  for (int it = 0; it < k.iters; ++it) {
-    a.it = it;
-    a.last = it == k.iters - 1;         // its completion writes xmpc (nmpc.py:58-60)
+  a.iters = k.iters;                    // the last round's completion writes xmpc (nmpc.py:58-60)
+  if (p->per_round) {
+    a.rounds = 1;
+    for (int it = 0; it < k.iters; ++it) {
+      a.it = it;
+      HIP_TRY(launch_nlp(a, s));
+    }
+  } else {                              // every round in one launch (nlp.hpp nlp_persistent)
+    a.it = 0;
+    a.rounds = k.iters;
     HIP_TRY(launch_nlp(a, s));
   }
   // the last round's completion writes the result into pinned memory and then the tag
@@ -1667,7 +1680,7 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
     }
   }
   p->calls++;
-  b->launches += k.iters;
+  b->launches += p->per_round ? k.iters : 1;
   const NlpResult* r = const_cast<const NlpResult*>(p->h_res);
   for (int i = 0; i < H; ++i)
     for (int j = 0; j < 2; ++j) umpc[2 * i + j] = r->best_u[i][j];

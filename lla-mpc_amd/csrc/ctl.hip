@@ -51,6 +51,24 @@ __host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n) {
   return L;
 }
 constexpr size_t kCtlPollBytes = 4096;   // ctl_complete's area (layout there)
+// ctl_complete's record words (one 8-byte word per lane of wave 0)
+static_assert(offsetof(llampc_plan_out, window_full) == 4 && offsetof(llampc_plan_out, K) == 8 &&
+                  offsetof(llampc_plan_out, sel_owned) == 12 && offsetof(llampc_plan_out, lb_best) == 16 &&
+                  offsetof(llampc_plan_out, lb_best_val) == 24 && offsetof(llampc_plan_out, sel_model) == 32 &&
+                  offsetof(llampc_plan_out, sel_cand) == 40 && offsetof(llampc_plan_out, n_nonfinite) == 44 &&
+                  offsetof(llampc_plan_out, sel_cost) == 48 && offsetof(llampc_plan_out, la_best_model) == 56 &&
+                  offsetof(llampc_plan_out, la_best_cand) == 64 && offsetof(llampc_plan_out, status) == 68 &&
+                  offsetof(llampc_plan_out, la_best_cost) == 72 && offsetof(llampc_plan_out, topk) == 80,
+              "llampc_plan_out header words");
+static_assert(offsetof(llampc_ctl_out, tick) == sizeof(llampc_plan_out) &&
+                  offsetof(llampc_ctl_out, projidx) == offsetof(llampc_ctl_out, tick) + 8 &&
+                  offsetof(llampc_ctl_out, warm) == offsetof(llampc_ctl_out, tick) + 12 &&
+                  offsetof(llampc_ctl_out, mu_used) == offsetof(llampc_ctl_out, tick) + 16 &&
+                  offsetof(llampc_ctl_out, scale_used) == offsetof(llampc_ctl_out, tick) + 24 &&
+                  offsetof(llampc_ctl_out, mu_pred) == offsetof(llampc_ctl_out, tick) + 32 &&
+                  offsetof(llampc_ctl_out, dr_mean) == offsetof(llampc_ctl_out, tick) + 40 &&
+                  offsetof(llampc_ctl_out, df_mean) == offsetof(llampc_ctl_out, tick) + 48,
+              "llampc_ctl_out words");
 
 #ifdef LLAMPC_STAMPS
 // Diagnostic build only: s_memrealtime (100 MHz) per block and phase of the last launch
@@ -150,6 +168,8 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     pmu[2] = mu_pred;
     pmu[3] = c.use_mu ? mu_old : c.mu_fixed;                       // the mu this tick's walk used
   }
+  // the current model (this block writes it after the poll): loaded now, off the tail
+  const int64_t cur_model = (tid < 64 && warm) ? st->current_model : 0;
   // every slot's result (tagged words of the look-ahead blocks)
   int late = 0;
   if (tid < c.nslots) {
@@ -198,62 +218,66 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     if (tid < 2) st->u_prev[tid] = v;
   }
   if (tid < 6) st->x_prev[tid] = c.x_t[tid];
-  if (tid == 0) {
-    const int64_t sel = warm ? st->current_model : c.fin.goff + (int64_t)cs.ids[c.K];
-    // look-ahead best over the rolled-out slots (flattened (model, candidate) order)
-    double lav = nan;
-    int64_t lai = kNoIndex;
-    int nf = 0;
-    for (int q = 0; q < c.nslots; ++q) {
-      nf += pnf[q];
-      if (warm || pcand[q] < 0 || cs.ids[q] == kNoLocal) continue;
-      const int64_t key = (c.fin.goff + (int64_t)cs.ids[q]) * C + pcand[q];
-      if (less_bf<0>(pcost[q], key, lav, lai)) {
-        lav = pcost[q];
-        lai = key;
-      }
-    }
+  if (tid < 64) {
+    // wave 0: the look-ahead best over the rolled-out slots (flattened (model, candidate)
+    // order, NaN last, ties to the lower key) as a wave pick, then the record's scalars as
+    // one 8-byte word per lane — one store instruction into the pinned host record (thread 0
+    // storing the ~25 fields one by one over PCIe took ~4 us, profiles/r04/ctl_record_split.txt)
+    const int q = tid;
+    const bool slot = q < c.nslots;
+    const bool valid = slot && !warm && pcand[q] >= 0 && cs.ids[q] != kNoLocal;
+    double lav = valid ? pcost[q] : nan;
+    int64_t lai = valid ? (c.fin.goff + (int64_t)cs.ids[q]) * C + pcand[q] : kNoIndex;
+    wave_pick_nl64(lav, lai);
+    const int nf = wave_sum(slot ? pnf[q] : 0);
     int anyl = 0;
     for (int w = 0; w < kWaves; ++w) anyl |= late_w[w];
-    po->window_count = c.fin.window_count;
-    po->window_full = c.fin.full;
-    po->K = c.K;
-    po->sel_owned = 1;
-    if (warm) {
-      po->lb_best = -1;
-      po->lb_best_val = nan;
-    }
-    po->sel_model = sel;
-    po->sel_cand = pcand[ss];
-    po->sel_cost = pcost[ss];
-    po->n_nonfinite = nf;
-    po->la_best_model = lai == kNoIndex ? -1 : lai / C;
-    po->la_best_cand = lai == kNoIndex ? -1 : (int32_t)(lai % C);
-    po->la_best_cost = lai == kNoIndex ? nan : lav;
-    po->status = anyl ? kPollTimeoutStatus : 0;
+    const int64_t sel = warm ? cur_model : c.fin.goff + (int64_t)cs.ids[c.K];
     const double dr = pmu[0], df = pmu[1], mu_pred = pmu[2];
-    st->mu_pred = mu_pred;
     int pj = pmisc[0];
     if (pj > c.lap_projidx) pj = 0;                                // rt.py:287-296
-    st->projidx = pj;
-    st->has_seq = 1;
-    if (!warm) st->current_model = sel;
-    o->tick = (int64_t)c.tick;
-    o->projidx = pj;
-    o->warm = c.warm;
-    o->mu_used = pmu[3];
-    o->scale_used = c.use_mu ? c.v_factor : c.scale_fixed;
-    o->mu_pred = mu_pred;
-    o->dr_mean = dr;
-    o->df_mean = df;
-    __hip_atomic_store(&c.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t lm;
+    int32_t lc;
+    split_key(lai == kNoIndex ? 0 : lai, C, lm, lc);
+    auto pack = [](int32_t lo, int32_t hi) { return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32); };
+    auto bits = [](double v) { return (uint64_t)__double_as_longlong(v); };
+    // llampc_plan_out words 0..9 (lb_best / lb_best_val, words 2 and 3, are lb_final's unless
+    // warm), then llampc_ctl_out's words after the plan record (static_asserts below)
+    uint64_t w = 0;
+    bool store = true;
+    uint64_t* dst = reinterpret_cast<uint64_t*>(po) + q;
+    switch (q) {
+      case 0: w = pack(c.fin.window_count, c.fin.full); break;
+      case 1: w = pack(c.K, 1); break;                                 // sel_owned
+      case 2: w = (uint64_t)(int64_t)-1; store = warm; break;
+      case 3: w = bits(nan); store = warm; break;
+      case 4: w = (uint64_t)sel; break;
+      case 5: w = pack(pcand[ss], nf); break;
+      case 6: w = bits(pcost[ss]); break;
+      case 7: w = (uint64_t)(lai == kNoIndex ? (int64_t)-1 : lm); break;
+      case 8: w = pack(lai == kNoIndex ? -1 : lc, anyl ? kPollTimeoutStatus : 0); break;
+      case 9: w = bits(lai == kNoIndex ? nan : lav); break;
+      case 10: w = (uint64_t)(int64_t)c.tick; break;
+      case 11: w = pack(pj, c.warm); break;
+      case 12: w = bits(pmu[3]); break;                                // mu_used
+      case 13: w = bits(c.use_mu ? c.v_factor : c.scale_fixed); break;
+      case 14: w = bits(mu_pred); break;
+      case 15: w = bits(dr); break;
+      case 16: w = bits(df); break;
+      default: store = false;
+    }
+    if (q >= 10) dst = reinterpret_cast<uint64_t*>(&o->tick) + (q - 10);
+    if (store) *dst = w;
+    if (q == 0) {
+      st->mu_pred = mu_pred;
+      st->projidx = pj;
+      st->has_seq = 1;
+      if (!warm) st->current_model = sel;
+      __hip_atomic_store(&c.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   CTL_STAMP(blockIdx.x, 11);
-#ifdef LLAMPC_CTL_WAITCNT   // diagnostic A/B: this wave's stores complete, no L2 write-back
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-#else
-  __threadfence_system();
-#endif
+  __threadfence_system();              // ~0.4 us (a plain vmcnt wait: ~0.3, ctl_record_split.txt)
   __syncthreads();
   CTL_STAMP(blockIdx.x, 9);
   if (tid == 0) __hip_atomic_store(c.host_tag, c.host_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

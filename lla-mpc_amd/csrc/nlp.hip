@@ -60,18 +60,20 @@ __device__ __forceinline__ void nlp_z2(uint32_t pair, uint64_t call, uint64_t se
   z1 = (double)hi * 0x1p-16 - 2.0;
 }
 
-// sample s of iteration `it` before the rate chain (the bounds applied), given its variate z
-__device__ __forceinline__ double nlp_raw_z(const NlpLaunch& a, const NlpState* st, int s, int k, int j, double z) {
+// sample s of round `it` before the rate chain (the bounds applied), given its variate z;
+// ms = the round's mean [H][2] then std [H][2] (LDS)
+__device__ __forceinline__ double nlp_raw_z(const NlpLaunch& a, const double* ms, int it, int s, int k, int j,
+                                            double z) {
 #pragma clang fp contract(off)
-  const double m = st->mean[k][j];
+  const double m = ms[2 * k + j];
   double u;
   if (s == 0) {
     u = m;
-  } else if (s == 1 && a.it == 0 && a.has_hold) {
+  } else if (s == 1 && it == 0 && a.has_hold) {
     u = j ? a.up1 : a.up0;
   } else {
     const double zu = z * 1.7320508075688772;       // unit variance (sqrt(3), as np.sqrt(3.0))
-    const double d = zu * st->std_[k][j];
+    const double d = zu * ms[2 * (a.H + k) + j];
     u = m + d;
   }
   return np_clip(u, j ? a.umin1 : a.umin0, j ? a.umax1 : a.umax0);
@@ -126,7 +128,7 @@ __device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, unsigned char
   double* sx = ub + 2 * (size_t)H;      // after the sequence: xref [H+1][2], x0 [6]
   double* x0 = sx + 2 * (size_t)(H + 1);
   for (int e = tid; e < 2 * H; e += kBlock) {
-    const double v = better ? ub[e] : (&st->best_u[0][0])[e];
+    const double v = better ? ub[e] : ld_wt(&st->best_u[0][0] + e);   // an earlier round's completion
     ub[e] = v;
     (&res->best_u[0][0])[e] = v;
   }
@@ -174,7 +176,10 @@ __device__ __forceinline__ void nlp_traj_quad(const NlpLaunch& a, const double* 
   }
 }
 
-__device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem) {
+// Round `it`'s completion (the block that added the last ticket): the elite, the next mean /
+// std, the best so far.  The state is handed to the next round's blocks (other CUs, other
+// XCDs) by sc1 stores and loads, as the sample blocks' lists (st_wt / ld_wt).
+__device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem, int it) {
 #pragma clang fp contract(off)
   const int tid = threadIdx.x, H = a.H, E = a.elite;
   const int len = nlp_list_len(E), nl = (int)gridDim.x;
@@ -227,38 +232,59 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   __syncthreads();
   NLP_STAMP(6);
   const double c0 = nlp_unkey(kA[0]);
-  const bool better = c0 < st->best_j;              // the best sequence so far (NaN never)
+  const double bj0 = ld_wt(&st->best_j);
+  const int bit0 = ld_wt(&st->best_it);
+  const bool better = c0 < bj0;                     // the best sequence so far (NaN never)
   __syncthreads();                                  // every thread has read best_j
   if (tid < 2 * H) {
     // mean / std over the elite in np.mean(axis=0) / np.std(axis=0)'s order: an axis-0
     // reduction adds the rows in sequence (checked against NumPy), std = sqrt(mean((x - m)^2))
     const int k = tid >> 1, j = tid & 1;
     auto at = [&](int e) { return eu[(2 * (size_t)e * H) + 2 * k + j]; };
+    // in row order, eight LDS reads issued ahead of their adds (one read per dependent add
+    // waited an LDS round trip per row)
     double acc = 0.0;
-    for (int e = 0; e < E; ++e) acc += at(e);
+    int e = 0;
+    for (; e + 8 <= E; e += 8) {
+      double v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = at(e + i);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc += v[i];
+    }
+    for (; e < E; ++e) acc += at(e);
     const double m = acc / E;
     double s = 0.0;
-    for (int e = 0; e < E; ++e) {
+    for (e = 0; e + 8 <= E; e += 8) {
+      double v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = at(e + i);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const double d = v[i] - m;
+        s += d * d;
+      }
+    }
+    for (; e < E; ++e) {
       const double d = at(e) - m;
       s += d * d;
     }
-    st->mean[k][j] = m;
-    st->std_[k][j] = sqrt(s / E) + a.std_floor;
-    if (better) st->best_u[k][j] = eu[2 * k + j];
+    st_wt(&st->mean[k][j], m);
+    st_wt(&st->std_[k][j], sqrt(s / E) + a.std_floor);
+    if (better) st_wt(&st->best_u[k][j], eu[2 * k + j]);
   }
   // the result (the last round): best objective and round, before this round's update
-  const double bj = better ? c0 : st->best_j;
-  const int bit = better ? a.it : st->best_it;
-  __syncthreads();                                  // read before thread 0 updates them
+  const double bj = better ? c0 : bj0;
+  const int bit = better ? it : bit0;
   if (tid == 0) {
     if (better) {
-      st->best_j = c0;
-      st->best_it = a.it;
+      st_wt(&st->best_j, c0);
+      st_wt(&st->best_it, it);
     }
     __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   NLP_STAMP(8);
-  if (a.last) nlp_trajectory(a, smem, eu, better, bj, bit);
+  if (it == a.iters - 1) nlp_trajectory(a, smem, eu, better, bj, bit);
 }
 
 }  // namespace
@@ -268,6 +294,10 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
 // [k][c][kStageW]), so the rollout loop reads them instead of forming them per step; when
 // 64 x H x 64 B fit beside the rest (H <= kNlpStageH).
 constexpr int kNlpStageH = 28;
+
+// s_memrealtime ticks (100 MHz) a block waits for a round's state before it gives up (never
+// expected: the solve then reports that its completion tag did not arrive)
+constexpr uint64_t kNlpRoundWait = 5000000;
 
 template <bool ST>
 __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
@@ -280,114 +310,143 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   double* Ul = sx + 2 * (H + 1);                                            // [64][H][2]
   double* x0 = Ul + 2 * (size_t)kPerBlock * H;                              // [6]
   uint64_t* ks = reinterpret_cast<uint64_t*>(x0 + 6);                       // [64] the samples' keys
-  double* su = reinterpret_cast<double*>(ks + 64);                          // ST: [H][64][kStageW]
+  double* ms = reinterpret_cast<double*>(ks + 64);                          // the round's mean, std [2][H][2]
+  double* su = ms + 4 * (size_t)H;                                          // ST: [H][64][kStageW]
+  int* rflag = flag + 1;                // the round wait's verdict (flag is ticket_last's)
   const NlpState* st = a.st;
-  NLP_STAMP(0);
-  for (int e = tid; e <= H; e += kBlock) {
-    sx[2 * e] = a.xref[e];
-    sx[2 * e + 1] = a.xref[(H + 1) + e];
-  }
-  if (tid < 6) x0[tid] = a.x0[tid];
-  // value i = (s H + k) 2 + j of the round; pair i / 2 = (s H + k): the (j = 0, 1) values of
-  // one (sample, step) share a Philox call
-  for (int e = tid; e < kPerBlock * H; e += kBlock) {
-    const int r = e / H, k = e - r * H, s = blk * kPerBlock + r;
-    double z0, z1;
-    nlp_z2((uint32_t)(s * H + k), a.call, a.seed, (uint32_t)(a.it + 1), z0, z1);
-    Ul[2 * e] = nlp_raw_z(a, st, s, k, 0, z0);
-    Ul[2 * e + 1] = nlp_raw_z(a, st, s, k, 1, z1);
-  }
-  __syncthreads();
-  NLP_STAMP(1);
-  if (tid < 2 * kPerBlock) {
-    const int r = tid >> 1, j = tid & 1;
-    nlp_rate_chain(Ul + 2 * (size_t)r * H + j, H, j ? a.up1 : a.up0, j ? a.rlo1 : a.rlo0, j ? a.rhi1 : a.rhi0);
-  }
-  __syncthreads();
-  NLP_STAMP(2);
-  for (int e = tid; e < kPerBlock * H * 2; e += kBlock) st_wt(&a.cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
-  const fm::FmK K = fm::FmK::load();
-  if constexpr (ST) {
-    const CostK& q0 = a.la.cost;
-    // consecutive threads take consecutive candidates of one step: their 64-B records are
-    // adjacent in LDS (one step per thread-row was a 4 KB stride: every write one bank)
-    for (int f = tid; f < kPerBlock * H; f += kBlock) {
-      const int k = f >> 6, c = f & (kPerBlock - 1), e = c * H + k;
-      const double ua = Ul[2 * e], dl = Ul[2 * e + 1];
-      double sd, cd;
-      if (fm::sincos_fast_ok(dl)) fm::sincos_fast(dl, &sd, &cd, K);
-      else LL_SINCOS(dl, &sd, &cd);
-      const double p0 = k ? Ul[2 * e - 2] : a.up0, p1 = k ? Ul[2 * e - 1] : a.up1;
-      const double d0 = ua - p0, d1 = dl - p1;
-      double* o = su + kStageW * (k * kPerBlock + c);
-      o[0] = ua;
-      o[1] = dl;
-      o[2] = sd;
-      o[3] = cd;
-      o[6] = act_term(q0, d0, d1);
-      o[7] = (!q0.enforce || input_feasible(q0, ua, dl, d0, d1)) ? 1.0 : 0.0;
+  for (int r = 0; r < a.rounds; ++r) {
+    const int it = a.it + r;
+    if (r > 0) {                        // the previous round's completion published round it
+      if (tid == 0) {
+        const uint64_t want = tag_word((uint32_t)a.host_seq, (uint32_t)it);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int ok = 1;
+        while (ld_wt(a.round_tag) != want)
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kNlpRoundWait) {
+            ok = 0;
+            break;
+          }
+        *rflag = ok;
+      }
+      __syncthreads();
+      if (!*rflag) return;
+    }
+    NLP_STAMP(0);
+    // the round's inputs (the completing block of the previous round used this LDS)
+    for (int e = tid; e <= H; e += kBlock) {
+      sx[2 * e] = a.xref[e];
+      sx[2 * e + 1] = a.xref[(H + 1) + e];
+    }
+    if (tid < 6) x0[tid] = a.x0[tid];
+    for (int e = tid; e < 4 * H; e += kBlock)
+      ms[e] = ld_wt(e < 2 * H ? &st->mean[0][0] + e : &st->std_[0][0] + (e - 2 * H));
+    __syncthreads();
+    // value i = (s H + k) 2 + j of the round; pair i / 2 = (s H + k): the (j = 0, 1) values of
+    // one (sample, step) share a Philox call
+    for (int e = tid; e < kPerBlock * H; e += kBlock) {
+      const int rr = e / H, k = e - rr * H, s = blk * kPerBlock + rr;
+      double z0, z1;
+      nlp_z2((uint32_t)(s * H + k), a.call, a.seed, (uint32_t)(it + 1), z0, z1);
+      Ul[2 * e] = nlp_raw_z(a, ms, it, s, k, 0, z0);
+      Ul[2 * e + 1] = nlp_raw_z(a, ms, it, s, k, 1, z1);
     }
     __syncthreads();
-    NLP_STAMP(9);
-  }
-  // rollouts: a quad per sample (the plan kernel's NLP-Euler fast stage + the general re-run)
-  const int sub = tid % LPM, c = tid / LPM;
-  const Tire t = load_tire(a.la.params, 1, 0);
-  CostK q = a.la.cost;
-  VehK veh = a.la.veh;
-  double Ts = a.la.Ts;
-  for (int m = 0; m < 4; ++m) {
-    pin_vgpr(q.Q[m]);
-    pin_vgpr(q.R[m]);
-    pin_vgpr(q.P[m]);
-  }
-  for (int m = 0; m < 2; ++m) {
-    pin_vgpr(q.umin[m]);
-    pin_vgpr(q.umax[m]);
-    pin_vgpr(q.dmax[m]);
-  }
-  pin_vgpr(Ts);
-  const StageK sk = make_stage<LPM>(veh, t, sub, 1.0);
-  const FusedK fq = make_fused(veh, sk, Ts, false);
-  bool bad = false;
-  double J;
-  if constexpr (ST)
-    J = rollout<1, true, LPM, 0, true>(a.la, c, 0, x0, sx, su, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, bad);
-  else
-    J = rollout<1, false, LPM, 0, true, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, bad);
-  int bi = bad;
-  bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX1, 0xF, 0xF, false);
-  bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX2, 0xF, 0xF, false);
-  if (__builtin_expect(__any(bi), 0)) {
-    bool unused = false;
-    if (bi) {
-      if constexpr (ST)
-        J = rollout<1, true, LPM, 0, false>(a.la, c, 0, x0, sx, su, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, unused);
-      else
-        J = rollout<1, false, LPM, 0, false, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K, fq,
-                                                          unused);
+    NLP_STAMP(1);
+    if (tid < 2 * kPerBlock) {
+      const int rr = tid >> 1, j = tid & 1;
+      nlp_rate_chain(Ul + 2 * (size_t)rr * H + j, H, j ? a.up1 : a.up0, j ? a.rlo1 : a.rlo0, j ? a.rhi1 : a.rhi0);
+    }
+    __syncthreads();
+    NLP_STAMP(2);
+    for (int e = tid; e < kPerBlock * H * 2; e += kBlock) st_wt(&a.cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
+    const fm::FmK K = fm::FmK::load();
+    if constexpr (ST) {
+      const CostK& q0 = a.la.cost;
+      // consecutive threads take consecutive candidates of one step: their 64-B records are
+      // adjacent in LDS (one step per thread-row was a 4 KB stride: every write one bank)
+      for (int f = tid; f < kPerBlock * H; f += kBlock) {
+        const int k = f >> 6, c = f & (kPerBlock - 1), e = c * H + k;
+        const double ua = Ul[2 * e], dl = Ul[2 * e + 1];
+        double sd, cd;
+        if (fm::sincos_fast_ok(dl)) fm::sincos_fast(dl, &sd, &cd, K);
+        else LL_SINCOS(dl, &sd, &cd);
+        const double p0 = k ? Ul[2 * e - 2] : a.up0, p1 = k ? Ul[2 * e - 1] : a.up1;
+        const double d0 = ua - p0, d1 = dl - p1;
+        double* o = su + kStageW * (k * kPerBlock + c);
+        o[0] = ua;
+        o[1] = dl;
+        o[2] = sd;
+        o[3] = cd;
+        o[6] = act_term(q0, d0, d1);
+        o[7] = (!q0.enforce || input_feasible(q0, ua, dl, d0, d1)) ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      NLP_STAMP(9);
+    }
+    // rollouts: a quad per sample (the plan kernel's NLP-Euler fast stage + the general re-run)
+    const int sub = tid % LPM, c = tid / LPM;
+    const Tire t = load_tire(a.la.params, 1, 0);
+    CostK q = a.la.cost;
+    VehK veh = a.la.veh;
+    double Ts = a.la.Ts;
+    for (int m = 0; m < 4; ++m) {
+      pin_vgpr(q.Q[m]);
+      pin_vgpr(q.R[m]);
+      pin_vgpr(q.P[m]);
+    }
+    for (int m = 0; m < 2; ++m) {
+      pin_vgpr(q.umin[m]);
+      pin_vgpr(q.umax[m]);
+      pin_vgpr(q.dmax[m]);
+    }
+    pin_vgpr(Ts);
+    const StageK sk = make_stage<LPM>(veh, t, sub, 1.0);
+    const FusedK fq = make_fused(veh, sk, Ts, false);
+    bool bad = false;
+    double J;
+    if constexpr (ST)
+      J = rollout<1, true, LPM, 0, true>(a.la, c, 0, x0, sx, su, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, bad);
+    else
+      J = rollout<1, false, LPM, 0, true, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, bad);
+    int bi = bad;
+    bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX1, 0xF, 0xF, false);
+    bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX2, 0xF, 0xF, false);
+    if (__builtin_expect(__any(bi), 0)) {
+      bool unused = false;
+      if (bi) {
+        if constexpr (ST)
+          J = rollout<1, true, LPM, 0, false>(a.la, c, 0, x0, sx, su, veh, t, sk, q, Ts, a.up0, a.up1, K, fq, unused);
+        else
+          J = rollout<1, false, LPM, 0, false, false, true>(a.la, c, 0, x0, sx, Ul, veh, t, sk, q, Ts, a.up0, a.up1, K,
+                                                            fq, unused);
+      }
+    }
+    NLP_STAMP(3);
+    if (sub == 0) ks[c] = nlp_key(J);
+    __syncthreads();
+    if (tid < 64) {                     // wave 0: the block's 64 keys sorted (bitonic, in registers)
+      uint64_t k = ks[tid];
+      uint32_t x = (uint32_t)(blk * kPerBlock + tid);
+      for (int w = 2; w <= 64; w <<= 1)
+        for (int j = w >> 1; j > 0; j >>= 1) nlp_cx(k, x, j, ((tid & j) == 0) == ((tid & w) == 0));
+      const int len = nlp_list_len(a.elite);
+      if (tid < len) {
+        st_wt(&a.top_key[(size_t)blk * len + tid], k);
+        st_wt(&a.top_idx[(size_t)blk * len + tid], x);
+      }
+    }
+    if (!ticket_last(a.ticket, gridDim.x, flag)) continue;
+    nlp_complete(a, smem, it);
+    if (r + 1 < a.rounds) {             // publish the next round: its state stored sc1, drained
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) st_wt(a.round_tag, tag_word((uint32_t)a.host_seq, (uint32_t)(it + 1)));
     }
   }
-  NLP_STAMP(3);
-  if (sub == 0) ks[c] = nlp_key(J);
-  __syncthreads();
-  if (tid < 64) {                       // wave 0: the block's 64 keys sorted (bitonic, in registers)
-    uint64_t k = ks[tid];
-    uint32_t x = (uint32_t)(blk * kPerBlock + tid);
-    for (int w = 2; w <= 64; w <<= 1)
-      for (int j = w >> 1; j > 0; j >>= 1) nlp_cx(k, x, j, ((tid & j) == 0) == ((tid & w) == 0));
-    const int len = nlp_list_len(a.elite);
-    if (tid < len) {
-      st_wt(&a.top_key[(size_t)blk * len + tid], k);
-      st_wt(&a.top_idx[(size_t)blk * len + tid], x);
-    }
-  }
-  if (!ticket_last(a.ticket, gridDim.x, flag)) return;
-  nlp_complete(a, smem);
 }
 
 size_t nlp_lds_bytes(int H, int samples, int elite) {
-  const size_t blocks = kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 48 + 8 * 64 +
+  const size_t blocks = kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 48 + 8 * 64 + 32 * (size_t)H +
                         (H <= kNlpStageH ? 8 * kStageW * 64 * (size_t)H : 0);
   const size_t nll = (size_t)(samples / 64) * nlp_list_len(elite);
   const size_t last = kScratchBytes + 24 * nll + 16 * (size_t)elite * H + 16 * (size_t)(H + 1) + 48;

@@ -20,8 +20,11 @@ struct NlpState {
   int32_t pad;
 };
 
-// One CEM iteration's launch.  Scalars only (no arrays): the kernel never takes the address of
-// its argument (which would copy it to scratch).
+// A launch of CEM rounds [it, it + rounds): every round of the solve in one launch when the
+// sample blocks are few enough to be co-resident (nlp_persistent), the blocks then waiting for
+// each round's completion on a tagged word (round_tag); else one launch per round.  Scalars
+// only (no arrays): the kernel never takes the address of its argument (which would copy it to
+// scratch).
 // The solve's result as the last round's completion writes it into pinned host memory (then
 // a system-scope fence and the host tag): no D2H copy, no stream synchronisation.
 struct NlpResult {
@@ -43,13 +46,20 @@ struct NlpLaunch {
   uint64_t* host_tag;            //   then this solve's number (host alias spun on by the caller)
   uint64_t host_seq;
   unsigned* ticket;
+  uint64_t* round_tag;           // (host_seq, r): round r's state is published (r >= 1)
   uint64_t seed, call;           // Philox key; counter word 1 = the solve call number
   double up0, up1;               // uprev (du_0, nmpc.py:65-66)
   double umin0, umin1, umax0, umax1;
   double rlo0, rlo1, rhi0, rhi1; // per-step rate bounds (x Ts); lo > hi: none
   double std_floor;
-  int32_t it, H, samples, elite, has_hold, last;
+  int32_t it, rounds, iters;     // the launch's first round, its round count, the solve's
+  int32_t H, samples, elite, has_hold;
 };
+
+// every round in one launch: the sample blocks (one per CU: the LDS request) must all be
+// resident at once, since each waits for the others' rounds
+constexpr int kNlpPersistentBlocks = 64;
+__host__ __device__ __forceinline__ bool nlp_persistent(int samples) { return samples / 64 <= kNlpPersistentBlocks; }
 
 // the length of each sample block's sorted list: next power of two >= elite (elite <= 64)
 __host__ __device__ __forceinline__ int nlp_list_len(int elite) {

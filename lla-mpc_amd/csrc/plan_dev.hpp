@@ -225,6 +225,26 @@ __device__ __forceinline__ T ld_wt(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// key = m C + c (0 <= c < C, 0 <= key < 2^63) split without the 64-bit integer division's
+// ~150-instruction software sequence (the controller record's look-ahead best): the fp64
+// quotient of the key is within 2^11 of m (the key's rounding), that of the exact remainder
+// within 1, and one fix-up step makes the split exact.
+__device__ __forceinline__ void split_key(int64_t key, int32_t C, int64_t& m, int32_t& c) {
+  const double dc = (double)C;
+  int64_t q = (int64_t)((double)key / dc);
+  q += (int64_t)((double)(key - q * C) / dc);
+  int64_t r = key - q * C;
+  if (r < 0) {
+    q -= 1;
+    r += C;
+  } else if (r >= C) {
+    q += 1;
+    r -= C;
+  }
+  m = q;
+  c = (int32_t)r;
+}
+
 // Tagged 64-bit words of the polled completion: launch tag in the high half, payload low.
 __device__ __forceinline__ uint64_t tag_word(uint32_t seq, uint32_t payload) {
   return ((uint64_t)seq << 32) | payload;

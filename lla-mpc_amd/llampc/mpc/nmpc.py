@@ -12,7 +12,8 @@ start first: the previous solution shifted one step; the held uprev is a candida
 first round) with a per-(step, input) spread, clipped to the bounds and rate-clipped in order,
 every one rolled out with the NLP's own Euler transcription and scored with its objective
 (infeasible: +inf); the ``elite`` best set the next mean and spread (the cross-entropy
-method).  All rounds run back to back on the GPU with one copy back.  Every returned
+method).  All rounds run in ONE launch on the GPU (the sample blocks wait for each round's
+mean and spread), the result comes back through pinned host memory.  Every returned
 ``umpc`` satisfies the NLP's bounds and rate constraints; ``fval`` is the objective of
 ``umpc`` and ``xmpc`` its Euler trajectory — the same triple IPOPT's feasible point would give.
 
