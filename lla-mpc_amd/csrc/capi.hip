@@ -1169,6 +1169,7 @@ static_assert(sizeof(llampc_ctl_out) == sizeof(llampc_plan_out) + 56 + 16 * LLAM
 struct llampc_ctl {
   llampc_bank* b = nullptr;
   llampc_ctl_cfg cfg{};
+  bool no_stage = false;                 // LLAMPC_CTL_NO_STAGE=1: unstaged look-ahead inputs (A/B)
   CtlState* d_st = nullptr;
   double* d_pts = nullptr;               // points [2][np] | prefix [np - 1]
   int32_t np = 0;
@@ -1229,6 +1230,7 @@ int llampc_ctl_create(llampc_bank* b, const llampc_ctl_cfg* cfg, const double* p
   auto* c = new llampc_ctl();
   c->b = b;
   c->cfg = k;
+  if (const char* e = std::getenv("LLAMPC_CTL_NO_STAGE")) c->no_stage = e[0] == '1';
   c->np = np;
   auto cleanup = [&](int code) {
     llampc_ctl_destroy(c);
@@ -1365,7 +1367,7 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   }
   const double sqrt3 = std::sqrt(3.0);
   for (int j = 0; j < 2; ++j) {
-    L.nscale[j] = sqrt3 * k.sigma[j];    // sqrt(3) sigma_j, one rounding (ctl.hpp ctl_cand_raw)
+    L.nscale[j] = sqrt3 * k.sigma[j];    // sqrt(3) sigma_j, one rounding (ctl.hpp ctl_cand_one)
     L.rate[j] = k.cost.rate_max[j] < 0 ? -1.0 : k.cost.rate_max[j] * k.Ts;
     L.umin[j] = k.cost.umin[j];
     L.umax[j] = k.cost.umax[j];
@@ -1394,7 +1396,13 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   L.K = k.K;
   L.nb_lb = L.fin.nb_lb;
   L.nb_la = (L.nslots + L.mpb - 1) / L.mpb;
-  size_t lds = ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &L.poll_off);
+  // the look-ahead blocks stage every (candidate, step)'s input terms when they fit in LDS
+  // (CtlLaunch.s4; LLAMPC_CTL_NO_STAGE=1 at create: never, for A/B runs)
+  size_t poll_s4 = 0;
+  const size_t lds_s4 = ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &poll_s4, true);
+  L.s4 = (!c->no_stage && lds_s4 <= 160 * 1024) ? 1 : 0;
+  size_t lds = L.s4 ? lds_s4 : ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &L.poll_off);
+  if (L.s4) L.poll_off = poll_s4;
   lds = std::max<size_t>(lds, 82 * 1024); // one block per CU, as the plan launch (sc1 hand-offs)
   {
     TimedLaunch tl(b, 0, b->stream);

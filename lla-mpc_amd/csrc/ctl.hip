@@ -29,13 +29,15 @@ namespace llampc {
 // LDS layout of the controller launch (byte offsets; 16-B aligned regions).  Look-ahead
 // blocks: xref [H+1][2] | U [C][H][2] | knots [n + pad] | the two speed profiles bracketing mu
 // interleaved per segment [n-1][2][4] (a, b, c, d of lo, then of hi: one segment's values are
-// four 16-B reads) | misc.  The completing block: lb_final's region from kScratchBytes (then
-// the candidates [C][H][2]), its own area at poll_off (CtlPollLds).
+// four 16-B reads) | with s4: sin / cos delta [C][H][2], then per candidate the summed
+// input-rate cost and its feasibility flag [C][2] (staged during the walk) | misc.
+// The completing block: lb_final's region from kScratchBytes (then the candidates [C][H][2]),
+// its own area at poll_off (CtlPollLds).
 struct CtlLds {
-  size_t sx, ul, kn, spd, misc, end;
+  size_t sx, ul, kn, spd, s4, misc, end;
 };
 __host__ __device__ __forceinline__ size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
-__host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n) {
+__host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n, bool s4 = false) {
   CtlLds L;
   size_t o = kScratchBytes;
   L.sx = o;
@@ -46,6 +48,8 @@ __host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n) {
   o = align16(o + 8 * (size_t)(n + kKnotPad));
   L.spd = o;
   o = align16(o + 64 * (size_t)(n - 1));
+  L.s4 = o;
+  if (s4) o = align16(o + 16 * (size_t)C * H + 16 * (size_t)C);
   L.misc = o;
   L.end = o + 1024;
   return L;
@@ -125,10 +129,10 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   const double up0 = st->u_prev[0], up1 = st->u_prev[1];
   {
     const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
-    for (int e = tid; e < 2 * C * H; e += kBlock) {
-      const int cc = e / (2 * H), r = e - cc * 2 * H, j = r & 1;
-      cu[e] = ctl_cand_raw(cc, r >> 1, j, H, prev_seq, j ? up1 : up0, j ? c.nscale[1] : c.nscale[0],
-                           j ? c.umin[1] : c.umin[0], j ? c.umax[1] : c.umax[0], c.tick, c.seed, 0);
+    const double up[2] = {up0, up1};
+    for (int p = tid; p < C * H; p += kBlock) {
+      const int cc = p / H, k = p - cc * H;
+      ctl_cand_pair(cc, k, H, prev_seq, up, c.nscale, c.umin, c.umax, c.tick, c.seed, 0, cu + 2 * (size_t)p);
     }
   }
   __syncthreads();
@@ -429,12 +433,60 @@ __device__ __forceinline__ int cs_walk_wave(const RacelineK& rl, const MuBracket
 // A look-ahead block: the tick's reference and candidates (redundantly per block: they only
 // read the state and the tables), then its slots' rollouts.
 // ------------------------------------------------------------------------------------
+// Waves 1-3 of a look-ahead block while wave 0 walks: an arrival count in LDS joins them (a
+// block barrier would wait for the walk).  Every wave's LDS stores are complete before it
+// arrives; the count only grows within a launch (targets 3, 6).
+__device__ __forceinline__ void ctl_group_sync(int* arrived, int target) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(arrived, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(arrived, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+  }
+}
+
+// The staged look-ahead inputs (s4; waves 1-3, t in [0, 192), after the rate clip): sin / cos
+// delta of every (candidate, step) — make_input_fast's values — and per candidate the
+// rollout's input-rate cost sum (act_term over k in order from 0, nmpc.py:65-68, 111) and
+// its feasibility (1 / 0, nmpc.py:102-105; NaN: a steering outside sincos_fast's domain, so
+// the rollout re-runs in the general evaluation).  The same arithmetic as the unstaged step.
+__device__ __forceinline__ void ctl_stage(const CtlLaunch& c, const double* Ul, double* s4, int t, double up0,
+                                          double up1) {
+  const int H = c.la.H, C = c.la.C;
+  constexpr int kThreads = kBlock - 64;
+  const int ns = C < kThreads / 2 ? C : kThreads / 2;                 // threads summing per candidate
+  if (t < ns) {
+    const CostK& q = c.la.cost;
+    for (int cc = t; cc < C; cc += ns) {
+      const double* u = Ul + 2 * (size_t)cc * H;
+      double act = 0.0, p0 = up0, p1 = up1;
+      bool feas = true, bad = false;
+      for (int k = 0; k < H; ++k) {
+        const double ua = u[2 * k], ud = u[2 * k + 1];
+        const double d0 = ua - p0, d1 = ud - p1;
+        if (q.enforce) feas = (int)feas & (int)input_feasible(q, ua, ud, d0, d1);
+        act = act + act_term(q, d0, d1);
+        bad = (int)bad | (int)!fm::sincos_fast_ok(ud);
+        p0 = ua;
+        p1 = ud;
+      }
+      *reinterpret_cast<double2*>(s4 + 2 * (size_t)C * H + 2 * cc) =
+          double2{act, bad ? __builtin_nan("") : (feas ? 1.0 : 0.0)};
+    }
+  } else {
+    const fm::FmK K = fm::FmK::load();
+    for (int f = t - ns; f < C * H; f += kThreads - ns) {
+      double sd, cd;
+      fm::sincos_fast(Ul[2 * f + 1], &sd, &cd, K);
+      *reinterpret_cast<double2*>(s4 + 2 * (size_t)f) = double2{sd, cd};
+    }
+  }
+}
+
 template <int LPM>
 __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsigned char* smem, const Scratch& sc) {
   const int tid = threadIdx.x;
   const int H = c.la.H, C = c.la.C;
   const RacelineK rl = c.la.rl;
-  const CtlLds L = ctl_lds(H, C, rl.n);
+  const CtlLds L = ctl_lds(H, C, rl.n, c.s4 != 0);
   double* sx = reinterpret_cast<double*>(smem + L.sx);
   double* Ul = reinterpret_cast<double*>(smem + L.ul);
   double* kn = reinterpret_cast<double*>(smem + L.kn);
@@ -443,8 +495,11 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   uint32_t* slot_id = reinterpret_cast<uint32_t*>(smem + L.misc + 128);   // [mpb] (<= 64)
   int32_t* sel_late = reinterpret_cast<int32_t*>(smem + L.misc + 384);    // [mpb]
   double* x0 = reinterpret_cast<double*>(smem + L.misc + 640);            // [6] x_t (no kernarg address taken)
+  int* arrived = reinterpret_cast<int*>(smem + L.misc + 688);              // waves 1-3 (ctl_group_sync)
+  double* s4 = reinterpret_cast<double*>(smem + L.s4);                      // s4: the staged inputs
   CTL_STAMP(blockIdx.x, 0);
   if (tid < 6) x0[tid] = c.x_t[0 + tid];
+  if (tid == 0) *arrived = 0;
   const CtlState* st = c.st;
   const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
   const int p0 = st->projidx;
@@ -468,10 +523,19 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
                        sx, &vr);
     CTL_STAMP(blockIdx.x, 10);
   } else {
-    for (int e = tid - 64; e < 2 * C * H; e += kBlock - 64) {
-      const int cc = e / (2 * H), r = e - cc * 2 * H, j = r & 1;
-      Ul[e] = ctl_cand_raw(cc, r >> 1, j, H, prev_seq, j ? up1 : up0, j ? c.nscale[1] : c.nscale[0],
-                           j ? c.umin[1] : c.umin[0], j ? c.umax[1] : c.umax[0], c.tick, c.seed, 0);
+    const double up[2] = {up0, up1};
+    for (int p = tid - 64; p < C * H; p += kBlock - 64) {
+      const int cc = p / H, k = p - cc * H;
+      ctl_cand_pair(cc, k, H, prev_seq, up, c.nscale, c.umin, c.umax, c.tick, c.seed, 0, Ul + 2 * (size_t)p);
+    }
+    if (c.s4) {                         // block-uniform: still during the walk, clip and stage
+      ctl_group_sync(arrived, kWaves - 1);
+      for (int t = tid - 64; t < 2 * C; t += kBlock - 64) {
+        const int j = t & 1;
+        ctl_rate_chain(Ul + 2 * (size_t)(t >> 1) * H + j, H, j ? up1 : up0, j ? c.rate[1] : c.rate[0]);
+      }
+      ctl_group_sync(arrived, 2 * (kWaves - 1));
+      ctl_stage(c, Ul, s4, tid - 64, up0, up1);
     }
   }
   __syncthreads();
@@ -480,12 +544,13 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   //     the selection (tagged words of the look-back ticket winner), or the nominal model
   //     while the window fills
   const int mpb = c.mpb;
-  if (tid >= 64) {
+  if (!c.s4 && tid >= 64) {
     for (int t = tid - 64; t < 2 * C; t += kBlock - 64) {
       const int j = t & 1;
       ctl_rate_chain(Ul + 2 * (size_t)(t >> 1) * H + j, H, j ? up1 : up0, j ? c.rate[1] : c.rate[0]);
     }
-  } else if (tid < mpb) {
+  }
+  if (tid < mpb) {                      // wave 0 (mpb <= 64): this block's slots
     const int slot = blk * mpb + tid;
     uint32_t id = kNoLocal;
     int late = 0;
@@ -586,12 +651,20 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
       if (cc >= C) break;
       bool bad = false;
       double J;
-      if (kSplit && diagQP)
+      if (c.s4) {                       // block-uniform: the staged input terms
+        if (kSplit && diagQP)
+          J = rollout<0, false, LPM, 0, true, kSplit, true, false, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts,
+                                                                        up0, up1, K, fq, bad, nullptr, s4);
+        else
+          J = rollout<0, false, LPM, 0, true, false, true, false, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts,
+                                                                       up0, up1, K, fq, bad, nullptr, s4);
+      } else if (kSplit && diagQP) {
         J = rollout<0, false, LPM, 0, true, kSplit, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts, up0, up1, K,
                                                          fq, bad);
-      else
+      } else {
         J = rollout<0, false, LPM, 0, true, false, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts, up0, up1, K,
                                                         fq, bad);
+      }
       if (LPM == 2) {
         const int bi = bad;
         bad = __builtin_amdgcn_mov_dpp(bi, kPair0, 0xF, 0xF, false) | __builtin_amdgcn_mov_dpp(bi, kPair1, 0xF, 0xF, false);
@@ -732,8 +805,8 @@ hipError_t launch_constant_speed(const CsLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off) {
-  const CtlLds L = ctl_lds(H, C, n);
+size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4) {
+  const CtlLds L = ctl_lds(H, C, n, s4);
   const size_t M = (size_t)nb_lb * K, Lb = nb_lb;    // lb_final's region (launch_plan's formula)
   const size_t lbf = kScratchBytes + 8 * (3 * M + Lb) + sizeof(Ent) * Lb * kWaves + 4 * (3 * M + Lb + LLAMPC_KMAX + 2) + 8 + 16;
   const size_t rank = kScratchBytes + (size_t)kWaves * kRankBytes + kBlockMergeBytes;

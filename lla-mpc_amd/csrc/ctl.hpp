@@ -56,14 +56,19 @@ __host__ __device__ __forceinline__ Philox4 philox4x32_10(Philox4 c, uint32_t k0
   return c;
 }
 
-// Unit-variance noise of element i = (c H + k) 2 + j of tick `tick`: the four words of one
-// Philox call summed (a 4-term Irwin-Hall variate, exact in fp64: < 2^34), centred; the
-// caller scales by sqrt(3) sigma_j (variance 1/3 per uniform sum of four -> 1).
-__host__ __device__ __forceinline__ double ctl_z(uint32_t i, uint64_t tick, uint64_t seed, uint32_t stream) {
-  const Philox4 w = philox4x32_10(Philox4{i, (uint32_t)tick, (uint32_t)(tick >> 32), stream}, (uint32_t)seed,
+// The candidates' noise: one Philox4x32-10 call per (candidate, step) PAIR p = c H + k,
+// counter (p, tick lo, tick hi, stream), key (seed lo, seed hi); input j takes the 16-bit
+// halves (j = 0 low, 1 high) of the four words: z_j = (h0 + h1 + h2 + h3 + 2) 2^-16 - 2, the
+// centred 4-term Irwin-Hall variate (variance 1/3 - 1/(3 2^32); exact in fp64), as the NLP
+// search's (nlp.hip nlp_z2) — half the Philox calls of one call per value.
+__host__ __device__ __forceinline__ void ctl_z2(uint32_t p, uint64_t tick, uint64_t seed, uint32_t stream, double& z0,
+                                                double& z1) {
+  const Philox4 w = philox4x32_10(Philox4{p, (uint32_t)tick, (uint32_t)(tick >> 32), stream}, (uint32_t)seed,
                                   (uint32_t)(seed >> 32));
-  const uint64_t s = (uint64_t)w.x + w.y + w.z + w.w;
-  return (double)s * 0x1p-32 - 2.0;
+  const uint32_t lo = (w.x & 0xFFFFu) + (w.y & 0xFFFFu) + (w.z & 0xFFFFu) + (w.w & 0xFFFFu) + 2u;
+  const uint32_t hi = (w.x >> 16) + (w.y >> 16) + (w.z >> 16) + (w.w >> 16) + 2u;
+  z0 = (double)lo * 0x1p-16 - 2.0;
+  z1 = (double)hi * 0x1p-16 - 2.0;
 }
 
 // np.clip for float64 (numpy clip.cpp: _NPY_MIN(_NPY_MAX(x, lo), hi), NaN passes through)
@@ -75,20 +80,28 @@ __host__ __device__ __forceinline__ double np_clip(double x, double lo, double h
 // Candidate element before the rate clip: base + noise (c >= 1), then the input bounds.
 // base = the previous chosen sequence shifted one step (or uprev held); noise = z nscale_j
 // with nscale_j = sqrt(3) sigma_j: two roundings, reproducible in NumPy.
-__host__ __device__ __forceinline__ double ctl_cand_raw(int c, int k, int j, int H, const double* prev_seq /*[H][2] or null*/,
-                                                        double up_j, double ns_j, double lo_j, double hi_j, uint64_t tick,
-                                                        uint64_t seed, uint32_t stream) {
+__host__ __device__ __forceinline__ double ctl_cand_one(int c, int k, int j, int H, const double* prev_seq, double up_j,
+                                                        double ns_j, double lo_j, double hi_j, double z) {
 #ifdef __clang__
 #pragma clang fp contract(off)
 #endif
   const double base = prev_seq ? prev_seq[2 * (k + 1 < H ? k + 1 : H - 1) + j] : up_j;
   double u = base;
   if (c > 0) {
-    const double z = ctl_z((uint32_t)((c * H + k) * 2 + j), tick, seed, stream);
     const double noise = z * ns_j;
     u = base + noise;
   }
   return np_clip(u, lo_j, hi_j);
+}
+// Both inputs of candidate c at step k (one Philox call) into u[0], u[1].
+__host__ __device__ __forceinline__ void ctl_cand_pair(int c, int k, int H, const double* prev_seq /*[H][2] or null*/,
+                                                       const double* up, const double* ns, const double* lo,
+                                                       const double* hi, uint64_t tick, uint64_t seed, uint32_t stream,
+                                                       double* u) {
+  double z0 = 0.0, z1 = 0.0;
+  if (c > 0) ctl_z2((uint32_t)(c * H + k), tick, seed, stream, z0, z1);
+  u[0] = ctl_cand_one(c, k, 0, H, prev_seq, up[0], ns[0], lo[0], hi[0], z0);
+  u[1] = ctl_cand_one(c, k, 1, H, prev_seq, up[1], ns[1], lo[1], hi[1], z1);
 }
 
 // The rate clip of one (candidate, input) chain in order over k (controller.py
@@ -100,7 +113,23 @@ __host__ __device__ __forceinline__ void ctl_rate_chain(double* u, int H, double
 #endif
   if (!(r >= 0.0)) return;
   double prev = up;
-  for (int k = 0; k < H; ++k) {
+  int k = 0;
+  for (; k + 8 <= H; k += 8) {          // eight loads ahead of the dependent clips
+    double v[8];
+#ifdef __clang__
+#pragma unroll
+#endif
+    for (int i = 0; i < 8; ++i) v[i] = u[2 * (k + i)];
+#ifdef __clang__
+#pragma unroll
+#endif
+    for (int i = 0; i < 8; ++i) {
+      const double lo = prev - r, hi = prev + r;
+      prev = np_clip(v[i], lo, hi);
+      u[2 * (k + i)] = prev;
+    }
+  }
+  for (; k < H; ++k) {
     const double lo = prev - r, hi = prev + r;
     prev = np_clip(u[2 * k], lo, hi);
     u[2 * k] = prev;
@@ -217,6 +246,7 @@ struct CtlLaunch {
   int32_t np, lap_projidx;
   int32_t do_lb, warm, use_mu, full, nslots, mpb, G, cpl, S, K;
   int32_t nb_lb, nb_la;
+  int32_t s4;                 // stage each (candidate, step)'s sincos / cost terms (CtlLds.s4)
 };
 
 // llampc_ctl_reference's launch: ConstantSpeed alone (planner.py:12-67) on the device.
@@ -230,8 +260,9 @@ struct CsLaunch {
 };
 hipError_t launch_constant_speed(const CsLaunch& a, hipStream_t s);
 
-// LDS bytes of the controller launch and the completing block's area offset (ctl.hip).
-size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off);
+// LDS bytes of the controller launch and the completing block's area offset (ctl.hip); s4:
+// with the staged input terms (CtlLaunch.s4).
+size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4 = false);
 hipError_t launch_ctl(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s);
 
 }  // namespace llampc

@@ -47,9 +47,10 @@ namespace {
 
 // The search's noise: one Philox4x32-10 call per PAIR of values, the counter (i / 2, call lo,
 // call hi, round + 1): value i takes the 16-bit halves (low for even i, high for odd) of the
-// four words, z = (h0 + h1 + h2 + h3 + 2) 2^-16 - 2 — the 4-term Irwin-Hall variate of the
-// controller's candidates (ctl_z) on 16-bit cells (centred: mean 0, variance 1/3 - 1/(3 2^32)),
-// at half the Philox calls (the sample blocks' draw was 4.3 of a 26 us round).
+// four words, z = (h0 + h1 + h2 + h3 + 2) 2^-16 - 2 — the 4-term Irwin-Hall variate on
+// 16-bit cells of the controller's candidates too (ctl.hpp ctl_z2; centred: mean 0, variance
+// 1/3 - 1/(3 2^32)), at half the Philox calls of one per value (the sample blocks' draw was
+// 4.3 of a 26 us round).
 __device__ __forceinline__ void nlp_z2(uint32_t pair, uint64_t call, uint64_t seed, uint32_t stream, double& z0,
                                        double& z1) {
   const Philox4 w = philox4x32_10(Philox4{pair, (uint32_t)call, (uint32_t)(call >> 32), stream}, (uint32_t)seed,

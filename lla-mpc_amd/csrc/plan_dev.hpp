@@ -590,14 +590,21 @@ __device__ __forceinline__ bool input_feasible(const CostK& q, double ua, double
 // position component (dyn.hpp k_fused) and accumulates its tracking term; the quad's J is
 // (J_X + J_Y) + act by two DPP broadcasts at the end.
 // ULDS (the controller tick, ctl.hip): the raw candidates U [C][H][2] are at `su` (LDS)
-// instead of a.U; only with STAGE = false.
-template <int INTEG, bool STAGE, int LPM, int XM, bool FAST, bool SPLIT = false, bool ULDS = false, bool TRAJ = false>
+// instead of a.U; only with STAGE = false.  S4 (with ULDS, FAST): the steering's sin / cos
+// per (candidate, step) at s4 [C][H][2], then per candidate the input-rate cost sum and the
+// feasibility (1 / 0; NaN: a steering outside sincos_fast's domain, so the rollout re-runs in
+// the general evaluation) at s4 + 2CH [C][2] (LDS; ctl.hip ctl_stage) — the step reads two
+// values instead of forming them, with the same values and roundings.
+template <int INTEG, bool STAGE, int LPM, int XM, bool FAST, bool SPLIT = false, bool ULDS = false, bool TRAJ = false,
+          bool S4 = false>
 __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64_t n,
                                           const double* x0, const double* sx, const double* su, const VehK& veh,
                                           const Tire& t, const StageK& sk, const CostK& q,
                                           double Ts, double up0, double up1, const fm::FmK& K,
-                                          const FusedK& fq, bool& bad, double* traj = nullptr) {
+                                          const FusedK& fq, bool& bad, double* traj = nullptr,
+                                          const double* s4 = nullptr) {
   static_assert(!TRAJ || (INTEG != 0 && !SPLIT), "trajectory output: unscaled, unsplit state");
+  static_assert(!S4 || (ULDS && FAST && !STAGE), "staged sincos / cost terms: the controller's fast rollout");
   static_assert(!SPLIT || (FAST && INTEG == 0 && LPM == 4), "position split: fused RK4 quads only");
   static_assert(!ULDS || !STAGE, "candidates in LDS: unstaged rollout");
   const int H = a.H, C = a.C;
@@ -646,11 +653,20 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     } else {
       ua = Ub[2 * ((int64_t)c * H + k)];
       ud = Ub[2 * ((int64_t)c * H + k) + 1];
-      if (FAST) u = make_input_fast(ua, ud, K, bad);
-      else u = make_input(ua, ud);
+      if (S4) {
+        const double2 sc2 = *reinterpret_cast<const double2*>(s4 + 2 * ((int64_t)c * H + k));
+        u.a = ua;
+        u.d = ud;
+        u.sd = sc2.x;
+        u.cd = sc2.y;
+      } else if (FAST) {
+        u = make_input_fast(ua, ud, K, bad);
+      } else {
+        u = make_input(ua, ud);
+      }
     }
     const double d0 = ua - p0, d1 = ud - p1;          // nmpc.py:65-68
-    if (!STAGE && q.enforce) feas = (int)feas & (int)input_feasible(q, ua, ud, d0, d1);
+    if (!STAGE && !S4 && q.enforce) feas = (int)feas & (int)input_feasible(q, ua, ud, d0, d1);
     if (FAST && INTEG == 0 && STAGE) step_fused<LPM, SPLIT>(sk, fq, x, fi, ud, K, dm);
     else if (FAST && INTEG == 0) step_fused<LPM, SPLIT>(sk, fq, x, u, K, dm);
     else if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, dm);
@@ -670,13 +686,18 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
       const double e0 = x[0] - xr0, e1 = x[1] - xr1;
       track = track + (e0 * (q.Q[0] * e0 + q.Q[1] * e1) + e1 * (q.Q[2] * e0 + q.Q[3] * e1));
     }
-    if (!STAGE) act = act + act_term(q, d0, d1);
+    if (!STAGE && !S4) act = act + act_term(q, d0, d1);
     p0 = ua;
     p1 = ud;
     if (TRAJ && traj != nullptr) {      // the state after step k (every lane of a quad holds it)
 #pragma unroll
       for (int m = 0; m < 6; ++m) traj[6 * (k + 1) + m] = x[m];
     }
+  }
+  if (S4) {                             // the candidate's summed input-rate cost, feasibility
+    const double2 af = *reinterpret_cast<const double2*>(s4 + 2 * (int64_t)C * H + 2 * c);
+    act = af.x;
+    feas_s = af.y;
   }
   double J;
   if (SPLIT) {                                                    // nmpc.py:48, :111
@@ -695,8 +716,9 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     constexpr bool kPaired = INTEG == 0 && LPM == 1 && kLeanLA && kPairLA;   // dyn.hpp chain_pair
     const bool dok = kPaired ? dm.ok_paired() : dm.ok();
     bad = (int)bad | (int)!sk.sok | (int)!dok | (int)!(fabs(J) <= __DBL_MAX__);
+    if (S4) bad = (int)bad | (int)(feas_s != feas_s);   // a steering outside sincos_fast's domain
   }
-  if (STAGE) feas = feas_s != 0.0;
+  if (STAGE || S4) feas = feas_s != 0.0;
   if (!feas) J = __builtin_inf();
   return J;
 }

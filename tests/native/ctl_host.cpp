@@ -44,9 +44,7 @@ int main(int argc, char** argv) {
     const double* prev = has_prev ? in.data() + 15 : nullptr;
     std::vector<double> U((size_t)C * H * 2);
     for (int c = 0; c < C; ++c)
-      for (int k = 0; k < H; ++k)
-        for (int j = 0; j < 2; ++j)
-          U[((size_t)c * H + k) * 2 + j] = ctl_cand_raw(c, k, j, H, prev, up[j], ns[j], lo[j], hi[j], tick, seed, 0);
+      for (int k = 0; k < H; ++k) ctl_cand_pair(c, k, H, prev, up, ns, lo, hi, tick, seed, 0, &U[((size_t)c * H + k) * 2]);
     for (int c = 0; c < C; ++c)
       for (int j = 0; j < 2; ++j) ctl_rate_chain(U.data() + (size_t)c * H * 2 + j, H, up[j], r[j]);
     for (double v : U) std::printf("%.17g\n", v);
