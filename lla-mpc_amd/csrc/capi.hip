@@ -1182,6 +1182,8 @@ struct llampc_ctl {
   uint64_t* d_slot_tag = nullptr;        // [kCtlSlotsMax][4]
   unsigned* d_tickets = nullptr;         // [1]
   double* d_dbg = nullptr;               // xref [2][H+1] | U [C][H][2] (debug_inputs)
+  double* d_znoise = nullptr;            // [2][C H][2] the candidates' variates (CtlLaunch.znoise)
+  uint64_t* d_ztag = nullptr;            // [2]
   uint32_t seq = 0;
   int64_t t = 0;
   bool pending = false;
@@ -1196,7 +1198,7 @@ int llampc_ctl_destroy(llampc_ctl* c) {
   {
     DeviceGuard g(c->b ? c->b->device : 0);
     if (c->b && c->b->stream) (void)hipStreamSynchronize(c->b->stream);
-    void* d[] = {c->d_st, c->d_pts, c->d_sel_tag, c->d_slot_tag, c->d_tickets, c->d_dbg};
+    void* d[] = {c->d_st, c->d_pts, c->d_sel_tag, c->d_slot_tag, c->d_tickets, c->d_dbg, c->d_znoise, c->d_ztag};
     for (void* p : d)
       if (p) (void)hipFree(p);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1239,7 +1241,8 @@ int llampc_ctl_create(llampc_bank* b, const llampc_ctl_cfg* cfg, const double* p
   int rc;
   if ((rc = dev_alloc(&c->d_st, 1)) || (rc = dev_alloc(&c->d_pts, 3 * (size_t)np - 1)) ||
       (rc = dev_alloc(&c->d_sel_tag, kCtlSlotsMax)) || (rc = dev_alloc(&c->d_slot_tag, 4 * (size_t)kCtlSlotsMax)) ||
-      (rc = dev_alloc(&c->d_tickets, 1)))
+      (rc = dev_alloc(&c->d_tickets, 1)) || (rc = dev_alloc(&c->d_znoise, 4 * (size_t)k.C * k.H)) ||
+      (rc = dev_alloc(&c->d_ztag, 2)))
     return cleanup(rc);
   if (k.debug_inputs && (rc = dev_alloc(&c->d_dbg, 2 * (size_t)(k.H + 1) + 2 * (size_t)k.C * k.H))) return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&c->h_out), sizeof(llampc_ctl_out),
@@ -1258,7 +1261,8 @@ int llampc_ctl_create(llampc_bank* b, const llampc_ctl_cfg* cfg, const double* p
       hipMemcpy(c->d_pts + 2 * (size_t)np, prefix, ((size_t)np - 1) * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(c->d_sel_tag, 0, kCtlSlotsMax * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->d_slot_tag, 0, 4 * kCtlSlotsMax * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->d_tickets, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      hipMemset(c->d_tickets, 0, sizeof(unsigned)) != hipSuccess ||
+      hipMemset(c->d_ztag, 0, 2 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "controller upload failed"));
   *out = c;
   return LLAMPC_OK;
@@ -1357,6 +1361,8 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   L.slot_tag = c->d_slot_tag;
   L.tickets = c->d_tickets;
   L.dbg = c->d_dbg;
+  L.znoise = c->d_znoise;
+  L.ztag = c->d_ztag;
   L.pts = c->d_pts;
   L.prefix = c->d_pts + 2 * (size_t)c->np;
   L.tick = (uint64_t)t;

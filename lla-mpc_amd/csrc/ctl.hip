@@ -99,6 +99,56 @@ __device__ __forceinline__ bool ctl_late(uint64_t t0, uint32_t poll) {
   return __builtin_amdgcn_s_memrealtime() - t0 > ((uint64_t)poll << 16);
 }
 
+// The raw candidates [C][H][2] (before the rate clip) by threads t0 + i stride, i >= 0: from
+// this tick's variates when the previous tick's completion drew them (znoise, tagged), four
+// pairs' loads in flight per thread; else one Philox call per pair here.
+__device__ __forceinline__ void ctl_draw(const CtlLaunch& c, const double* prev_seq, double up0, double up1,
+                                         double* U, int t0, int stride) {
+  const int H = c.la.H, C = c.la.C, CH = C * H;
+  const double up[2] = {up0, up1};
+  const int half = (int)(c.tick & 1);
+  if (c.znoise && c.ztag[half] == c.tick + 1) {                     // launch-uniform
+    const double* zb = c.znoise + 2 * (size_t)CH * half;
+    for (int p0 = t0; p0 < CH; p0 += 4 * stride) {
+      double z[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = p0 + i * stride < CH ? p0 + i * stride : CH - 1;
+        z[i][0] = zb[2 * p];
+        z[i][1] = zb[2 * p + 1];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = p0 + i * stride;
+        if (p < CH) {
+          const int cc = p / H, k = p - cc * H;
+          ctl_cand_pair_z(cc, k, H, prev_seq, up, c.nscale, c.umin, c.umax, z[i][0], z[i][1], U + 2 * (size_t)p);
+        }
+      }
+    }
+  } else {
+    for (int p = t0; p < CH; p += stride) {
+      const int cc = p / H, k = p - cc * H;
+      ctl_cand_pair(cc, k, H, prev_seq, up, c.nscale, c.umin, c.umax, c.tick, c.seed, 0, U + 2 * (size_t)p);
+    }
+  }
+}
+
+// The next tick's variates into znoise half (t + 1) & 1 (the completing block's waves 1-3
+// while wave 0 polls), then its tag; the next launch reads them after this one has ended.
+__device__ __forceinline__ void ctl_draw_next(const CtlLaunch& c, int t0, int stride) {
+  if (!c.znoise) return;
+  const int H = c.la.H, CH = c.la.C * H;
+  const uint64_t nt = c.tick + 1;
+  double* zb = c.znoise + 2 * (size_t)CH * (int)(nt & 1);
+  for (int p = t0; p < CH; p += stride) {
+    double z0 = 0.0, z1 = 0.0;
+    if (p >= H) ctl_z2((uint32_t)p, nt, c.seed, 0, z0, z1);           // candidate 0 has none
+    *reinterpret_cast<double2*>(zb + 2 * (size_t)p) = double2{z0, z1};
+  }
+  if (t0 == 0) c.ztag[nt & 1] = nt + 1;
+}
+
 // ------------------------------------------------------------------------------------
 // The completing block (after lb_final<true>, or alone on ticks without a look-back).
 // ------------------------------------------------------------------------------------
@@ -129,11 +179,7 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   const double up0 = st->u_prev[0], up1 = st->u_prev[1];
   {
     const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
-    const double up[2] = {up0, up1};
-    for (int p = tid; p < C * H; p += kBlock) {
-      const int cc = p / H, k = p - cc * H;
-      ctl_cand_pair(cc, k, H, prev_seq, up, c.nscale, c.umin, c.umax, c.tick, c.seed, 0, cu + 2 * (size_t)p);
-    }
+    ctl_draw(c, prev_seq, up0, up1, cu, tid, kBlock);
   }
   __syncthreads();
   for (int t = tid; t < 2 * C; t += kBlock) {
@@ -174,6 +220,8 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   }
   // the current model (this block writes it after the poll): loaded now, off the tail
   const int64_t cur_model = (tid < 64 && warm) ? st->current_model : 0;
+  // waves 1-3 draw the next tick's variates while wave 0 polls (off every critical path)
+  if (tid >= 64) ctl_draw_next(c, tid - 64, kBlock - 64);
   // every slot's result (tagged words of the look-ahead blocks)
   int late = 0;
   if (tid < c.nslots) {
@@ -523,11 +571,7 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
                        sx, &vr);
     CTL_STAMP(blockIdx.x, 10);
   } else {
-    const double up[2] = {up0, up1};
-    for (int p = tid - 64; p < C * H; p += kBlock - 64) {
-      const int cc = p / H, k = p - cc * H;
-      ctl_cand_pair(cc, k, H, prev_seq, up, c.nscale, c.umin, c.umax, c.tick, c.seed, 0, Ul + 2 * (size_t)p);
-    }
+    ctl_draw(c, prev_seq, up0, up1, Ul, tid - 64, kBlock - 64);
     if (c.s4) {                         // block-uniform: still during the walk, clip and stage
       ctl_group_sync(arrived, kWaves - 1);
       for (int t = tid - 64; t < 2 * C; t += kBlock - 64) {

@@ -93,15 +93,21 @@ __host__ __device__ __forceinline__ double ctl_cand_one(int c, int k, int j, int
   }
   return np_clip(u, lo_j, hi_j);
 }
-// Both inputs of candidate c at step k (one Philox call) into u[0], u[1].
+// Both inputs of candidate c at step k into u[0], u[1], given the pair's variates (z0, z1).
+__host__ __device__ __forceinline__ void ctl_cand_pair_z(int c, int k, int H, const double* prev_seq, const double* up,
+                                                         const double* ns, const double* lo, const double* hi,
+                                                         double z0, double z1, double* u) {
+  u[0] = ctl_cand_one(c, k, 0, H, prev_seq, up[0], ns[0], lo[0], hi[0], z0);
+  u[1] = ctl_cand_one(c, k, 1, H, prev_seq, up[1], ns[1], lo[1], hi[1], z1);
+}
+// ... drawing them (one Philox call).
 __host__ __device__ __forceinline__ void ctl_cand_pair(int c, int k, int H, const double* prev_seq /*[H][2] or null*/,
                                                        const double* up, const double* ns, const double* lo,
                                                        const double* hi, uint64_t tick, uint64_t seed, uint32_t stream,
                                                        double* u) {
   double z0 = 0.0, z1 = 0.0;
   if (c > 0) ctl_z2((uint32_t)(c * H + k), tick, seed, stream, z0, z1);
-  u[0] = ctl_cand_one(c, k, 0, H, prev_seq, up[0], ns[0], lo[0], hi[0], z0);
-  u[1] = ctl_cand_one(c, k, 1, H, prev_seq, up[1], ns[1], lo[1], hi[1], z1);
+  ctl_cand_pair_z(c, k, H, prev_seq, up, ns, lo, hi, z0, z1, u);
 }
 
 // The rate clip of one (candidate, input) chain in order over k (controller.py
@@ -233,6 +239,9 @@ struct CtlLaunch {
   uint64_t* slot_tag;         // [kCtlSlotsMax][4] slot results: cost hi, lo, cand, nf | late << 31
   unsigned* tickets;          // [1] the look-back ticket
   double* dbg;                // null, or this tick's xref [2][H+1] then U [C][H][2]
+  double* znoise;             // [2][C H][2]: the candidates' variates of tick t in half t & 1
+  uint64_t* ztag;             // [2]: t + 1 once half t & 1 holds tick t's (the completing block
+                              //   of tick t - 1 draws them while it polls)
   const double* pts;          // raceline points [2][np] (project_fast's polyline)
   const double* prefix;       // [np - 1] start arc length per projection index
   uint64_t tick, seed;
