@@ -78,8 +78,9 @@ static_assert(offsetof(llampc_ctl_out, tick) == sizeof(llampc_plan_out) &&
 // Diagnostic build only: s_memrealtime (100 MHz) per block and phase of the last launch
 // (tools/diag/ctl_phases.py).  Look-ahead blocks: 0 entry, 1 staged, 10 walk done, 2 walk
 // barrier, 3 selection, 4 rolled out, 5 published; look-back blocks: 0 entry, 6 scored,
-// 7 lb_final done (ticket winner), 8 slots polled, 11 record stores issued, 9 record written.
-static __device__ unsigned long long g_ctl_ph[64][12];
+// 7 lb_final done (ticket winner), 8 slots polled, 12 top-K / sequence stores issued, 13 the
+// record words computed, 11 record stores issued, 9 record written.
+static __device__ unsigned long long g_ctl_ph[64][16];
 #define CTL_STAMP(blk, slot)                                                                   \
   do {                                                                                         \
     if (threadIdx.x == 0 && (blk) < 64) g_ctl_ph[blk][slot] = __builtin_amdgcn_s_memrealtime(); \
@@ -220,6 +221,17 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   }
   // the current model (this block writes it after the poll): loaded now, off the tail
   const int64_t cur_model = (tid < 64 && warm) ? st->current_model : 0;
+  // x_prev: every look-back block has read it (this block holds the last ticket) and the
+  // look-ahead blocks never do — stored now, so no load of x_t (kernel argument, global)
+  // sits behind the record's host stores after the poll
+  if (tid < 6) st->x_prev[tid] = c.x_t[tid];
+  // the record's scalar kernel arguments, loaded (and kept) before the poll: the tail used
+  // to wait for them one by one after it
+  int32_t a_wc = c.fin.window_count, a_full = c.fin.full, a_K = c.K, a_warm = c.warm, a_lap = c.lap_projidx;
+  int64_t a_goff = c.fin.goff, a_tick = (int64_t)c.tick;
+  double a_scale = c.use_mu ? c.v_factor : c.scale_fixed;
+  asm volatile("" : "+s"(a_wc), "+s"(a_full), "+s"(a_K), "+s"(a_warm), "+s"(a_lap));
+  asm volatile("" : "+s"(a_goff), "+s"(a_tick), "+s"(a_scale));
   // waves 1-3 draw the next tick's variates while wave 0 polls (off every critical path)
   if (tid >= 64) ctl_draw_next(c, tid - 64, kBlock - 64);
   // every slot's result (tagged words of the look-ahead blocks)
@@ -250,6 +262,8 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   // the record and the state
   const int ss = warm ? 0 : c.K;                                   // the selected model's slot
   const int scand = pcand[ss] >= 0 ? pcand[ss] : 0;
+  // (assembling the record in LDS and copying it with 16-B stores made the system fence wait
+  // ~2 us for the ~100 wide host stores: +1 us on the tail, profiles/r04/s4/ctl_phases_image.txt)
   llampc_ctl_out* o = c.out;
   llampc_plan_out* po = &o->plan;
   const double nan = __builtin_nan("");
@@ -269,7 +283,7 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     (&st->useq[0][0])[tid] = v;
     if (tid < 2) st->u_prev[tid] = v;
   }
-  if (tid < 6) st->x_prev[tid] = c.x_t[tid];
+  CTL_STAMP(blockIdx.x, 12);
   if (tid < 64) {
     // wave 0: the look-ahead best over the rolled-out slots (flattened (model, candidate)
     // order, NaN last, ties to the lower key) as a wave pick, then the record's scalars as
@@ -279,15 +293,15 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     const bool slot = q < c.nslots;
     const bool valid = slot && !warm && pcand[q] >= 0 && cs.ids[q] != kNoLocal;
     double lav = valid ? pcost[q] : nan;
-    int64_t lai = valid ? (c.fin.goff + (int64_t)cs.ids[q]) * C + pcand[q] : kNoIndex;
+    int64_t lai = valid ? (a_goff + (int64_t)cs.ids[q]) * C + pcand[q] : kNoIndex;
     wave_pick_nl64(lav, lai);
     const int nf = wave_sum(slot ? pnf[q] : 0);
     int anyl = 0;
     for (int w = 0; w < kWaves; ++w) anyl |= late_w[w];
-    const int64_t sel = warm ? cur_model : c.fin.goff + (int64_t)cs.ids[c.K];
+    const int64_t sel = warm ? cur_model : a_goff + (int64_t)cs.ids[a_K];
     const double dr = pmu[0], df = pmu[1], mu_pred = pmu[2];
     int pj = pmisc[0];
-    if (pj > c.lap_projidx) pj = 0;                                // rt.py:287-296
+    if (pj > a_lap) pj = 0;                                        // rt.py:287-296
     int64_t lm;
     int32_t lc;
     split_key(lai == kNoIndex ? 0 : lai, C, lm, lc);
@@ -295,30 +309,30 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     auto bits = [](double v) { return (uint64_t)__double_as_longlong(v); };
     // llampc_plan_out words 0..9 (lb_best / lb_best_val, words 2 and 3, are lb_final's unless
     // warm), then llampc_ctl_out's words after the plan record (static_asserts below)
-    uint64_t w = 0;
-    bool store = true;
-    uint64_t* dst = reinterpret_cast<uint64_t*>(po) + q;
-    switch (q) {
-      case 0: w = pack(c.fin.window_count, c.fin.full); break;
-      case 1: w = pack(c.K, 1); break;                                 // sel_owned
-      case 2: w = (uint64_t)(int64_t)-1; store = warm; break;
-      case 3: w = bits(nan); store = warm; break;
-      case 4: w = (uint64_t)sel; break;
-      case 5: w = pack(pcand[ss], nf); break;
-      case 6: w = bits(pcost[ss]); break;
-      case 7: w = (uint64_t)(lai == kNoIndex ? (int64_t)-1 : lm); break;
-      case 8: w = pack(lai == kNoIndex ? -1 : lc, anyl ? kPollTimeoutStatus : 0); break;
-      case 9: w = bits(lai == kNoIndex ? nan : lav); break;
-      case 10: w = (uint64_t)(int64_t)c.tick; break;
-      case 11: w = pack(pj, c.warm); break;
-      case 12: w = bits(pmu[3]); break;                                // mu_used
-      case 13: w = bits(c.use_mu ? c.v_factor : c.scale_fixed); break;
-      case 14: w = bits(mu_pred); break;
-      case 15: w = bits(dr); break;
-      case 16: w = bits(df); break;
-      default: store = false;
-    }
-    if (q >= 10) dst = reinterpret_cast<uint64_t*>(&o->tick) + (q - 10);
+    // every word uniform, each lane selects its own (no per-lane branches)
+    const uint64_t W[17] = {pack(a_wc, a_full),
+                            pack(a_K, 1),                                  // sel_owned
+                            (uint64_t)(int64_t)-1,
+                            bits(nan),
+                            (uint64_t)sel,
+                            pack(pcand[ss], nf),
+                            bits(pcost[ss]),
+                            (uint64_t)(lai == kNoIndex ? (int64_t)-1 : lm),
+                            pack(lai == kNoIndex ? -1 : lc, anyl ? kPollTimeoutStatus : 0),
+                            bits(lai == kNoIndex ? nan : lav),
+                            (uint64_t)a_tick,
+                            pack(pj, a_warm),
+                            bits(pmu[3]),                                  // mu_used
+                            bits(a_scale),
+                            bits(mu_pred),
+                            bits(dr),
+                            bits(df)};
+    uint64_t w = W[0];
+#pragma unroll
+    for (int i = 1; i < 17; ++i) w = q == i ? W[i] : w;
+    const bool store = q < 17 && (warm || (q != 2 && q != 3));
+    uint64_t* dst = q < 10 ? reinterpret_cast<uint64_t*>(po) + q : reinterpret_cast<uint64_t*>(&o->tick) + (q - 10);
+    CTL_STAMP(blockIdx.x, 13);
     if (store) *dst = w;
     if (q == 0) {
       st->mu_pred = mu_pred;

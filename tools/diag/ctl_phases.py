@@ -55,14 +55,14 @@ def step(paced_until=None):
 
 for i in range(40):
     step()
-buf = (ctypes.c_ulonglong * (64 * 12))()
+buf = (ctypes.c_ulonglong * (64 * 16))()
 for mode in ("paced", "back-to-back"):
     nxt = time.perf_counter()
     for i in range(T):
         nxt += 1e-3
         hb, hw, hr = step(nxt if mode == "paced" else None)
         lib.llampc_debug_ctl_stamps(buf)
-        Z = np.frombuffer(buf, dtype=np.uint64).reshape(64, 12).astype(np.int64)
+        Z = np.frombuffer(buf, dtype=np.uint64).reshape(64, 16).astype(np.int64)
         live = Z[:, 0] > 0
         base = Z[live, 0].min()
         us = lambda v: (v - base) / 100.0  # noqa: E731
@@ -70,7 +70,8 @@ for mode in ("paced", "back-to-back"):
         la = [k for k in range(64) if live[k] and Z[k, 5] >= base and Z[k, 1] >= base]
         parts = [f"{mode} tick: host begin {hb:.1f} wait {hw:.1f} result {hr:.1f} us |"]
         parts.append(f"lb(block {win}): scored {us(Z[win, 6]):.1f} lb_final {us(Z[win, 7]):.1f} "
-                     f"polled {us(Z[win, 8]):.1f} stored {us(Z[win, 11]):.1f} record {us(Z[win, 9]):.1f} |")
+                     f"polled {us(Z[win, 8]):.1f} seq {us(Z[win, 12]):.1f} words {us(Z[win, 13]):.1f} "
+                     f"stored {us(Z[win, 11]):.1f} record {us(Z[win, 9]):.1f} |")
         for slot in (1, 10, 2, 3, 4, 5):
             v = np.array([us(Z[k, slot]) for k in la])
             parts.append(f"{NAMES[slot]} {v.min():.1f}/{v.max():.1f}")

@@ -1,6 +1,6 @@
 """Diagnostic (build-time): VALU+SALU instructions per H-step of the fast look-ahead rollout
 loop for each lane split (LPM 1/2/4) of plan_kernel<RK4, staged, LPM, xref shared> and of the
-controller tick's ctl_kernel<LPM> (unstaged, candidates in LDS), from hipcc -S listings of the
+controller tick's ctl_kernel<LPM> (candidates in LDS, input terms staged: the shortest loop), from hipcc -S listings of the
 translation units that hold them.  bench.py's ISSUE_INSTR_PER_STEP holds the plan numbers.
 usage: python tools/diag/isa_counts.py [extra hipcc flags, e.g. -DLLAMPC_LEAN_TERMS=7]"""
 import collections
@@ -61,4 +61,4 @@ report("plan LPM 1 (staged)", loop_of(asm1, r"^_ZN6llampc11plan_kernelILi0ELb1EL
 report("plan LPM 1 (work queue, 8 waves)", loop_of(asm1, r"^_ZN6llampc11plan_kernelILi0ELb1ELi1ELi0ELb0ELi2E\S+:"))
 asmc = listing("ctl")
 for lpm in (4, 2, 1):
-    report(f"ctl LPM {lpm} (candidates in LDS)", loop_of(asmc, rf"^_ZN6llampc10ctl_kernelILi{lpm}EEEvNS_9CtlLaunchE:"))
+    report(f"ctl LPM {lpm} (staged inputs)", loop_of(asmc, rf"^_ZN6llampc10ctl_kernelILi{lpm}EEEvNS_9CtlLaunchE:"))
