@@ -570,6 +570,22 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   const double mu = c.use_mu ? ld_wt(&st->mu_pred) : c.mu_fixed;
   const double scale = c.use_mu ? c.v_factor : c.scale_fixed;
   const MuBracket br = mu_bracket(rl.mus, rl.M, mu);
+  // waves 1-3: this tick's candidate variates (the previous tick's completion drew them) are
+  // loaded now, their latency under the tables' (used only when their tag matches: ctl_draw)
+  constexpr int kZPre = 16;
+  const int CH = C * H;
+  const bool zfit = c.znoise != nullptr && CH <= kZPre * (kBlock - 64);
+  double zr[kZPre][2];
+  if (tid >= 64 && zfit) {
+    const double* zb = c.znoise + 2 * (size_t)CH * (int)(c.tick & 1);
+#pragma unroll
+    for (int i = 0; i < kZPre; ++i) {
+      const int p = tid - 64 + i * (kBlock - 64);
+      const int pc = p < CH ? p : CH - 1;
+      zr[i][0] = zb[2 * pc];
+      zr[i][1] = zb[2 * pc + 1];
+    }
+  }
   // (a) tables: knots, x/y rows, the two speed profiles bracketing mu (cs_stage); (b)
   //     project_fast of x_t on raceline[:, p0 : p0 + 10] (track.py:147-160)
   cs_stage(rl, br, kn, spd);
@@ -585,7 +601,19 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
                        sx, &vr);
     CTL_STAMP(blockIdx.x, 10);
   } else {
-    ctl_draw(c, prev_seq, up0, up1, Ul, tid - 64, kBlock - 64);
+    if (zfit && c.ztag[(int)(c.tick & 1)] == c.tick + 1) {          // launch-uniform
+      const double up[2] = {up0, up1};
+#pragma unroll
+      for (int i = 0; i < kZPre; ++i) {
+        const int p = tid - 64 + i * (kBlock - 64);
+        if (p < CH) {
+          const int cc = p / H, k = p - cc * H;
+          ctl_cand_pair_z(cc, k, H, prev_seq, up, c.nscale, c.umin, c.umax, zr[i][0], zr[i][1], Ul + 2 * (size_t)p);
+        }
+      }
+    } else {
+      ctl_draw(c, prev_seq, up0, up1, Ul, tid - 64, kBlock - 64);
+    }
     if (c.s4) {                         // block-uniform: still during the walk, clip and stage
       ctl_group_sync(arrived, kWaves - 1);
       for (int t = tid - 64; t < 2 * C; t += kBlock - 64) {
