@@ -205,3 +205,41 @@ def test_ctl_two_tracks_async_equal_sequential(nat):
         assert ra[:2] == rb[:2] and ra[3] == rb[3]
         assert ra[2] == rb[2] or (np.isnan(ra[2]) and np.isnan(rb[2]))
         np.testing.assert_array_equal(ra[4], rb[4])
+
+
+def test_ctl_staged_inputs_equal_unstaged(nat, monkeypatch):
+    """The look-ahead's staged input terms (sin / cos delta per (candidate, step), the summed
+    input-rate cost and feasibility per candidate, ctl.hip ctl_stage) against the rollout
+    forming them per step (LLAMPC_CTL_NO_STAGE=1 at create): the same records, bitwise, over
+    ticks through the warm-up and the selection, with the variates of ticks >= 1 drawn one tick
+    ahead by the completion (ctl_draw_next) and those of tick 0 in the launch."""
+    from llampc.mpc import DeviceController, ModelBank, generate_bank
+    from llampc.params import ORCA
+    nominal = [ORCA()[k] for k in ("Bf", "Cf", "Df", "Br", "Cr", "Dr")]
+    tr, _ = tracks("ETHZ")
+    p = generate_bank(2000, seed=3)
+    x_start = start_state("ETHZ", tr)
+    recs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("LLAMPC_CTL_NO_STAGE", flag)
+        b = ModelBank(p, W=5, device=0)
+        ctl = DeviceController(b, tr, H=40, C=64, K=10, nominal6=nominal)
+        x = x_start.copy()
+        plant = O.Vehicle.from_params(O.orca_params())
+        got = []
+        try:
+            for t in range(12):
+                o = ctl.tick(x)
+                got.append((o.plan.sel_model, o.plan.sel_cand, o.plan.sel_cost, o.plan.la_best_model,
+                            o.plan.la_best_cand, o.plan.la_best_cost, o.projidx, o.mu_pred,
+                            np.ctypeslib.as_array(o.plan.topk_cand).copy(), np.ctypeslib.as_array(o.plan.topk_cost).copy(),
+                            np.ctypeslib.as_array(o.u_seq)[:40].copy()))
+                xn, _ = O.sim_continuous(plant, x, np.array(o.u_seq[0][:]).reshape(2, 1), [0, TS])
+                x = xn[:, -1]
+        finally:
+            ctl.close()
+            b.close()
+        recs.append(got)
+    for a, c in zip(*recs):
+        for va, vc in zip(a, c):
+            np.testing.assert_array_equal(np.asarray(va), np.asarray(vc))

@@ -1244,6 +1244,36 @@ def test_setupnlp_cem_equals_oracle(nat):
         nlp.close()
 
 
+def test_setupnlp_one_launch_equals_round_launches(nat, monkeypatch):
+    """Every CEM round in one launch (the sample blocks wait for each round's mean / std on a
+    tagged word, nlp.hpp nlp_persistent) against one launch per round
+    (LLAMPC_NLP_ROUND_LAUNCHES=1 at create): the same umpc, fval and xmpc, bitwise, over four
+    successive solves (the warm start and the best-so-far carried across rounds)."""
+    from llampc.mpc.planner import ConstantSpeed
+    from llampc.tracks import ETHZ
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    tr = ETHZ('optimal', True)
+    outs = []
+    for per_round in ("0", "1"):
+        monkeypatch.setenv("LLAMPC_NLP_ROUND_LAUNCHES", per_round)
+        nlp, _ = _nlp()
+        try:
+            got = []
+            for t in (10, 11, 12, 13):
+                x0, up = s[:, t].copy(), u[:, t - 1].copy()
+                xref, _, _ = ConstantSpeed(x0[:2], x0[3], tr, 20, TS, 0)
+                umpc, fval, xmpc, _ = nlp.solve(x0, xref, up)
+                got.append((np.array(umpc, copy=True), float(fval), np.array(xmpc, copy=True)))
+        finally:
+            nlp.close()
+        outs.append(got)
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a[0], b[0])
+        assert a[1] == b[1]
+        np.testing.assert_array_equal(a[2], b[2])
+
+
 @pytest.mark.parametrize("samples,elite,iters,H", [(64, 5, 3, 20), (256, 17, 3, 20), (4096, 64, 2, 20), (1024, 1, 2, 20),
                                                    (512, 32, 3, 40)])
 def test_setupnlp_cem_shapes_equal_oracle(nat, samples, elite, iters, H):
