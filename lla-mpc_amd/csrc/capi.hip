@@ -174,6 +174,7 @@ struct llampc_bank {
   double* d_rl = nullptr;          // raceline table: knots | xy | speed | mus
   int32_t rl_n = 0, rl_M = 0;
   double rl_hmin = 1.0, rl_vmax = 0.0;   // the walkers' speed-window bounds (raceline.hpp)
+  std::vector<double> rl_mus;            // the profiles' mu values (host copy: the controller's bracket)
   double* d_xref_pm = nullptr;     // per-model references [n][H][2] (RACELINE ticks)
   size_t xref_pm_cap = 0;
   int64_t timing_seen[3] = {0, 0, 0};
@@ -860,6 +861,7 @@ int llampc_bank_set_raceline(llampc_bank* b, const double* knots, int32_t n, con
   HIP_TRY(hipMemcpy(d + n + 8 * m + 4 * m * M, mus, M * sizeof(double), hipMemcpyHostToDevice));
   b->rl_n = n;
   b->rl_M = M;
+  b->rl_mus.assign(mus, mus + M);
   double hmin = knots[1] - knots[0];
   for (int32_t i = 2; i < n; ++i) hmin = std::min(hmin, knots[i] - knots[i - 1]);
   b->rl_hmin = hmin;
@@ -1170,6 +1172,12 @@ struct llampc_ctl {
   llampc_bank* b = nullptr;
   llampc_ctl_cfg cfg{};
   bool no_stage = false;                 // LLAMPC_CTL_NO_STAGE=1: unstaged look-ahead inputs (A/B)
+  // the state's projidx / mu-hat as the last record left them (the look-ahead prologue's
+  // projection and mu bracket come as kernel arguments); hint_ok = false after a failed wait:
+  // the next tick reads them from the device first
+  bool hint_ok = true;
+  int32_t hint_p0 = 0;
+  double hint_mu = std::nan("");
   CtlState* d_st = nullptr;
   double* d_pts = nullptr;               // points [2][np] | prefix [np - 1]
   int32_t np = 0;
@@ -1392,6 +1400,16 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   L.do_lb = do_lb;
   L.warm = warm;
   L.use_mu = t > W + 1;                  // rt.py:278
+  if (!c->hint_ok) {                     // after a failed wait: the state itself
+    CtlState hs{};
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipMemcpy(&hs, c->d_st, sizeof hs, hipMemcpyDeviceToHost));
+    c->hint_p0 = hs.projidx;
+    c->hint_mu = hs.mu_pred;
+    c->hint_ok = true;
+  }
+  L.p0_walk = c->hint_p0;
+  L.br_walk = mu_bracket(b->rl_mus.data(), b->rl_M, L.use_mu ? c->hint_mu : L.mu_fixed);   // rt.py:278-282
   L.full = full;
   L.nslots = warm ? 1 : k.K + 1;
   L.G = lookahead_group(k.C);
@@ -1432,6 +1450,7 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
   std::lock_guard<std::mutex> lc(c->mu);
   if (!c->pending) return fail(LLAMPC_E_STATE, "no controller tick outstanding");
   c->pending = false;
+  c->hint_ok = false;                    // until this tick's record is read
   DeviceGuard g(c->b->device);
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t spins = 0;
@@ -1446,6 +1465,9 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
   std::memcpy(out, const_cast<const llampc_ctl_out*>(c->h_out), sizeof(llampc_ctl_out));
   if (out->plan.status)
     return fail(LLAMPC_E_DEVICE, "controller tick record status %d (an in-launch wait timed out)", out->plan.status);
+  c->hint_p0 = out->projidx;             // the state this tick left (ctl_complete writes both)
+  c->hint_mu = out->mu_pred;
+  c->hint_ok = true;
   return LLAMPC_OK;
 }
 

@@ -79,7 +79,8 @@ static_assert(offsetof(llampc_ctl_out, tick) == sizeof(llampc_plan_out) &&
 // (tools/diag/ctl_phases.py).  Look-ahead blocks: 0 entry, 1 staged, 10 walk done, 2 walk
 // barrier, 3 selection, 4 rolled out, 5 published; look-back blocks: 0 entry, 6 scored,
 // 7 lb_final done (ticket winner), 8 slots polled, 12 top-K / sequence stores issued, 13 the
-// record words computed, 11 record stores issued, 9 record written.
+// record words computed, 11 record stores issued, 9 record written; look-ahead prologue: 14 the
+// mu bracket known, 15 the tables' LDS stores issued.
 static __device__ unsigned long long g_ctl_ph[64][16];
 #define CTL_STAMP(blk, slot)                                                                   \
   do {                                                                                         \
@@ -564,12 +565,13 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   if (tid == 0) *arrived = 0;
   const CtlState* st = c.st;
   const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
-  const int p0 = st->projidx;
-  // rt.py:278-282 (mu-hat read as an atomic load: a select between it and the kernel argument
-  // would be folded into a select of their addresses, which keeps the argument in scratch)
-  const double mu = c.use_mu ? ld_wt(&st->mu_pred) : c.mu_fixed;
+  // rt.py:278-282: projidx and the mu bracket (mu-hat or the fixed mu) come from the host's
+  // copy of the state (CtlLaunch.p0_walk / br_walk): the tables' loads follow the kernel
+  // arguments directly (profiles/r04/s4/ctl_phases_prologue.txt: 2.5 us to the bracket before)
+  const int p0 = c.p0_walk;
   const double scale = c.use_mu ? c.v_factor : c.scale_fixed;
-  const MuBracket br = mu_bracket(rl.mus, rl.M, mu);
+  const MuBracket br = c.br_walk;
+  CTL_STAMP(blockIdx.x, 14);
   // waves 1-3: this tick's candidate variates (the previous tick's completion drew them) are
   // loaded now, their latency under the tables' (used only when their tag matches: ctl_draw)
   constexpr int kZPre = 16;
@@ -589,6 +591,7 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   // (a) tables: knots, x/y rows, the two speed profiles bracketing mu (cs_stage); (b)
   //     project_fast of x_t on raceline[:, p0 : p0 + 10] (track.py:147-160)
   cs_stage(rl, br, kn, spd);
+  CTL_STAMP(blockIdx.x, 15);
   const int segs = cs_project(c.pts, c.np, p0, c.x_t[0], c.x_t[1], dist);
   __syncthreads();
   CTL_STAMP(blockIdx.x, 1);

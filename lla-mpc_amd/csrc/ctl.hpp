@@ -256,6 +256,9 @@ struct CtlLaunch {
   int32_t do_lb, warm, use_mu, full, nslots, mpb, G, cpl, S, K;
   int32_t nb_lb, nb_la;
   int32_t s4;                 // stage each (candidate, step)'s sincos / cost terms (CtlLds.s4)
+  int32_t p0_walk;            // the state's projidx and the walk's mu bracket (rt.py:278-282),
+  MuBracket br_walk;          //   from the host's copy of the last record: the look-ahead
+                              //   prologue's table loads wait on no state or mu-table load
 };
 
 // llampc_ctl_reference's launch: ConstantSpeed alone (planner.py:12-67) on the device.

@@ -16,3 +16,4 @@ for rep in 1 2 3; do
 done
 timeout -k 10 180 python -u tools/diag/ctl_phases.py 10000 4 > $OUT/ctl_phases.txt 2>&1 || { tail -5 $OUT/ctl_phases.txt; exit 1; }
 cut -c1-300 $OUT/ctl_phases.txt | grep tick
+cut -c150-420 $OUT/ctl_phases.txt | grep -v amdgpu
