@@ -7,6 +7,7 @@ ticks enqueued back to back with no synchronisation, so the mailbox's two slots 
 under load) and "host" (gloo gather,
 merge_kernel).  Every rank's merged record, tick after tick, must equal the unsharded tick of
 the whole bank on the same inputs."""
+import datetime
 import os
 import socket
 import sys
@@ -66,7 +67,8 @@ def _worker(rank, world, port, q, transport, C=3):
         from llampc.mpc import generate_bank
         from llampc.mpc.sharded import ShardedBank, _bytes_of
         torch.cuda.set_device(0)
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=60))
         sb = ShardedBank(generate_bank(n_models(world, C), seed=12), rank, world, 0, W=W)
         assert sb.transport == transport, (sb.transport, transport)
         pins = [sb.make_plan_in(sb.stage(*a)["pack"], C, H, K=K, current_model=5) for a in _ticks(C)]
@@ -88,6 +90,40 @@ def _worker(rank, world, port, q, transport, C=3):
         q.put((rank, None, traceback.format_exc()))
 
 
+def _run_ranks(world, transport, C):
+    """The ranks in spawned processes; a rendezvous port taken by another process between
+    _free_port and the store's bind (EADDRINUSE) is retried on a new port, and every rank
+    process is reaped whatever happens (a rank left waiting on its rendezvous would keep the
+    test runner from exiting)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    for attempt in range(3):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, q, transport, C)) for r in range(world)]
+        for p in procs:
+            p.start()
+        got, errs = {}, []
+        try:
+            for _ in range(world):
+                rank, recs, err = q.get(timeout=150)
+                if err is not None:
+                    errs.append((rank, err))
+                    break
+                got[rank] = recs
+        finally:
+            for p in procs:
+                p.join(timeout=30 if not errs else 1)
+                if p.is_alive():
+                    p.terminate()
+                    p.join(timeout=10)
+        if not errs:
+            return got
+        if "EADDRINUSE" not in errs[0][1] or attempt == 2:
+            raise AssertionError(f"rank {errs[0][0]}:\n{errs[0][1]}")
+    raise AssertionError("unreachable")
+
+
 CASES = ([(w, "peer", 3) for w in (2, 3, 4, 8)] + [(w, "host", 3) for w in (2, 3, 8)] +
          [(w, "peer-split", 3) for w in (2, 4)] + [(w, "peer-ticket", 3) for w in (2, 3, 8)] +
          [(2, "peer", 64), (3, "peer-ticket", 64), (2, "peer-wq8", 64), (3, "peer-ticket-wq8", 64)])
@@ -97,26 +133,13 @@ CASES = ([(w, "peer", 3) for w in (2, 3, 4, 8)] + [(w, "host", 3) for w in (2, 3
 def test_sharded_tick_equals_unsharded_on_gpu(world, transport, C):
     """peer-ticket: LLAMPC_NO_POLL=1, so the record's look-back half is written by lb_final in
     another block than the one that pushes it to the peers (the sc1 hand-off of peer_finish)."""
-    import torch.multiprocessing as mp
     from llampc import _native as nat
     from llampc.mpc import ModelBank, generate_bank
     from llampc.mpc.sharded import _out_of
     nat.load()
     if nat.device_count() < 1:
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X")
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, transport, C)) for r in range(world)]
-    for p in procs:
-        p.start()
-    got = {}
-    for _ in range(world):
-        rank, recs, err = q.get(timeout=150)
-        assert err is None, f"rank {rank}:\n{err}"
-        got[rank] = recs
-    for p in procs:
-        p.join(timeout=30)
+    got = _run_ranks(world, transport, C)
     ref = []
     with ModelBank(generate_bank(n_models(world, C), seed=12), W=W, device=0) as b:
         for a in _ticks(C):
