@@ -49,6 +49,11 @@ FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation
 # capacity: 1,024 SIMDs x 16 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md max clock).
 ISSUE_INSTR_PER_STEP = {4: 444, 2: 556, 1: 777}   # tools/diag/isa_counts.py (LPM 1: work queue)
 ISSUE_PEAK_LANE_INSTR = 1024 * 16 * 2.4e9
+# the controller's and the NLP search's rollout steps (tools/diag/isa_counts.py): the
+# controller's LPM-4 step with its staged input terms, the NLP's LPM-4 Euler step with staged terms
+CTL_INSTR_PER_STEP = 446
+NLP_INSTR_PER_STEP = 159
+LOOKBACK_INSTR_PER_MODEL = ISSUE_INSTR_PER_STEP[1]   # one LPM-1 RK4 step + error + ring per model (upper bound)
 
 
 EXCHANGE_DESC = {
@@ -83,44 +88,10 @@ def parse():
 
 
 def make_ticks(args, T, seed=0):
-    """T ticks of (x_prev, u_prev, x_now, uprev, xref, U) for the gradual-friction scenario."""
-    from llampc.models import Dynamic
-    from llampc.mpc import CandidateGenerator, ConstantSpeed
-    from llampc.params import ORCA
-    from llampc.tracks import ETHZ, ETHZMobil
-    d = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))
-    u_rec = d["inputs"]
-    p = ORCA()
-    plant = Dynamic(**p, device=torch_device_index())
-    x = d["states"][:, 0].copy()
-    track = ETHZ('optimal', True) if args.track == "ETHZ" else ETHZMobil('optimal', True)
-    gen = CandidateGenerator(args.C, args.H, seed=2)
-    H, Ts = args.H, 0.02
-    scenario = getattr(args, "scenario", None) or ("sudden" if args.track == "ETHZMobil" else "gradual")
-    if scenario == "gradual":
-        k0 = 100                                # ticks into the decay (SURVEY §8d config 2)
-        Df, Dr = p["Df"] * (1 - 1 / 2600.) ** k0, p["Dr"] * (1 - 1 / 2600.) ** k0
-    else:                                       # config 3: the 9-tick drop x21/22 (rt.py:132-141)
-        Df, Dr = p["Df"], p["Dr"]
-    packs, projidx = [], 0
-    for t in range(T + 1):
-        u = u_rec[:, t % u_rec.shape[1]]
-        plant.Df, plant.Dr = Df, Dr
-        xn, _ = plant.sim_continuous(x, u.reshape(2, 1), [0, Ts])
-        x_next = xn[:, -1]
-        if t >= 1:
-            mu = (Df + Dr) / (9.81 * p["mass"])
-            xref, projidx, _ = ConstantSpeed(x_next[:2], x_next[3], track, H, Ts, projidx, curr_mu=mu, scale=0.9)
-            U = gen(None, u)
-            packs.append(np.concatenate([x, u, x_next, u, xref.ravel(), U.ravel()]))
-        x = x_next
-        if scenario == "gradual":
-            Df -= Df / 2600.
-            Dr -= Dr / 2600.
-        elif 2 <= t < 11:                       # nine ticks of D -= D/22 (rt.py:132-140)
-            Df -= Df / 22.
-            Dr -= Dr / 22.
-    return np.stack(packs[:T])
+    """T ticks of (x_prev, u_prev, x_now, uprev, xref, U) of the config's friction scenario
+    (llampc.mpc.scenarios: config 2 gradual on ETHZ, config 3 sudden on ETHZMobil)."""
+    from llampc.mpc.scenarios import scenario_ticks
+    return scenario_ticks(args.track, args.H, args.C, T, getattr(args, "scenario", None), device=torch_device_index())
 
 
 _DEV = [0]
@@ -289,20 +260,22 @@ def spawn_ranks(n: int, cmd=None) -> int:
     """`bench.py --gpus N` (N > 1) started WITHOUT a launcher (no RANK in the environment):
     start N rank processes of this same command line, one per GPU, with the environment
     torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE,
-    MASTER_ADDR=127.0.0.1, a free MASTER_PORT), and return their exit status.  This parent
-    never touches the GPU — no torch import, no HIP call, no exec — it starts, watches and, if
-    one rank fails, stops its own children by PID so the rest do not wait in a rendezvous."""
+    MASTER_ADDR=127.0.0.1) and, for the rendezvous, LLAMPC_INIT_FILE: a FileStore path in a
+    private temporary directory (no TCP port to probe and then lose to another process), and
+    return their exit status.  This parent never touches the GPU — no torch import, no HIP call,
+    no exec — it starts, watches and, if one rank fails, stops its own children by PID so the
+    rest do not wait in a rendezvous."""
+    import shutil
     import signal
-    import socket
     import subprocess
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="llampc_rdzv_")
     cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", LLAMPC_INIT_FILE=os.path.join(tmp, "store"))
+        env.pop("MASTER_PORT", None)
         procs.append(subprocess.Popen(cmd, env=env))
     rc, live = 0, list(procs)
     try:
@@ -324,7 +297,20 @@ def spawn_ranks(n: int, cmd=None) -> int:
             if q.poll() is None:
                 q.kill()
                 q.wait()
+        shutil.rmtree(tmp, ignore_errors=True)
     return rc
+
+
+def init_group(backend, rank, world, device=None):
+    """torch.distributed rendezvous: the FileStore of a self-spawned job (LLAMPC_INIT_FILE,
+    spawn_ranks), else env:// (torch.distributed.run's MASTER_ADDR / MASTER_PORT)."""
+    import torch.distributed as dist
+    kw = {"device_id": device} if device is not None else {}
+    path = os.environ.get("LLAMPC_INIT_FILE")
+    if path:
+        dist.init_process_group(backend, init_method=f"file://{path}", rank=rank, world_size=world, **kw)
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
 
 
 def main():
@@ -348,10 +334,7 @@ def main():
     # LLAMPC_FORCE_EXCHANGE=1 (diagnostic, under torch.distributed.run with one rank): the
     # tick runs the collective + device merge of the N > 1 path on a 1-rank group
     if world > 1 or os.environ.get("LLAMPC_FORCE_EXCHANGE"):
-        if backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend, rank=rank, world_size=world)
+        init_group(backend, rank, world, torch.device("cuda", local) if backend == "nccl" else None)
     from llampc import _native as nat
     from llampc.mpc import generate_bank
     from llampc.mpc.sharded import ShardedBank
@@ -787,6 +770,7 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
     setups = []
     for seed, tr in ((0, ETHZ('optimal', True)), (1, ETHZMobil('optimal', True))):
         b = ModelBank(generate_bank(args.n_per_gpu, seed=seed), W=args.W, device=dev)
+        b.set_concurrency(2)                # two controllers tick together: a hardware queue each
         ctl = LLAMPC(b, tr, H=H, C=C, K=args.K, mode="device")
         plant = Dynamic(**p, device=dev)
         if tr.name == "ETHZ":
@@ -830,10 +814,34 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
             s[1].close()
             s[0].close()
     q = pctl(np.array(lat[warm:warm + ticks]) * 1e6)
+    N, K, W = args.n_per_gpu, args.K, args.W
+    steps_tick = N + (K + 1) * C * H              # look-back steps + the (K+1) x C rollouts' steps
+    # algorithmic HBM bytes of one controller launch: the look-back's params + ring read/write per
+    # model, the rolled-out models' params, the raceline tables one block stages (knots + two
+    # speed profiles), the candidates' variates read and the next tick's written, the state and
+    # the record
+    m = 700                                       # raceline knots (ETHZ 700, Mobil 500: upper)
+    ctl_bytes = N * (48 + 8 * W + 8) + (K + 1) * 48 + 8 * m + 64 * (m - 1) + 2 * 16 * C * H + 2 * 1024 + 2048
+    lane_instr = (K + 1) * C * H * 4 * CTL_INSTR_PER_STEP + N * LOOKBACK_INSTR_PER_MODEL
+    kmean = float(np.mean(kern)) if kern else 0.0
+    issue = None
+    if kmean > 0:
+        ach = lane_instr / (kmean * 1e-6)
+        issue = {"bound": "fp64-valu-issue", "achieved": ach, "peak": ISSUE_PEAK_LANE_INSTR,
+                 "unit": "lane-instructions/s", "frac": ach / ISSUE_PEAK_LANE_INSTR, "lane_instr_per_launch": lane_instr,
+                 "pmc": pmc_issue("ctl_kernel", kmean),
+                 "note": f"static count: (K+1) C H rollout steps x 4 lanes x {CTL_INSTR_PER_STEP} + N x "
+                         f"{LOOKBACK_INSTR_PER_MODEL} (look-back, upper bound) over the mean launch; pmc: "
+                         "SQ_INSTS_VALU x 64 of the committed PMC pass over the same launch time"}
+    extra_ctl = {"rollout_steps_per_tick": steps_tick,
+                 "rollout_steps_per_s_at_p50": 2 * steps_tick / (q["p50"] * 1e-6),
+                 "bytes_per_launch": ctl_bytes,
+                 "hbm_frac": (ctl_bytes / (kmean * 1e-6) / 1e9 / HBM_PEAK_GBS) if kmean > 0 else None,
+                 "issue": issue}
     return {"p50": q["p50"], "p99": q["p99"], "max": q["max"], "ticks": q["ticks"], "period_us": period * 1e6,
             "budget_us": 1000.0, "met": q["p99"] < 1000.0, "tracks": ["ETHZ", "ETHZMobil"],
             "N_per_track": args.n_per_gpu, "H": H, "C": C, "K": args.K, "W": args.W,
-            "kernel_us_avg": kern, "sel_models": sel, "projidx": laps,
+            "kernel_us_avg": kern, "sel_models": sel, "projidx": laps, **extra_ctl,
             "host_split_us_p50": {"begin": float(np.median([a for a, _ in split[warm:warm + ticks]]) * 1e6),
                                   "end": float(np.median([b for _, b in split[warm:warm + ticks]]) * 1e6)},
             "note": "LLAMPC.tick (device mode, llampc_ctl_tick_async/wait: one launch per track per step) for "
@@ -863,18 +871,40 @@ def solve_latency(args, n=200, warm=10, H=20):
         xref, projidx, _ = ConstantSpeed(s[:2, t], s[3, t], tr, H, 0.02, projidx)
         cases.append((s[:, t].copy(), xref, u[:, t - 1].copy()))
     lat, fv = [], []
+    from llampc import _native as nat
+    lib = nat.load()
+    avg = (ctypes.c_double * 3)()
+    cnt = (ctypes.c_int64 * 3)()
     try:
         for i in range(n + warm):
             x0, xref, up = cases[i % len(cases)]
+            if i == warm:                       # per-launch HIP events on the solver's bank
+                nat.check(lib.llampc_bank_timing(nlp._bank.handle, 1, n + 8))
             t0 = time.perf_counter()
             _, fval, _, _ = nlp.solve(x0, xref, up)
             lat.append(time.perf_counter() - t0)
             fv.append(fval)
+        nat.check(lib.llampc_bank_timing_read(nlp._bank.handle, avg, cnt))
     finally:
         nlp.close()
     q = pctl(np.array(lat[warm:]) * 1e6)
+    kus = avg[0] * 1e3
+    steps = nlp.samples * nlp.iters * H
+    lane_instr = steps * 4 * NLP_INSTR_PER_STEP
+    nlp_bytes = nlp.iters * (nlp.samples * (16 * H + 16 * H + 16)) + 16 * (H + 1) + 48 * H + 6 * 8 * (H + 1)
+    issue = None
+    if kus > 0:
+        ach = lane_instr / (kus * 1e-6)
+        issue = {"bound": "fp64-valu-issue", "achieved": ach, "peak": ISSUE_PEAK_LANE_INSTR,
+                 "unit": "lane-instructions/s", "frac": ach / ISSUE_PEAK_LANE_INSTR, "lane_instr_per_launch": lane_instr,
+                 "pmc": pmc_issue("nlp_kernel", kus),
+                 "note": f"static count: samples x rounds x H steps x 4 lanes x {NLP_INSTR_PER_STEP} over the "
+                         "launch (all rounds in one launch); pmc: SQ_INSTS_VALU x 64 of the committed PMC pass"}
     return {"p50": q["p50"], "p99": q["p99"], "max": q["max"], "solves": q["ticks"], "H": H,
             "samples": nlp.samples, "rounds": nlp.iters, "elite": nlp.elite,
+            "kernel_us_avg": kus, "launches_timed": int(cnt[0]), "rollout_steps_per_solve": steps,
+            "rollout_steps_per_s_at_p50": steps / (q["p50"] * 1e-6), "bytes_per_launch": nlp_bytes,
+            "issue": issue,
             "reference_s_per_control_step": 0.03, "fval_p50": float(np.median(fv)),
             "note": "setupNLP(...).solve from Python: the CEM rounds back to back on the GPU + the Euler "
                     "trajectory + one copy back; the reference's 0.03 s is its whole tick incl. IPOPT "
@@ -907,6 +937,22 @@ def lpm_of(n, C):
     if n * G <= 16384 and G <= 64:
         return 4
     return 2 if (n * G <= 32768 and G <= 128) else 1
+
+
+def pmc_issue(kernel: str, kernel_us: float):
+    """Issue fraction of `kernel` from the committed PMC summary (profiles/r05/pmc_kernels.json,
+    tools/pmc_kernels.py): SQ_INSTS_VALU wave-instructions per dispatch x 64 lanes / kernel_us /
+    the chip's issue capacity; None when no pass is committed for the kernel."""
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "r05", "pmc_kernels.json")))
+    except (OSError, ValueError):
+        return None
+    v = d.get(kernel)
+    if not v or not kernel_us:
+        return None
+    lane = v["SQ_INSTS_VALU"] * 64
+    return {"lane_instr_per_launch": lane, "frac": lane / (kernel_us * 1e-6) / ISSUE_PEAK_LANE_INSTR,
+            "source": "profiles/r05/pmc_kernels.json"}
 
 
 def pmc_traffic(args):

@@ -170,13 +170,16 @@ int llampc_bank_launches(const llampc_bank* bank, int64_t* launches);
 int llampc_bank_window(llampc_bank* bank, double* ring, int32_t* window_count);
 /* stream the bank launches on (hipStream_t as void*); NULL = its own stream */
 int llampc_bank_set_stream(llampc_bank* bank, void* stream);
-/* the stream the bank launches on now (its own — a hardware queue of its own, see
- * INTEGRATION.md — or the one set above), for callers that enqueue their own work with it */
+/* the stream the bank launches on now (its own or the one set above), for callers that
+ * enqueue their own work with it */
 int llampc_bank_stream(const llampc_bank* bank, void** stream);
 /* the number of banks the caller ticks concurrently on this device (default 1; BASELINE
  * config 5 ticks two tracks together: 2).  The look-ahead sizes its launch for 1/banks of the
- * chip (its lane split), so the concurrent launches are resident together — replaces nothing
- * in the reference (one process per track there) */
+ * chip (its lane split), so the concurrent launches are resident together, and banks > 1 gives
+ * the bank's own stream a hardware queue of its own (a full-CU-mask stream: two banks' launches
+ * on one of HIP's shared queues would run one after the other).  Other banks
+ * keep a plain non-blocking stream (LLAMPC_DEDICATED_QUEUE=1 at create: a dedicated queue
+ * anyway).  Replaces nothing in the reference (one process per track there) */
 int llampc_bank_set_concurrency(llampc_bank* bank, int32_t banks);
 
 /* Per-kernel HIP-event timing of the bank's launches, on the stream they run on (for the

@@ -141,6 +141,7 @@ struct llampc_bank {
   VehK veh{};
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  bool dedicated = false;                // its own stream has a hardware queue of its own (bank_stream)
   int32_t share = 1;                     // banks ticked concurrently (llampc_bank_set_concurrency)
   double* d_params = nullptr;
   double* d_ring = nullptr;
@@ -519,6 +520,23 @@ bool host_completion(const llampc_bank* b) {
   return b->h_tag && b->h_rec && getenv("LLAMPC_SYNC_COMPLETION") == nullptr;
 }
 
+// After a tick whose record reports a device-side status (an in-launch wait gave up) or whose
+// completion never arrived: once the stream has drained, every in-launch counter is zeroed —
+// the work-queue counter (straggler blocks may have taken units after final_write reset it)
+// and the tickets — so the next launch starts from a clean hand-off state.
+int recover_counters(llampc_bank* b) {
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_wq, 0, sizeof(uint64_t), b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_tickets, 0, 2 * sizeof(unsigned), b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return LLAMPC_OK;
+}
+
+int status_fail(llampc_bank* b, int32_t status) {
+  (void)recover_counters(b);
+  return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", status);
+}
+
 // Spin until the plan kernel has published tick `seq` in h_tag, then copy the record out.
 // A tag that never arrives (a device fault) ends the spin after 10 s: the stream is then
 // synchronised so the HIP error, if any, is the one reported.
@@ -530,6 +548,7 @@ int wait_host_tag(llampc_bank* b, uint64_t seq, llampc_plan_out* out) {
     if ((++spins & 0xFFF) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
       HIP_TRY(hipStreamSynchronize(b->stream));
       if (__atomic_load_n(b->h_tag, __ATOMIC_ACQUIRE) == seq) break;
+      (void)recover_counters(b);
       return fail(LLAMPC_E_DEVICE, "tick %llu: completion tag never arrived", (unsigned long long)seq);
     }
   }
@@ -548,9 +567,12 @@ namespace {
 // step measured 172 us instead of 98 us whenever two other streams were in use first
 // (tools/diag/bench_extra.py).  A stream with a CU mask gets a hardware queue of its own;
 // the mask holds every CU, so nothing else changes.  LLAMPC_SHARED_QUEUES=1 keeps the plain
-// stream; the plain stream is also the fallback.
-hipError_t bank_stream(int device, hipStream_t* s) {
-  if (!std::getenv("LLAMPC_SHARED_QUEUES")) {
+// stream; the plain stream is also the fallback.  Only banks ticked concurrently get one
+// (llampc_bank_set_concurrency(> 1), or LLAMPC_DEDICATED_QUEUE=1 at create): every other bank
+// — a setupNLP's one-model bank, a host-mode nominal bank — keeps a plain non-blocking stream,
+// so a process never opens more hardware queues than it has concurrent banks.
+hipError_t bank_stream(int device, bool dedicated, hipStream_t* s) {
+  if (dedicated && !std::getenv("LLAMPC_SHARED_QUEUES")) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
       std::vector<uint32_t> mask((cus + 31) / 32, 0xFFFFFFFFu);
@@ -608,7 +630,9 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
     llampc_bank_destroy(b);
     return code;
   };
-  if (bank_stream(device, &b->stream) != hipSuccess) return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
+  if (const char* e = std::getenv("LLAMPC_DEDICATED_QUEUE")) b->dedicated = e[0] == '1';
+  if (bank_stream(device, b->dedicated, &b->stream) != hipSuccess)
+    return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
   b->own_stream = true;
   const int64_t lbl = (int64_t)lookback_blocks(n) * (kBlock / 64);   // look-back lists (waves)
   const int64_t lab = n;                 // worst case: one model per block (wave-role, G=64)
@@ -732,6 +756,17 @@ int llampc_bank_set_concurrency(llampc_bank* b, int32_t banks) {
   if (banks < 1 || banks > 64) return fail(LLAMPC_E_ARG, "banks=%d outside [1, 64]", banks);
   std::lock_guard<std::mutex> lk(b->mu);
   b->share = banks;
+  if (banks > 1 && !b->dedicated) {      // concurrent banks: a hardware queue of its own (bank_stream)
+    b->dedicated = true;
+    if (b->own_stream) {
+      DeviceGuard g(b->device);
+      HIP_TRY(hipStreamSynchronize(b->stream));
+      hipStream_t s = nullptr;
+      HIP_TRY(bank_stream(b->device, true, &s));
+      (void)hipStreamDestroy(b->stream);
+      b->stream = s;
+    }
+  }
   return LLAMPC_OK;
 }
 
@@ -745,7 +780,7 @@ int llampc_bank_set_stream(llampc_bank* b, void* stream) {
     b->stream = (hipStream_t)stream;
     b->own_stream = false;
   } else {
-    HIP_TRY(bank_stream(b->device, &b->stream));
+    HIP_TRY(bank_stream(b->device, b->dedicated, &b->stream));
     b->own_stream = true;
   }
   return LLAMPC_OK;
@@ -812,7 +847,7 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
     if ((rc = plan_launch(b, din, b->d_rec, nullptr, nullptr, nullptr, s, b->d_tag, seq, inl ? &pk : nullptr)))
       return rc;
     if ((rc = wait_host_tag(b, seq, out))) return rc;
-    if (out->status) return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", out->status);
+    if (out->status) return status_fail(b, out->status);
     return LLAMPC_OK;
   }
   llampc_plan_in din;
@@ -830,7 +865,7 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
     HIP_TRY(hipMemcpyAsync(cost_out, d_cost, (size_t)b->n * in->C * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   *out = *b->h_out;
-  if (out->status) return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", out->status);
+  if (out->status) return status_fail(b, out->status);
   return LLAMPC_OK;
 }
 
@@ -909,7 +944,7 @@ int llampc_plan_wait(llampc_bank* b, llampc_plan_out* out) {
     HIP_TRY(hipStreamSynchronize(b->stream));
     *out = *b->h_out;
   }
-  if (out->status) return fail(LLAMPC_E_DEVICE, "tick record status %d (in-launch completion timed out)", out->status);
+  if (out->status) return status_fail(b, out->status);
   return LLAMPC_OK;
 }
 
@@ -1199,6 +1234,17 @@ struct llampc_ctl {
   std::mutex mu;
 };
 
+// A failed controller tick (a wait that gave up, or a completion that never arrived): once the
+// stream has drained, the look-back ticket is zeroed so the next launch's ticket_last counts
+// from 0.  The tick still consumed its step on the device (the window slot, the tick number);
+// the Python controller refuses further ticks until it is rebuilt (LLAMPC.tick).
+static int ctl_recover(llampc_ctl* c) {
+  HIP_TRY(hipStreamSynchronize(c->b->stream));
+  HIP_TRY(hipMemsetAsync(c->d_tickets, 0, sizeof(unsigned), c->b->stream));
+  HIP_TRY(hipStreamSynchronize(c->b->stream));
+  return LLAMPC_OK;
+}
+
 extern "C" {
 
 int llampc_ctl_destroy(llampc_ctl* c) {
@@ -1459,12 +1505,15 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
     if ((++spins & 0xFFF) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
       HIP_TRY(hipStreamSynchronize(c->b->stream));
       if (__atomic_load_n(c->h_tag, __ATOMIC_ACQUIRE) == c->pend_seq) break;
+      (void)ctl_recover(c);
       return fail(LLAMPC_E_DEVICE, "controller tick %llu: completion tag never arrived", (unsigned long long)c->pend_seq);
     }
   }
   std::memcpy(out, const_cast<const llampc_ctl_out*>(c->h_out), sizeof(llampc_ctl_out));
-  if (out->plan.status)
+  if (out->plan.status) {
+    (void)ctl_recover(c);
     return fail(LLAMPC_E_DEVICE, "controller tick record status %d (an in-launch wait timed out)", out->plan.status);
+  }
   c->hint_p0 = out->projidx;             // the state this tick left (ctl_complete writes both)
   c->hint_mu = out->mu_pred;
   c->hint_ok = true;
@@ -1607,8 +1656,14 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
       (rc = dev_alloc(&p->d_ticket, 4)))
     return cleanup(rc);
   {
+    // every round in one launch needs all samples / 64 blocks resident together (each waits
+    // for the others' rounds; one block per CU by its LDS request): not on a device, or a
+    // partition of one, with fewer CUs than blocks — then one launch per round
     const char* e = std::getenv("LLAMPC_NLP_ROUND_LAUNCHES");
-    p->per_round = !nlp_persistent(k.samples) || (e && e[0] == '1');
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device) != hipSuccess) cus = 0;
+    const bool resident = k.samples / 64 <= cus;
+    p->per_round = !nlp_persistent(k.samples) || !resident || (e && e[0] == '1');
   }
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(NLP staging) failed"));
@@ -1696,11 +1751,13 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
     a.rounds = 1;
     for (int it = 0; it < k.iters; ++it) {
       a.it = it;
+      TimedLaunch tl(b, 0, s);           // llampc_bank_timing on the solver's bank: per round
       HIP_TRY(launch_nlp(a, s));
     }
   } else {                              // every round in one launch (nlp.hpp nlp_persistent)
     a.it = 0;
     a.rounds = k.iters;
+    TimedLaunch tl(b, 0, s);             // llampc_bank_timing on the solver's bank: per solve
     HIP_TRY(launch_nlp(a, s));
   }
   // the last round's completion writes the result into pinned memory and then the tag
@@ -1712,6 +1769,12 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
     if ((++spins & 0xFFF) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
       HIP_TRY(hipStreamSynchronize(s));
       if (__atomic_load_n(p->h_tag, __ATOMIC_ACQUIRE) == want) break;
+      // the launch has ended (its blocks give up a round wait after kNlpRoundWait): the next
+      // solve must not meet this one's state — a new call number (so stale round tags never
+      // match) and a zero ticket / round tag (ticket_last would fire early on a stale count)
+      p->calls++;
+      HIP_TRY(hipMemsetAsync(p->d_ticket, 0, 4 * sizeof(unsigned), s));
+      HIP_TRY(hipStreamSynchronize(s));
       return fail(LLAMPC_E_DEVICE, "NLP solve %llu: completion tag never arrived", (unsigned long long)want);
     }
   }

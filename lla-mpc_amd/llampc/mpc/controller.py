@@ -341,6 +341,7 @@ class LLAMPC:
         self.current_model = 0          # rt.py:264
         self.projidx = 0
         self.t = 0
+        self.failed = None              # the tick that failed on the device (device mode), if any
         self.x_prev = None
         self.u_prev = None
         self.u_seq = None
@@ -423,16 +424,35 @@ class LLAMPC:
         controllers of several banks (e.g. two tracks) run concurrently; tick_end() completes it."""
         if self.mode != "device":
             raise nat.NativeError("tick_begin/tick_end need mode='device'")
+        self._usable()
         self._pending_x = x = np.array(x_t, dtype=np.float64)
         self._ctl.tick_async(x)
 
     def tick_end(self) -> PlanResult:
-        return self._finish_device(self._ctl.wait(), self._pending_x)
+        return self._guarded(lambda: self._finish_device(self._ctl.wait(), self._pending_x))
 
     def _tick_device(self, x_t) -> PlanResult:
         """ONE launch (llampc_ctl_tick): the device computes the reference, the candidates, the
         look-back, the look-ahead of the selected and top-K models, mu-hat and its state."""
-        return self._finish_device(self._ctl.tick(x_t), x_t)
+        self._usable()
+        return self._guarded(lambda: self._finish_device(self._ctl.tick(x_t), x_t))
+
+    def _usable(self):
+        if self.failed is not None:
+            raise nat.NativeError(f"controller unusable after the failed tick {self.failed}: a failed tick still "
+                                  "consumed its step on the device (window slot, tick number); rebuild the "
+                                  "bank and the controller")
+
+    def _guarded(self, fn):
+        """A device tick that raises (a wait that timed out, a record with status != 0) has still
+        advanced the device controller's tick and window: the host mirror records the step
+        (t advances) and the controller refuses further ticks."""
+        try:
+            return fn()
+        except Exception:
+            self.failed = self.t
+            self.t += 1
+            raise
 
     def _finish_device(self, o, x_t) -> CtlResult:
         res = CtlResult(o, self.H)

@@ -31,6 +31,10 @@ def raceline_start(x0, track, projidx):
     rl = track.raceline
     _, idx = track.project_fast(x0[0], x0[1], rl[:, projidx:projidx + 10])
     projidx = idx + projidx
+    table = getattr(track, "ctl_table", None)
+    if table is not None:                   # the cached prefix table: the same sum, O(1) per call
+        prefix = table()[1]
+        return float(prefix[min(projidx, prefix.shape[0] - 1)]), projidx
     seg = rl[:, :projidx + 2]
     return float(np.sum(np.linalg.norm(np.diff(seg), 2, axis=0))), projidx
 

@@ -20,7 +20,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
-REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+_ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
+REF = _ARGS[0] if _ARGS else "/root/reference"
 
 sys.dont_write_bytecode = True
 sys.path.insert(0, REF)
@@ -65,7 +66,56 @@ def batch_model(shared, params6):
                    Cr2=shared.Cr2, input_acc=False)
 
 
+def config1(states, inputs, first):
+    """BASELINE config 1 exactly as SURVEY.md §8(d) states it, computed by the reference:
+    ETHZ, N = 100 (rt.py bank, seed 0), H = 20, C = 1, W = 10, K = 10, nominal friction.
+    Look-back over DYN states[:, 490:501] / inputs[:, 490:500] (evaluate_models_vectorized +
+    the rt.py:347-366 window logic), x0 = states[:, 500], U = inputs[:, 500:520],
+    xref = ConstantSpeed(x0, vx0, ETHZ, 20, 0.02, projidx, curr_mu=0.9092, scale=0.9) with
+    projidx the raceline point nearest x0 minus 2 (the reference's warm-start hint; "auto"),
+    then H x _integrate_batch of every model under U (rk6.py:50-68 via model.py:32-40)."""
+    params = ORCA(control='pwm')
+    nominal = Dynamic(**params)
+    rt_sigma = {"Br": 0.2, "Cr": 0.1, "Dr": 0.5, "Bf": 0.2, "Cf": 0.1, "Df": 0.5}
+    N, H = 100, 20
+    models, bank = ref_bank(N, 0, rt_sigma)
+    p6 = tuple(bank)
+    i0 = 490 - first
+    s = states[:, i0:i0 + 11]
+    u = inputs[:, i0:i0 + 10]
+    win = np.zeros((N, W))
+    errs = []
+    for t in range(W):
+        pred = evaluate_models_vectorized(models, N, s[:, t], u[:, t], TS, p6)
+        e = np.mean((pred - s[0:4, t + 1]) ** 2, axis=1)
+        win = np.roll(win, -1, axis=1)
+        win[:, -1] = e
+        errs.append(e)
+    avg = np.mean(win, axis=1)
+    x0 = states[:, 500 - first]
+    U = inputs[:, 500 - first:520 - first].T[None].copy()
+    tr = ETHZ(reference='optimal', longer=True)
+    rl = np.asarray(tr.raceline)
+    near = int(np.argmin(np.hypot(rl[0] - x0[0], rl[1] - x0[1])))
+    pin = max(near - 2, 0)
+    xref, pout, vr = ConstantSpeed(x0=x0[:2], v0=x0[3], track=tr, N=H, Ts=TS, projidx=pin, scale=0.9, curr_mu=0.9092)
+    bm = batch_model(nominal, p6)
+    xb = np.tile(x0, (N, 1))
+    traj = [xb]
+    for k in range(H):
+        xb = bm._integrate_batch(xb, np.tile(U[0, k], (N, 1)), 0, TS)
+        traj.append(xb)
+    save("config1.npz", bank=bank, seed=np.array(0), states=s, inputs=u, x0=x0, U=U, uprev=u[:, -1].copy(),
+         xref=xref, projidx_in=np.array(pin), projidx_out=np.array(pout), vr=np.array(vr), mu=np.array(0.9092),
+         scale=np.array(0.9), errors=np.array(errs), window_mean=avg, best=np.array(np.argmin(avg)),
+         topk=avg.argsort()[:K], traj=np.array(traj), W=np.array(W), K=np.array(K), H=np.array(H))
+
+
 def main():
+    if "--only-config1" in sys.argv:
+        dyn = np.load(os.path.join(REF, "llampc/data/DYN-GPMPC-NOCONS-with_var_speedsETHZ.npz"))
+        config1(np.asarray(dyn["states"][:6], dtype=np.float64), np.asarray(dyn["inputs"], dtype=np.float64), 0)
+        return
     params = ORCA(control='pwm')
     nominal = Dynamic(**params)
     rt_sigma = {"Br": 0.2, "Cr": 0.1, "Dr": 0.5, "Bf": 0.2, "Cf": 0.1, "Df": 0.5}
@@ -101,6 +151,7 @@ def main():
     inputs = np.asarray(dyn["inputs"], dtype=np.float64)
     lo, hi = 470, 620
     save("dyn_slice.npz", states=states[:, lo:hi + 1], inputs=inputs[:, lo:hi], first_index=np.array(lo))
+    config1(states, inputs, 0)
 
     # ---------------- bank generation: rt.py loop vs randn(N,6) ----------------
     bank_models, bank = ref_bank(1000, 0, rt_sigma)

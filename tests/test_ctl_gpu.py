@@ -99,13 +99,17 @@ def test_ctl_reference_fast_starts_and_lap_end(nat, name):
             ctl.close()
 
 
-@pytest.mark.parametrize("N,C,H,W,K,name,ticks,lap", [
-    (200, 8, 20, 4, 10, "ETHZ", 14, None),
-    (6, 8, 20, 4, 10, "ETHZ", 10, None),            # N < K: top-K padded with -1, never in mu-hat
-    (1000, 64, 40, 10, 10, "ETHZMobil", 16, None),  # the bench shape of the controller (C = 64, H = 40)
-    (200, 8, 20, 4, 10, "ETHZ", 16, 3),             # lap_projidx = 3: the lap wrap (rt.py:287-296) every few ticks
+@pytest.mark.parametrize("N,C,H,W,K,name,ticks,lap,seed", [
+    (200, 8, 20, 4, 10, "ETHZ", 14, None, 21),
+    (6, 8, 20, 4, 10, "ETHZ", 10, None, 21),            # N < K: top-K padded with -1, never in mu-hat
+    (1000, 64, 40, 10, 10, "ETHZMobil", 16, None, 21),  # C = 64, H = 40 at a small bank
+    (200, 8, 20, 4, 10, "ETHZ", 16, 3, 21),             # lap_projidx = 3: the lap wrap (rt.py:287-296) every few ticks
+    # the bench's controller shape exactly (bench.py controller_ticks): N = 10^4 per track (40
+    # look-back blocks feed lb_final<true>), C = 64, H = 40, W = K = 10, the bench's seeds
+    (10000, 64, 40, 10, 10, "ETHZ", 15, None, 0),
+    (10000, 64, 40, 10, 10, "ETHZMobil", 15, None, 1),
 ])
-def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks, lap):
+def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks, lap, seed):
     """LLAMPC.tick in device mode (ONE launch per tick) against ControllerOracle in closed
     loop with the RK6 plant (friction dropping 1/260 per tick): every tick's reference (and the
     host ConstantSpeed on the same mu / scale / projidx), candidates, look-back top-K,
@@ -116,7 +120,7 @@ def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks, lap):
     tr, ref = tracks(name)
     if lap is not None:
         tr.lap_projidx = lap
-    bank_p = generate_bank(N, seed=21)
+    bank_p = generate_bank(N, seed=seed)
     orc = O.ControllerOracle(shared(), bank_p, ref, tr.lap_projidx, H=H, C=C, K=K, W=W, Ts=TS)
     wraps = 0
     plant = O.Vehicle.from_params(O.orca_params())

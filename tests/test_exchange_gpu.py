@@ -6,7 +6,7 @@ push over IPC-mapped memory, poll, merge — one kernel), RCCL issued natively
 (llampc_exchange_device on the tick's stream) and c10d.
 No per-tick synchronisation: the stream order alone must make the records right."""
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -14,12 +14,6 @@ import pytest
 from conftest import golden
 
 pytestmark = pytest.mark.gpu
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 @pytest.fixture(scope="module")
@@ -31,10 +25,11 @@ def nccl_world1():
     if _native.device_count() < 1:
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X")
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
-                            device_id=torch.device("cuda", 0))
-    yield
-    dist.destroy_process_group()
+    with tempfile.TemporaryDirectory(prefix="llampc_rdzv_") as tmp:   # a FileStore: no port to race for
+        dist.init_process_group("nccl", init_method=f"file://{os.path.join(tmp, 'store')}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        yield
+        dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("transport", ["peer", "peer-ticket", "peer-split", "rccl", "c10d"])

@@ -536,10 +536,12 @@ def test_llampc_controller_closed_loop_vs_oracle(nat, monkeypatch, N):
             x_prev, u_prev, x = x, u.copy(), xn[:, -1]
 
 
-@pytest.mark.parametrize("N,H,track", [(10000, 20, "ETHZ"), (10000, 40, "ETHZMobil"), (80000, 20, "ETHZ")])
+@pytest.mark.parametrize("N,H,track", [(10000, 20, "ETHZ"), (80000, 20, "ETHZ")])
 def test_baseline_sizes_properties(nat, N, H, track):
-    """BASELINE.json sizes: errors/costs vs the oracle on every model (numpy handles these
-    sizes in seconds), selection consistent with the returned arrays, top-K sorted."""
+    """BASELINE.json sizes on the DYN recording (ETHZ: configs 2 and 4's track): errors/costs vs
+    the oracle on every model (numpy handles these sizes in seconds), selection consistent with
+    the returned arrays, top-K sorted.  Config 3 (ETHZMobil) runs on its own synthetic Mobil
+    states in tests/test_configs_gpu.py."""
     from llampc.mpc import ModelBank, generate_bank, plan
     from llampc.mpc.planner import ConstantSpeed
     from llampc.tracks import ETHZ, ETHZMobil

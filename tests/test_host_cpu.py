@@ -415,7 +415,8 @@ def test_plan_in_builder_pointers_and_fields():
 
 def test_bench_spawn_ranks_environment_and_failure():
     """bench.py's self-spawn of `--gpus N` (no launcher): every rank gets torchrun's
-    environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, one shared free port),
+    environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1) and one shared FileStore
+    path for the rendezvous (LLAMPC_INIT_FILE: no port to race for),
     the parent's status is 0 when all ranks succeed, and when one rank fails the others are
     stopped and its exit status is returned (CPU only: the ranks are stand-in scripts)."""
     import importlib.util
@@ -426,7 +427,7 @@ def test_bench_spawn_ranks_environment_and_failure():
     spec.loader.exec_module(bench)
     with tempfile.TemporaryDirectory() as tmp:
         ok = ("import os, sys; open(os.path.join(%r, os.environ['RANK']), 'w').write("
-              "' '.join(os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')))") % tmp
+              "' '.join(os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'LLAMPC_INIT_FILE')))") % tmp
         assert bench.spawn_ranks(3, [sys.executable, "-c", ok]) == 0
         got = [open(os.path.join(tmp, str(r))).read().split() for r in range(3)]
         assert [g[:4] for g in got] == [[str(r), str(r), "3", "127.0.0.1"] for r in range(3)]

@@ -184,3 +184,32 @@ def test_cost_and_feasibility_sanity():
     assert list(ok) == [True, True]
     U[1, 1, 1] = 0.5
     assert list(O.candidates_feasible(U, np.zeros(2), [-0.1, -0.35], [1.0, 0.35], 5.0, 0.02)) == [True, False]
+
+
+def test_config1_plan_cpu_matches_reference():
+    """BASELINE config 1 exactly as SURVEY.md §8(d) states it (tests/golden/config1.npz, written
+    by the reference: N = 100, DYN states[:, 490:501], U = inputs[:, 500:520], ConstantSpeed with
+    mu = 0.9092, scale = 0.9): the oracle's bank, look-back window / argmin / top-K, H-step RK4
+    rollout (bitwise) and its ConstantSpeed (1e-12: banded vs dense spline solve)."""
+    g = golden("config1.npz")
+    N, W, K, H = g["bank"].shape[1], int(g["W"]), int(g["K"]), int(g["H"])
+    np.testing.assert_array_equal(O.make_bank(N, int(g["seed"])), g["bank"])
+    s, u = g["states"], g["inputs"]
+    win = O.LookbackWindow(N, W, K)
+    for t in range(W):
+        e = O.lookback_errors(O.evaluate_models_vectorized(shared(), tuple(g["bank"]), s[:, t], u[:, t], TS), s[:, t + 1])
+        np.testing.assert_array_equal(e, g["errors"][t])
+        full = win.push(e)
+    assert full and win.current == int(g["best"])
+    np.testing.assert_array_equal(win.avg, g["window_mean"])
+    np.testing.assert_array_equal(win.best_k, g["topk"])
+    traj = O.rollout_rk4(shared(), tuple(g["bank"]), g["x0"], g["U"], TS)
+    np.testing.assert_array_equal(traj, g["traj"])
+    import os
+    from conftest import REPO
+    td = np.load(os.path.join(REPO, "lla-mpc_amd", "llampc", "tracks", "data", "tracks.npz"))
+    ref = O.RacelineRef(td["ETHZ_x"], td["ETHZ_y"], td["ETHZ_speeds"], td["ETHZ_mus"])
+    xref, pidx = O.constant_speed(g["x0"][:2], g["x0"][3], ref, H, TS, int(g["projidx_in"]), scale=float(g["scale"]),
+                                  curr_mu=float(g["mu"]))[:2]
+    assert pidx == int(g["projidx_out"])
+    np.testing.assert_allclose(xref, g["xref"], rtol=1e-12, atol=1e-12)

@@ -4,8 +4,9 @@ them with the product's ``gather_merge_host`` (one all-gather) and must reproduc
 unsharded look-back selection / top-K / look-ahead best on every rank."""
 import datetime
 import os
-import socket
+import shutil
 import sys
+import tempfile
 
 import numpy as np
 import pytest
@@ -13,12 +14,6 @@ import pytest
 from conftest import REPO, PKG_ROOT, golden
 
 TS = 0.02
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _local_record(nat, p_all, lo, hi, states, inputs, W, K, U, xref, uprev):
@@ -56,7 +51,7 @@ def _local_record(nat, p_all, lo, hi, states, inputs, W, K, U, xref, uprev):
     return o, win, cost
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, store, q):
     try:
         for pth in (REPO, PKG_ROOT):
             sys.path.insert(0, pth)
@@ -64,7 +59,7 @@ def _worker(rank, world, port, q):
         from llampc import _native as nat
         from llampc.mpc import generate_bank, shard_range
         from llampc.mpc.sharded import gather_merge_host
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+        dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=120))
         d = golden("dyn_slice.npz")
         N, W, K, H, C = 601, 10, 10, 20, 3
@@ -90,33 +85,36 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc() + repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_merge_gloo(world):
+def run_gloo_ranks(target, world, timeout=240):
+    """``target(rank, world, store, q)`` in `world` spawned processes meeting at a FileStore in a
+    private temporary directory (no TCP port to race for); each puts (rank, "ok" | error) on q.
+    Every rank process is reaped whatever happens."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    # a rendezvous port taken between _free_port and the store's bind (EADDRINUSE) is retried
-    # on a new one; the rank processes are reaped whatever happens
-    for attempt in range(3):
-        q = ctx.Queue()
-        port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    tmp = tempfile.mkdtemp(prefix="llampc_rdzv_")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, os.path.join(tmp, "store"), q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = []
+    try:
+        for _ in procs:
+            res.append(q.get(timeout=timeout))
+            if res[-1][1] != "ok":
+                break
+    finally:
+        failed = any(msg != "ok" for _, msg in res)
         for pr in procs:
-            pr.start()
-        res = []
-        try:
-            for _ in procs:
-                res.append(q.get(timeout=240))
-                if res[-1][1] != "ok":
-                    break
-        finally:
-            failed = any(msg != "ok" for _, msg in res)
-            for pr in procs:
-                pr.join(timeout=1 if failed else 60)
-                if pr.is_alive():
-                    pr.terminate()
-                    pr.join(timeout=10)
-        bad = [(rank, msg) for rank, msg in res if msg != "ok"]
-        if not bad:
-            break
-        if "EADDRINUSE" not in bad[0][1] or attempt == 2:
-            raise AssertionError(f"rank {bad[0][0]}: {bad[0][1]}")
+            pr.join(timeout=1 if failed else 60)
+            if pr.is_alive():
+                pr.terminate()
+                pr.join(timeout=10)
+        shutil.rmtree(tmp, ignore_errors=True)
+    bad = [(rank, msg) for rank, msg in res if msg != "ok"]
+    if bad:
+        raise AssertionError(f"rank {bad[0][0]}: {bad[0][1]}")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_merge_gloo(world):
+    run_gloo_ranks(_worker, world)

@@ -9,8 +9,9 @@ merge_kernel).  Every rank's merged record, tick after tick, must equal the unsh
 the whole bank on the same inputs."""
 import datetime
 import os
-import socket
+import shutil
 import sys
+import tempfile
 
 import numpy as np
 import pytest
@@ -28,12 +29,6 @@ def n_models(world, C=3):
     return 6001 if C == 64 else (80000 if world == 8 else 3001)
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _ticks(C=3):
     d = golden("dyn_slice.npz")
     s, u = d["states"], d["inputs"]
@@ -46,7 +41,7 @@ def _ticks(C=3):
     return out
 
 
-def _worker(rank, world, port, q, transport, C=3):
+def _worker(rank, world, store, q, transport, C=3):
     try:
         if transport.endswith("-wq8"):         # the 8-wave work-queue layout at this size
             os.environ["LLAMPC_WQ_WAVES"] = "8"
@@ -67,7 +62,7 @@ def _worker(rank, world, port, q, transport, C=3):
         from llampc.mpc import generate_bank
         from llampc.mpc.sharded import ShardedBank, _bytes_of
         torch.cuda.set_device(0)
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+        dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=60))
         sb = ShardedBank(generate_bank(n_models(world, C), seed=12), rank, world, 0, W=W)
         assert sb.transport == transport, (sb.transport, transport)
@@ -91,37 +86,36 @@ def _worker(rank, world, port, q, transport, C=3):
 
 
 def _run_ranks(world, transport, C):
-    """The ranks in spawned processes; a rendezvous port taken by another process between
-    _free_port and the store's bind (EADDRINUSE) is retried on a new port, and every rank
+    """The ranks in spawned processes, meeting at a FileStore in a private temporary directory
+    (no TCP port: nothing another process can take between a probe and the bind); every rank
     process is reaped whatever happens (a rank left waiting on its rendezvous would keep the
     test runner from exiting)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
-    for attempt in range(3):
-        q = ctx.Queue()
-        port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, q, transport, C)) for r in range(world)]
+    tmp = tempfile.mkdtemp(prefix="llampc_rdzv_")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, os.path.join(tmp, "store"), q, transport, C))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got, errs = {}, []
+    try:
+        for _ in range(world):
+            rank, recs, err = q.get(timeout=150)
+            if err is not None:
+                errs.append((rank, err))
+                break
+            got[rank] = recs
+    finally:
         for p in procs:
-            p.start()
-        got, errs = {}, []
-        try:
-            for _ in range(world):
-                rank, recs, err = q.get(timeout=150)
-                if err is not None:
-                    errs.append((rank, err))
-                    break
-                got[rank] = recs
-        finally:
-            for p in procs:
-                p.join(timeout=30 if not errs else 1)
-                if p.is_alive():
-                    p.terminate()
-                    p.join(timeout=10)
-        if not errs:
-            return got
-        if "EADDRINUSE" not in errs[0][1] or attempt == 2:
-            raise AssertionError(f"rank {errs[0][0]}:\n{errs[0][1]}")
-    raise AssertionError("unreachable")
+            p.join(timeout=30 if not errs else 1)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+        shutil.rmtree(tmp, ignore_errors=True)
+    if errs:
+        raise AssertionError(f"rank {errs[0][0]}:\n{errs[0][1]}")
+    return got
 
 
 CASES = ([(w, "peer", 3) for w in (2, 3, 4, 8)] + [(w, "host", 3) for w in (2, 3, 8)] +

@@ -27,6 +27,7 @@ plant = Dynamic(**ORCA(), device=0)
 setups = []
 for seed, tr in ((0, ETHZ('optimal', True)), (1, ETHZMobil('optimal', True))):
     b = ModelBank(generate_bank(N, seed=seed), W=10, device=0)
+    b.set_concurrency(2)            # the two controllers' banks: a hardware queue each
     ctl = LLAMPC(b, tr, H=40, C=64, K=10, mode="device")
     if tr.name == "ETHZ":
         x = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))["states"][:, 0].copy()

@@ -2,6 +2,7 @@
 import csv, glob, os, sys
 from collections import defaultdict
 root = sys.argv[1]
+pats = sys.argv[2].split(",") if len(sys.argv) > 2 else ["plan_kernel", "merge"]   # kernel-name filters
 vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
@@ -13,7 +14,7 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
             continue
         vals[k][(name, r.get("Dispatch_Id"))].append(v)
 for k, d in vals.items():
-    if "plan_kernel" not in k and "merge" not in k:
+    if not any(p in k for p in pats):
         continue
     per = defaultdict(list)
     for (name, disp), v in d.items():
