@@ -360,6 +360,25 @@ int llampc_ctl_reference(llampc_ctl* ctl, const double* x0, double v0, int32_t H
                          double scale, double* xref, int32_t* projidx_out, double* vr);
 /* The last tick's reference xref [2][H+1] and candidates U [C][H][2] (cfg.debug_inputs = 1). */
 int llampc_ctl_inputs(llampc_ctl* ctl, double* xref, double* U);
+/* The controller over a bank SHARDED across ranks (BASELINE config 5: one process per GPU, each
+ * rank's controller on its contiguous shard; replaces the single-process loop rt.py:269-366 with
+ * its look-back over the whole bank).  Call on every rank before the first tick: `mb` is this
+ * rank's mailbox with every peer open (llampc_mailbox_*), `gparams` [6][n_global] the whole
+ * bank (rows Bf, Cf, Df, Br, Cr, Dr), copied to the device.  Then on every tick with a full
+ * window the look-back's completing block pushes the shard's top-K and argmin (window mean,
+ * global index) into every peer's mailbox, merges the `world` records (llampc_ctl_merge's order)
+ * and publishes the merged selection: every rank rolls out the same K + 1 models from the global
+ * table, so every rank's record and controller state equal the unsharded controller's.  All
+ * ranks must tick the same number of times (the mailbox's tick number is the tag); the tick's
+ * own launch does the exchange (no second kernel).  world <= 16, n_global < 2^32 - 1. */
+int llampc_ctl_set_exchange(llampc_ctl* ctl, llampc_mailbox* mb, const double* gparams, int64_t n_global);
+/* The sharded controller's merge on the host (the device exchange runs the same functions,
+ * csrc/ctl.hpp): G records of K + 1 entries each — vals / gids [G][K+1], entries 0..K-1 the
+ * shard's sorted top-K (gid -1: none), entry K its argmin — -> the merged top-K (argsort order
+ * of rt.py:360: NaN last, ties to the lower global index; -1 padded) and argmin (rt.py:359;
+ * NaN-first under LLAMPC_NAN_FIRST; -1 if none). */
+int llampc_ctl_merge(const double* vals, const int64_t* gids, int32_t G, int32_t K, int32_t nan_policy,
+                     int64_t* topk, double* topk_val, int64_t* best, double* best_val);
 int llampc_ctl_destroy(llampc_ctl* ctl);
 
 /* ---- setupNLP.solve drop-in ------------------------------------------------------ */

@@ -1231,6 +1231,10 @@ struct llampc_ctl {
   int64_t t = 0;
   bool pending = false;
   uint64_t pend_seq = 0;
+  // sharded (llampc_ctl_set_exchange): the peers' mailboxes and the replicated global table
+  llampc_mailbox* mb = nullptr;
+  double* d_gparams = nullptr;           // [6][n_global]
+  int64_t n_global = 0;
   std::mutex mu;
 };
 
@@ -1252,7 +1256,8 @@ int llampc_ctl_destroy(llampc_ctl* c) {
   {
     DeviceGuard g(c->b ? c->b->device : 0);
     if (c->b && c->b->stream) (void)hipStreamSynchronize(c->b->stream);
-    void* d[] = {c->d_st, c->d_pts, c->d_sel_tag, c->d_slot_tag, c->d_tickets, c->d_dbg, c->d_znoise, c->d_ztag};
+    void* d[] = {c->d_st, c->d_pts, c->d_sel_tag, c->d_slot_tag, c->d_tickets, c->d_dbg, c->d_znoise, c->d_ztag,
+                 c->d_gparams};
     for (void* p : d)
       if (p) (void)hipFree(p);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1466,12 +1471,39 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   L.K = k.K;
   L.nb_lb = L.fin.nb_lb;
   L.nb_la = (L.nslots + L.mpb - 1) / L.mpb;
+  // sharded: the exchange runs on every tick whose window is full (the same ticks on every
+  // rank); the selection is global, the look-ahead reads the replicated global table
+  L.sel_goff = b->goff;
+  std::unique_lock<std::mutex> lm;
+  uint32_t px_seq = 0;
+  if (c->mb) {
+    llampc_mailbox* mb = c->mb;
+    lm = std::unique_lock<std::mutex>(mb->mu);
+    if (!mb->box_synced) {
+      HIP_TRY(hipMemcpy(mb->d_box, mb->box, kPeerMax * sizeof(uint64_t*), hipMemcpyHostToDevice));
+      mb->box_synced = true;
+    }
+    L.la.params = c->d_gparams;
+    L.la.n = c->n_global;
+    L.la.goff = 0;
+    L.sel_goff = 0;
+    if (full) {
+      px_seq = next_seq(mb->seq);
+      L.px_box = mb->d_box;
+      L.px_G = mb->world;
+      L.px_rank = mb->rank;
+      L.px_seq = px_seq;
+      L.px_bound = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((mb->bound + 0xFFFF) >> 16, 1), UINT32_MAX);
+      L.poll = std::max(L.poll, L.px_bound);   // the look-ahead blocks wait for the merged selection
+    }
+  }
   // the look-ahead blocks stage every (candidate, step)'s input terms when they fit in LDS
   // (CtlLaunch.s4; LLAMPC_CTL_NO_STAGE=1 at create: never, for A/B runs)
   size_t poll_s4 = 0;
-  const size_t lds_s4 = ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &poll_s4, true);
+  const size_t lds_s4 = ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &poll_s4, true, L.px_G);
   L.s4 = (!c->no_stage && lds_s4 <= 160 * 1024) ? 1 : 0;
-  size_t lds = L.s4 ? lds_s4 : ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &L.poll_off);
+  size_t lds = L.s4 ? lds_s4 : ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &L.poll_off, false, L.px_G);
+  if (lds > 160 * 1024) return fail(LLAMPC_E_ARG, "controller tick needs %zu B of LDS (> 160 KiB)", lds);
   if (L.s4) L.poll_off = poll_s4;
   lds = std::max<size_t>(lds, 82 * 1024); // one block per CU, as the plan launch (sc1 hand-offs)
   {
@@ -1480,6 +1512,7 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   }
   c->hseq = hs;
   c->seq = seq;
+  if (L.px_G) c->mb->seq = px_seq;      // committed after the launch was enqueued (next_seq)
   c->t = t + 1;
   c->pending = true;
   c->pend_seq = hs;
@@ -1569,6 +1602,64 @@ int llampc_ctl_reference(llampc_ctl* c, const double* x0, double v0, int32_t H, 
   std::memcpy(xref, h.data(), 2 * (size_t)(H + 1) * sizeof(double));
   if (projidx_out) *projidx_out = (int32_t)h[2 * (H + 1)];
   if (vr) *vr = h[2 * (H + 1) + 1];
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_set_exchange(llampc_ctl* c, llampc_mailbox* mb, const double* gparams, int64_t n_global) {
+  if (!c || !mb || !gparams) return fail(LLAMPC_E_ARG, "NULL argument");
+  llampc_bank* b = c->b;
+  if (mb->device != b->device) return fail(LLAMPC_E_ARG, "mailbox on device %d, bank on %d", mb->device, b->device);
+  if (mb->world > kCtlPxMax) return fail(LLAMPC_E_ARG, "world %d > %d (the exchange's LDS)", mb->world, kCtlPxMax);
+  if (n_global < b->goff + b->n || n_global >= (int64_t)0xFFFFFFFFll)
+    return fail(LLAMPC_E_ARG, "n_global=%lld: must hold this shard [%lld, %lld) and be < 2^32 - 1", (long long)n_global,
+                (long long)b->goff, (long long)(b->goff + b->n));
+  for (int g = 0; g < mb->world; ++g)
+    if (!mb->box[g]) return fail(LLAMPC_E_STATE, "mailbox of peer %d not open", g);
+  std::lock_guard<std::mutex> lc(c->mu);
+  if (c->pending) return fail(LLAMPC_E_STATE, "a controller tick is outstanding");
+  if (c->t != 0) return fail(LLAMPC_E_STATE, "set the exchange before the first tick");
+  DeviceGuard g(b->device);
+  double* d = nullptr;
+  if (int rc = dev_alloc(&d, 6 * (size_t)n_global)) return rc;
+  if (hipMemcpy(d, gparams, 6 * (size_t)n_global * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return fail(LLAMPC_E_HIP, "global parameter table upload failed");
+  }
+  if (c->d_gparams) (void)hipFree(c->d_gparams);
+  c->d_gparams = d;
+  c->n_global = n_global;
+  c->mb = mb;
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_merge(const double* vals, const int64_t* gids, int32_t G, int32_t K, int32_t nan_policy,
+                     int64_t* topk, double* topk_val, int64_t* best, double* best_val) {
+  if (!vals || !gids || !topk || !topk_val || !best || !best_val) return fail(LLAMPC_E_ARG, "NULL argument");
+  if (G < 1 || G > kCtlPxMax || K < 1 || K > LLAMPC_KMAX) return fail(LLAMPC_E_ARG, "G=%d (1..%d) K=%d", G, kCtlPxMax, K);
+  const int M = G * K;
+  std::vector<uint64_t> key(M), id(M);
+  for (int e = 0; e < M; ++e) {
+    const int g = e / K, j = e - g * K;
+    ctl_entry_order(vals[g * (K + 1) + j], gids[g * (K + 1) + j], e, key[e], id[e]);
+  }
+  for (int k = 0; k < K; ++k) {
+    topk[k] = -1;
+    topk_val[k] = std::nan("");
+  }
+  for (int e = 0; e < M; ++e) {
+    const int r = ctl_merge_rank([&](int j) { return key[j]; }, [&](int j) { return id[j]; }, M, e);
+    if (r < K) {
+      const int g = e / K, j = e - g * K;
+      const int64_t gid = gids[g * (K + 1) + j];
+      topk[r] = gid < 0 ? -1 : gid;
+      topk_val[r] = gid < 0 ? std::nan("") : vals[g * (K + 1) + j];
+    }
+  }
+  ctl_merge_argmin([&](int g, double& v, int64_t& i) {
+                     v = vals[g * (K + 1) + K];
+                     i = gids[g * (K + 1) + K];
+                   },
+                   G, nan_policy == LLAMPC_NAN_FIRST, *best_val, *best);
   return LLAMPC_OK;
 }
 

@@ -229,7 +229,7 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   // the record's scalar kernel arguments, loaded (and kept) before the poll: the tail used
   // to wait for them one by one after it
   int32_t a_wc = c.fin.window_count, a_full = c.fin.full, a_K = c.K, a_warm = c.warm, a_lap = c.lap_projidx;
-  int64_t a_goff = c.fin.goff, a_tick = (int64_t)c.tick;
+  int64_t a_goff = c.sel_goff, a_tick = (int64_t)c.tick;
   double a_scale = c.use_mu ? c.v_factor : c.scale_fixed;
   asm volatile("" : "+s"(a_wc), "+s"(a_full), "+s"(a_K), "+s"(a_warm), "+s"(a_lap));
   asm volatile("" : "+s"(a_goff), "+s"(a_tick), "+s"(a_scale));
@@ -297,7 +297,7 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     int64_t lai = valid ? (a_goff + (int64_t)cs.ids[q]) * C + pcand[q] : kNoIndex;
     wave_pick_nl64(lav, lai);
     const int nf = wave_sum(slot ? pnf[q] : 0);
-    int anyl = 0;
+    int anyl = *cs.xlate;                // the sharded exchange gave up on a peer
     for (int w = 0; w < kWaves; ++w) anyl |= late_w[w];
     const int64_t sel = warm ? cur_model : a_goff + (int64_t)cs.ids[a_K];
     const double dr = pmu[0], df = pmu[1], mu_pred = pmu[2];
@@ -348,6 +348,159 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   __syncthreads();
   CTL_STAMP(blockIdx.x, 9);
   if (tid == 0) __hip_atomic_store(c.host_tag, c.host_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ------------------------------------------------------------------------------------
+// The sharded controller's exchange (ctl.hpp "sharded controller"; BASELINE config 5): run by
+// the look-back ticket winner after lb_final<2> left this shard's top-K and argmin in cs.ids /
+// cs.xv.  (a) The record — K + 1 entries of (window mean, global index) as 32-bit words — goes
+// to LDS and, tagged with the mailbox's tick number, into slot [seq & 1][rank] of every peer's
+// mailbox (system-scope stores over xGMI; the slot-reuse argument is peer_exchange_kernel's);
+// (b) this rank's mailbox is polled for the G - 1 peer records (every thread issues all of its
+// loads before checking any); (c) the merge: each top-K entry's rank among the G K gathered
+// ones (ctl_merge_rank), the argmin over the G argmins (ctl_merge_argmin); (d) the MERGED
+// selection is published for the look-ahead blocks (global indices: they roll the models out
+// from the replicated global parameter table) and (e) the record's look-back fields and the
+// top-K Dr / Df for mu-hat are written.  A peer that never arrives (past px_bound): this
+// shard's own selection is used and the record's status says so.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void ctl_exchange(const CtlLaunch& c, unsigned char* smem, const CtlSel& cs) {
+  const int tid = threadIdx.x;
+  const int G = c.px_G, rank = c.px_rank, K = c.K, nw = ctl_rec_words(K), M = G * K;
+  const int64_t goff = c.fin.goff;
+  unsigned char* base = smem + kScratchBytes;            // lb_final's region (dead)
+  uint32_t* rec32 = reinterpret_cast<uint32_t*>(base);   // [G][nw]
+  uint64_t* ekey = reinterpret_cast<uint64_t*>(base + align16(4 * (size_t)G * nw));
+  uint64_t* eid = ekey + M;
+  int* top = reinterpret_cast<int*>(eid + M);            // [KMAX] entry of each merged rank
+  int* wlate = top + LLAMPC_KMAX;                        // [kWaves]
+  __syncthreads();                                       // lb_final's wave 0 wrote cs.ids / xv
+  // (a) this shard's record: to LDS and, tagged, to every peer (one (peer, word) per thread)
+  const size_t slot0 = (size_t)(c.px_seq & 1) * G * kRecWords;
+  const size_t mine = slot0 + (size_t)rank * kRecWords;
+  for (int p = tid; p < G * nw; p += kBlock) {
+    const int g = p / nw, w = p - g * nw, e = w >> 2;
+    const uint32_t l = cs.ids[e];
+    const uint64_t q = (w & 2) ? (uint64_t)(l == kNoLocal ? (int64_t)-1 : goff + (int64_t)l)
+                               : (uint64_t)__double_as_longlong(cs.xv[e]);
+    const uint32_t word = (w & 1) ? (uint32_t)q : (uint32_t)(q >> 32);
+    if (g == rank) rec32[(size_t)rank * nw + w] = word;
+    else __hip_atomic_store(c.px_box[g] + mine + w, tag_word(c.px_seq, word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // (b) the peers' records from this rank's mailbox
+  constexpr int kPer = (kCtlPxMax * ctl_rec_words(LLAMPC_KMAX) + kBlock - 1) / kBlock;
+  const uint64_t* own = c.px_box[rank] + slot0;
+  const int total = G * nw;
+  uint64_t need = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int e = tid + j * kBlock;
+    if (e < total && e / nw != rank) need |= 1ull << j;
+  }
+  const uint64_t bound = (uint64_t)c.px_bound << 16;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  int late = 0;
+  while (need) {
+    uint64_t v[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int e = ((need >> j) & 1) ? tid + j * kBlock : rank * nw;   // idle: own slot (never read back)
+      const int g = e / nw, w = e - g * nw;
+      v[j] = __hip_atomic_load(own + (size_t)g * kRecWords + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (((need >> j) & 1) && tag_ok(v[j], c.px_seq)) {
+        rec32[tid + j * kBlock] = (uint32_t)v[j];
+        need &= ~(1ull << j);
+      }
+    }
+    if (!need) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {
+      late = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  const int wl = __any(late);
+  if ((tid & 63) == 0) wlate[tid >> 6] = wl;
+  __syncthreads();
+  late = 0;
+  for (int w = 0; w < kWaves; ++w) late |= wlate[w];
+  auto ent_v = [&](int g, int j) {
+    const uint32_t* r = rec32 + (size_t)g * nw + 4 * j;
+    return __longlong_as_double((long long)join_words(r[0], r[1]));
+  };
+  auto ent_id = [&](int g, int j) {
+    const uint32_t* r = rec32 + (size_t)g * nw + 4 * j;
+    return (int64_t)join_words(r[2], r[3]);
+  };
+  // (c) the merge (block-uniform branch): every top-K entry's merged rank
+  if (!late) {
+    for (int e = tid; e < M; e += kBlock) {
+      const int g = e / K, j = e - g * K;
+      ctl_entry_order(ent_v(g, j), ent_id(g, j), e, ekey[e], eid[e]);
+    }
+    __syncthreads();
+    for (int e = tid; e < M; e += kBlock) {
+      const int r = ctl_merge_rank([&](int j) { return ekey[j]; }, [&](int j) { return eid[j]; }, M, e);
+      if (r < K) top[r] = e;
+    }
+  } else if (tid < K) {
+    top[tid] = rank * K + tid;                           // this shard's own lists
+  }
+  __syncthreads();
+  if (tid >= 64) return;                                 // one wave finishes (the caller re-converges)
+  const int lane = tid;
+  const int Gm = late ? 1 : G;                           // argmin over every shard, or this one
+  double bv;
+  int64_t bi;
+  ctl_merge_argmin([&](int g, double& v, int64_t& id) {
+                     const int gg = late ? rank : g;
+                     v = ent_v(gg, K);
+                     id = ent_id(gg, K);
+                   },
+                   Gm, c.fin.nan_first != 0, bv, bi);
+  double kv = __builtin_nan("");
+  int64_t kid = -1;
+  if (lane < K) {
+    const int e = top[lane], g = e / K, j = e - g * K;
+    kv = ent_v(g, j);
+    kid = ent_id(g, j);
+  }
+  // (d) the merged selection (global indices < 2^32 - 1: llampc_ctl_set_exchange checks)
+  const uint32_t kl = kid < 0 ? kNoLocal : (uint32_t)kid;
+  const uint32_t al = bi < 0 ? kNoLocal : (uint32_t)bi;
+  if (lane < K) {
+    cs.ids[lane] = kl;
+    st_wt(&cs.tag[lane], tag_word(cs.seq, kl));
+  }
+  if (lane == 0) {
+    cs.ids[K] = al;
+    st_wt(&cs.tag[K], tag_word(cs.seq, al));
+    *cs.xlate = late;
+  }
+  // (e) the record's look-back half (pinned host memory, sc1 like lb_final's) and mu-hat's Dr / Df
+  const double* gp = c.la.params;                        // the replicated global table [6][n]
+  const int64_t gn = c.la.n;
+  llampc_plan_out* o = &c.out->plan;
+  const double nan = __builtin_nan("");
+  if (lane < LLAMPC_KMAX) {
+    const bool have = lane < K && kid >= 0;
+    const double df = have ? gp[2 * gn + kid] : nan, dr = have ? gp[5 * gn + kid] : nan;
+    st_wt(&o->topk[lane], have ? kid : (int64_t)-1);
+    st_wt(&o->topk_val[lane], have ? kv : nan);
+    st_wt(&o->topk_Df[lane], df);
+    st_wt(&o->topk_Dr[lane], dr);
+    if (lane < K) {
+      cs.dr[lane] = dr;
+      cs.df[lane] = df;
+    }
+  }
+  if (lane == 0) {
+    st_wt(&o->lb_best, bi);
+    st_wt(&o->lb_best_val, bi < 0 ? nan : bv);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -823,7 +976,9 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
 
 }  // namespace
 
-template <int LPM>
+// PX: the sharded controller (ctl_exchange after the shard's lb_final) — its own
+// instantiation, so the unsharded tick's code is unchanged
+template <int LPM, bool PX>
 __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Scratch sc(smem);
@@ -835,7 +990,9 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
   }
   unsigned char* pl = smem + c.poll_off;
   CtlSel cs{c.sel_tag, c.seq, reinterpret_cast<uint32_t*>(pl + 2048), reinterpret_cast<double*>(pl + 2304),
-            reinterpret_cast<double*>(pl + 2624)};
+            reinterpret_cast<double*>(pl + 2624), reinterpret_cast<double*>(pl + 3200),
+            reinterpret_cast<int32_t*>(pl + 3520)};
+  if (threadIdx.x == 0) *cs.xlate = 0;
   if (c.do_lb) {
     // x_now: this tick's x_t through LDS (pointing into the kernel argument itself would make
     // the compiler copy the whole argument to scratch)
@@ -849,7 +1006,12 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
     CTL_STAMP(blk, 6);
     if (!ticket_last(&c.tickets[0], (unsigned)c.nb_lb, flag)) return;
     if (c.full) {
-      lb_final<true>(c.fin, smem, &cs);
+      if constexpr (PX) {
+        lb_final<2>(c.fin, smem, &cs);  // this shard's lists, then the exchange and the merge
+        ctl_exchange(c, smem, cs);
+      } else {
+        lb_final<1>(c.fin, smem, &cs);
+      }
       __threadfence_system();           // the record's look-back half (pinned host memory)
     }
     CTL_STAMP(blk, 7);
@@ -894,29 +1056,36 @@ hipError_t launch_constant_speed(const CsLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4) {
+size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4, int px_G) {
   const CtlLds L = ctl_lds(H, C, n, s4);
   const size_t M = (size_t)nb_lb * K, Lb = nb_lb;    // lb_final's region (launch_plan's formula)
   const size_t lbf = kScratchBytes + 8 * (3 * M + Lb) + sizeof(Ent) * Lb * kWaves + 4 * (3 * M + Lb + LLAMPC_KMAX + 2) + 8 + 16;
   const size_t rank = kScratchBytes + (size_t)kWaves * kRankBytes + kBlockMergeBytes;
-  size_t off = std::max(L.end, std::max(lbf, rank));
+  const size_t px = px_G ? kScratchBytes + ctl_px_bytes(px_G, K) : 0;   // ctl_exchange's region
+  size_t off = std::max(std::max(L.end, px), std::max(lbf, rank));
   off = align16(off);
   *poll_off = off;
   return off + kCtlPollBytes;
 }
 
-hipError_t launch_ctl(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s) {
+template <bool PX>
+static void launch_ctl_px(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s) {
   const dim3 grid(c.nb_lb + c.nb_la), block(kBlock);
   if (lpm == 4) {
-    allow_lds(ctl_kernel<4>);
-    hipLaunchKernelGGL(ctl_kernel<4>, grid, block, lds, s, c);
+    allow_lds(ctl_kernel<4, PX>);
+    hipLaunchKernelGGL((ctl_kernel<4, PX>), grid, block, lds, s, c);
   } else if (lpm == 2) {
-    allow_lds(ctl_kernel<2>);
-    hipLaunchKernelGGL(ctl_kernel<2>, grid, block, lds, s, c);
+    allow_lds(ctl_kernel<2, PX>);
+    hipLaunchKernelGGL((ctl_kernel<2, PX>), grid, block, lds, s, c);
   } else {
-    allow_lds(ctl_kernel<1>);
-    hipLaunchKernelGGL(ctl_kernel<1>, grid, block, lds, s, c);
+    allow_lds(ctl_kernel<1, PX>);
+    hipLaunchKernelGGL((ctl_kernel<1, PX>), grid, block, lds, s, c);
   }
+}
+
+hipError_t launch_ctl(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s) {
+  if (c.px_G) launch_ctl_px<true>(c, lpm, lds, s);
+  else launch_ctl_px<false>(c, lpm, lds, s);
   return hipGetLastError();
 }
 

@@ -225,6 +225,77 @@ __host__ __device__ __forceinline__ double np_pairwise_ring(const double* v, int
   return s;
 }
 
+// ---- the sharded controller's exchange (llampc_ctl_set_exchange; BASELINE config 5) --------
+// Every rank ticks the controller on its contiguous shard of the global bank.  The look-back's
+// completing block pushes ONE record per tick into every peer's mailbox: its shard's sorted
+// top-K and its argmin as K + 1 entries (window mean, global model index), four 32-bit payload
+// words each (value hi, lo, index hi, lo; index -1: none).  Every rank merges the G records
+// the same way (below), so every rank holds the unsharded selection: the argmin (rt.py:359,
+// NaN-first under NAN_FIRST) and the top-K (rt.py:360: argsort order, NaN last, ties to the
+// lower global index).  Each then rolls out those K + 1 models itself from the replicated
+// global parameter table, so the controller state stays identical on every rank and no second
+// exchange is needed.  The host restatement (llampc_ctl_merge) runs the same functions.
+__host__ __device__ constexpr int ctl_rec_words(int K) { return 4 * (K + 1); }
+constexpr int kCtlPxMax = 16;               // largest world of the sharded controller (its LDS)
+
+// argsort order key of a window mean (order_key's: -0 -> +0, every NaN one value above +inf)
+__host__ __device__ __forceinline__ uint64_t ctl_okey(double w) {
+  const double wc = (w != w) ? __builtin_nan("") : w + 0.0;
+  const uint64_t b = __builtin_bit_cast(uint64_t, wc);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+// The merge order of a top-K entry e of the G K gathered ones: (key, id) with missing entries
+// after every real one, each unique by position (ids of real models are < 2^62).
+__host__ __device__ __forceinline__ void ctl_entry_order(double v, int64_t gid, int e, uint64_t& key, uint64_t& id) {
+  const bool none = gid < 0;
+  key = none ? ~0ull : ctl_okey(v);
+  id = none ? (0x7FFFFFFFFFFFFFFFull - 1024 + (uint64_t)e) : (uint64_t)gid;
+}
+__host__ __device__ __forceinline__ bool ctl_order_lt(uint64_t ka, uint64_t ia, uint64_t kb, uint64_t ib) {
+  return (ka < kb) | ((ka == kb) & (ia < ib));
+}
+// The merged argmin over the G shards' argmins (entry K of each record): np.argmin's order
+// (NaN-first: the lowest index holding NaN) or NaN-last; index -1 = none.  Returns the winner's
+// shard (or -1).
+// shard g's argmin entry comes from get(g, value, index).
+template <typename Get>
+__host__ __device__ __forceinline__ int ctl_merge_argmin(Get get, int G, bool nan_first, double& bv, int64_t& bi) {
+  bv = nan_first ? __builtin_inf() : __builtin_nan("");
+  bi = kNoIndex;
+  int owner = -1;
+  for (int g = 0; g < G; ++g) {
+    double v;
+    int64_t id;
+    get(g, v, id);
+    if (id < 0) continue;
+    if (key_less(nan_first, v, id, bv, bi)) {
+      bv = v;
+      bi = id;
+      owner = g;
+    }
+  }
+  if (owner < 0) {
+    bi = -1;
+    bv = __builtin_nan("");
+  }
+  return owner;
+}
+// The merged top-K position of entry e among the M = G K gathered ones (order = ctl_entry_order;
+// key(j) / id(j) give entry j's): its rank, < K for the entries that make the top-K.
+template <typename Key, typename Id>
+__host__ __device__ __forceinline__ int ctl_merge_rank(Key key, Id id, int M, int e) {
+  const uint64_t k = key(e), i = id(e);
+  int r = 0;
+  for (int j = 0; j < M; ++j) r += (int)ctl_order_lt(key(j), id(j), k, i);
+  return r;
+}
+// LDS bytes of the exchange (the completing block, from kScratchBytes): the G records as
+// 32-bit words, the M entries' keys and ids, the output ranks, the waves' late flags.
+__host__ __device__ __forceinline__ size_t ctl_px_bytes(int G, int K) {
+  const size_t rec = ((size_t)4 * G * ctl_rec_words(K) + 15) & ~(size_t)15;
+  return rec + 16 * (size_t)G * K + 4 * LLAMPC_KMAX + 16;
+}
+
 // The controller launch (ctl.hip ctl_kernel): every field set by the host (capi.hip
 // llampc_ctl_*) except the look-back's x_now, which the kernel points at x_t.
 struct CtlLaunch {
@@ -259,6 +330,14 @@ struct CtlLaunch {
   int32_t p0_walk;            // the state's projidx and the walk's mu bracket (rt.py:278-282),
   MuBracket br_walk;          //   from the host's copy of the last record: the look-ahead
                               //   prologue's table loads wait on no state or mu-table load
+  // sharded (px_G > 0, llampc_ctl_set_exchange): the selection's model indices are global, the
+  // look-ahead's params (la.params, la.n) the replicated global table, sel_goff = 0; else
+  // sel_goff = the bank's global offset (the selection's indices are local to the bank)
+  int64_t sel_goff;
+  uint64_t* const* px_box;    // every rank's mailbox as mapped here (device array)
+  int32_t px_G, px_rank;
+  uint32_t px_seq;            // the mailbox's tick number of this exchange
+  uint32_t px_bound;          // the peers' wait bound, units of 2^16 s_memrealtime ticks
 };
 
 // llampc_ctl_reference's launch: ConstantSpeed alone (planner.py:12-67) on the device.
@@ -274,7 +353,7 @@ hipError_t launch_constant_speed(const CsLaunch& a, hipStream_t s);
 
 // LDS bytes of the controller launch and the completing block's area offset (ctl.hip); s4:
 // with the staged input terms (CtlLaunch.s4).
-size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4 = false);
+size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4 = false, int px_G = 0);
 hipError_t launch_ctl(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s);
 
 }  // namespace llampc

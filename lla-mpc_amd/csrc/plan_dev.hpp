@@ -1292,15 +1292,20 @@ __device__ __forceinline__ E* tree_merge(E* buf0, E* buf1, int L, int K) {
 // The controller tick's use of lb_final (SEL = true, ctl.hip): the selection is also published
 // for the look-ahead blocks waiting on it — tagged words [K + 1] (local model index of top-K
 // entry k, kNoLocal = none; entry K: the argmin) — and kept in LDS for the completion.
+// SEL = 2 (the sharded controller, ctl.hip ctl_exchange): nothing is published and no record
+// field written — the shard's top-K and argmin (local index, value) go to ids / xv for the
+// exchange, which publishes the MERGED selection.
 struct CtlSel {
   uint64_t* tag;
   uint32_t seq;
   uint32_t* ids;         // LDS [K + 1]
   double* dr;            // LDS [K]: bank Dr / Df of the top-K (NaN: none)
   double* df;
+  double* xv;            // LDS [K + 1]: SEL = 2, the entries' window means
+  int32_t* xlate;        // LDS [1]: the exchange gave up waiting for a peer (status)
 };
 
-template <bool SEL = false>
+template <int SEL = 0>
 __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* smem, const CtlSel* cs = nullptr) {
   STAMP(0);
   const int tid = threadIdx.x;
@@ -1414,7 +1419,18 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
     kv = val[e];
   }
   STAMP(2);
-  if constexpr (SEL) {                     // the controller's selection first: the look-ahead
+  if constexpr (SEL == 2) {                // the sharded controller: the shard's lists only
+    if (lane < K) {
+      cs->ids[lane] = kl;
+      cs->xv[lane] = kv;
+    }
+    if (lane == 0) {
+      cs->ids[K] = li;
+      cs->xv[K] = v;
+    }
+    return;
+  }
+  if constexpr (SEL == 1) {                // the controller's selection first: the look-ahead
     if (lane < K) {                        // blocks wait on it (the record's stores below wait
       cs->ids[lane] = kl;                  // on the Pacejka loads of the top-K rows)
       st_wt(&cs->tag[lane], tag_word(cs->seq, kl));
@@ -1447,7 +1463,7 @@ __device__ __forceinline__ void lb_final(const FinalLaunch& f, unsigned char* sm
     st_wt(&o->lb_best, li == kNoLocal ? (int64_t)-1 : f.goff + (int64_t)li);
     st_wt(&o->lb_best_val, li == kNoLocal ? __builtin_nan("") : v);
   }
-  if constexpr (SEL) {
+  if constexpr (SEL == 1) {
     if (lane < K) {
       const bool have = kl != kNoLocal;
       cs->dr[lane] = have ? f.params[5 * f.n + kl] : __builtin_nan("");

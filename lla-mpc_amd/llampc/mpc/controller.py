@@ -208,6 +208,20 @@ class DeviceController:
             nat.check(rc)
         return out
 
+    def set_exchange(self, sharded):
+        """Tick this controller as one rank of a SHARDED bank (llampc_ctl_set_exchange): ``sharded``
+        is this rank's ShardedBank (its shard is the bank this controller drives; its peer
+        mailbox carries the per-tick exchange).  Every rank then holds the unsharded controller's
+        selection, record and state.  Call on every rank before the first tick."""
+        if sharded.bank is not self.bank:
+            raise ValueError("the controller must drive the ShardedBank's own shard")
+        if sharded.mailbox is None:
+            raise nat.NativeError("the sharded controller needs the peer mailbox transport "
+                                  f"(transport {sharded.transport!r}: {sharded.fallback_reason})")
+        pg = sharded.params_global
+        nat.check(nat.load().llampc_ctl_set_exchange(self._h, sharded.mailbox, nat.dptr(pg), int(pg.shape[1])))
+        self._gparams = pg
+
     def inputs(self):
         """The last tick's reference xref [2, H+1] and candidates U [C, H, 2] (debug_inputs)."""
         xref = np.empty((2, self.H + 1))
@@ -313,6 +327,14 @@ class LLAMPC:
         if mode not in ("device", "host"):
             raise ValueError(f"mode={mode!r}: 'device' or 'host'")
         self.mode = mode
+        # a ShardedBank: this rank's controller over its shard, exchanging the selection with the
+        # other ranks every tick (device mode; BASELINE config 5 across GPUs)
+        sharded = bank if hasattr(bank, "params_global") and hasattr(bank, "bank") else None
+        if sharded is not None:
+            if mode != "device":
+                raise ValueError("a sharded bank needs mode='device' (the exchange runs inside the tick's launch)")
+            bank = sharded.bank
+        self.sharded = sharded
         self.bank, self.track = bank, track
         nominal = ORCA(control='pwm') if nominal is None else nominal
         col = np.array([[float(nominal[k])] for k in BANK_ORDER])
@@ -325,6 +347,8 @@ class LLAMPC:
                                          S=S, sigma=sigma, seed=seed, nominal6=col[:, 0],
                                          cost=cost if cost is not None else nat.cost_struct(enforce_bounds=True),
                                          nan_policy=nan_policy, debug_inputs=debug_inputs)
+            if sharded is not None and sharded.exchange:
+                self._ctl.set_exchange(sharded)
         else:
             # a one-model bank: the warm-up look-ahead runs the same kernel on the nominal model
             self.nominal_bank = ModelBank(col, shared=bank.shared, W=1, device=bank.device)

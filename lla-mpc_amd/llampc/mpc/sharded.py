@@ -93,6 +93,22 @@ def probe_record(rank: int, world: int, K: int = 10) -> nat.PlanOut:
     return o
 
 
+def merge_ctl_records(vals, gids, nan_policy=nat.NAN_FIRST):
+    """The sharded controller's merge on the host (llampc_ctl_merge: the functions the device
+    exchange runs).  vals / gids [G, K+1]: each shard's sorted top-K (global index -1: none) and,
+    last, its argmin.  -> (topk [K] (-1 padded), topk_val [K], best, best_val)."""
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    gids = np.ascontiguousarray(gids, dtype=np.int64)
+    G, K1 = vals.shape
+    K = K1 - 1
+    topk = np.empty(K, dtype=np.int64)
+    tv = np.empty(K)
+    best, bv = C.c_int64(), C.c_double()
+    nat.check(nat.load().llampc_ctl_merge(nat.dptr(vals), gids.ctypes.data, G, K, int(nan_policy), topk.ctypes.data,
+                                          nat.dptr(tv), C.byref(best), C.byref(bv)))
+    return topk, tv, best.value, bv.value
+
+
 def records_equal(a: nat.PlanOut, b: nat.PlanOut) -> bool:
     A, B = nat.plan_out_to_dict(a), nat.plan_out_to_dict(b)
     for k in B:
@@ -120,7 +136,8 @@ class ShardedBank:
                  group=None, shared=None):
         import torch
         import torch.distributed as dist
-        params_global = np.asarray(params_global, dtype=np.float64)
+        params_global = np.ascontiguousarray(params_global, dtype=np.float64)
+        self.params_global = params_global     # the sharded controller's replicated table
         self.n_global = params_global.shape[1]
         self.rank, self.world, self.device, self.group = rank, world, device, group
         lo, hi = shard_range(self.n_global, rank, world)
@@ -331,6 +348,12 @@ class ShardedBank:
     def plan_device(self, staged: dict, stream=None, **kw):
         pin = self.make_plan_in(staged["pack"], staged["C"], staged["H"], **kw)
         return self.launch(pin, stream)
+
+    @property
+    def mailbox(self):
+        """This rank's peer mailbox (llampc_mailbox*), or None when the peer transport is not in
+        use (world 1, or a fallback transport)."""
+        return self._mailbox
 
     def close(self):
         if self._mailbox is not None:        # after this rank's last exchange (it synchronises)

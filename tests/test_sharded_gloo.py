@@ -118,3 +118,72 @@ def run_gloo_ranks(target, world, timeout=240):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_merge_gloo(world):
     run_gloo_ranks(_worker, world)
+
+
+def _ctl_merge_worker(rank, world, store, q):
+    """One rank of the sharded controller's selection (ctl.hpp "sharded controller"): its shard's
+    window (the oracle stands in for the look-back kernel), its record — the sorted top-K and the
+    argmin as (window mean, global index) — gathered over gloo and merged by the product's
+    llampc_ctl_merge (the functions the device exchange runs): every rank must hold the
+    unsharded argmin (np.argmin: first NaN) and top-K (stable argsort: NaN last, ties to the
+    lower index), on a bank with exact ties across shards and NaN models."""
+    try:
+        for pth in (REPO, PKG_ROOT):
+            sys.path.insert(0, pth)
+        import torch.distributed as dist
+        from llampc import _native as nat
+        from llampc.mpc import generate_bank, shard_range
+        from llampc.mpc.sharded import merge_ctl_records
+        from oracle import llampc_oracle as O
+        dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=120))
+        d = golden("dyn_slice.npz")
+        s, u = d["states"], d["inputs"]
+        pp = O.orca_params()
+        shared = {k: pp[k] for k in ("lf", "lr", "mass", "Iz", "Cm1", "Cm2", "Cr0", "Cr2")}
+        N, W, K = 907, 4, 10
+        b0 = None
+        for case in ("plain", "ties", "nan"):
+            p = generate_bank(N, seed=31)
+            if case == "ties":             # copies of the best model in every shard: equal means
+                p[:, [c for c in (5, 300, 301, 620, 906) if c != b0]] = p[:, [b0]]
+            elif case == "nan":            # NaN models in two shards: argmin = the first NaN
+                p[2, [777, 150]] = np.nan
+            with np.errstate(all="ignore"):
+                errs = [O.lookback_errors(O.evaluate_models_vectorized(shared, tuple(p), s[:, t], u[:, t], TS), s[:, t + 1])
+                        for t in range(W)]
+            full = O.LookbackWindow(N, W, K)
+            for e in errs:
+                full.push(e)
+            if case == "plain":
+                b0 = full.current
+            lo, hi = shard_range(N, rank, world)
+            avg = full.avg[lo:hi]          # the shard's own window means (same values)
+            order = np.argsort(avg, kind="stable")[:K]
+            vals = np.full(K + 1, np.nan)
+            gids = np.full(K + 1, -1, dtype=np.int64)
+            vals[:order.size], gids[:order.size] = avg[order], order + lo
+            vals[K], gids[K] = avg[int(np.argmin(avg))], int(np.argmin(avg)) + lo
+            parts = [None] * world
+            dist.all_gather_object(parts, (vals, gids))
+            topk, tv, best, bv = merge_ctl_records(np.stack([a for a, _ in parts]), np.stack([b for _, b in parts]),
+                                                   nat.NAN_FIRST)
+            want = np.argsort(full.avg, kind="stable")[:K]
+            np.testing.assert_array_equal(topk, want, err_msg=case)
+            np.testing.assert_array_equal(tv, full.avg[want])
+            assert best == int(np.argmin(full.avg)), (case, best)
+            if case == "nan":
+                assert best == 150 and np.isnan(bv)
+            if case == "ties":             # the copies' equal means did meet in the merge
+                assert np.sum(full.avg[topk] == full.avg[b0]) >= 5, topk
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_controller_merge_gloo(world):
+    run_gloo_ranks(_ctl_merge_worker, world)

@@ -175,3 +175,6 @@ def test_bench_spawns_its_own_ranks():
     assert rec["C64"]["ms_per_step"] > 0
     c5 = rec["config5"]
     assert c5["N_per_track"] == 4000 and c5["transport"] == ["peer", "peer"] and c5["p99_us"] > 0
+    # the sharded controller (config 5's real loop): both tracks' controllers over both ranks
+    ct = rec["controller_tick_us"]
+    assert ct["N_per_track"] == 4000 and ct["transport"] == ["peer", "peer"] and 0 < ct["p50"] <= ct["p99"]
