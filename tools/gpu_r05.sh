@@ -11,6 +11,8 @@ mkdir -p "$OUT"
 bash tools/gpu_check.sh "$OUT" "$3" || exit $?
 echo "[$(date +%T)] driver's command"
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench_k20.json" 2> "$OUT/bench_k20.err" || exit $?
+echo "[$(date +%T)] accuracy headroom"
+timeout -k 10 300 python -u tools/diag/accuracy_headroom.py "$OUT/accuracy.json" > "$OUT/accuracy.log" 2>&1 || exit $?
 if [ "$2" != "noprof" ]; then
   bash tools/gpu_r05_prof.sh "$OUT/prof5" || exit $?
 fi
