@@ -128,10 +128,29 @@ def wide_case():
             "final_state_integrate_api": relerr(xf, g["x_final"])}
 
 
+def nlp_case():
+    """setupNLP's objective against the committed SLSQP local optima (tests/golden/nlp_optimum.npz):
+    fval / f* per case (the test bounds it by 1.05)."""
+    from llampc.models import Dynamic
+    from llampc.mpc.nmpc import setupNLP
+    from llampc.tracks import ETHZ
+    g = np.load(os.path.join(REPO, "tests", "golden", "nlp_optimum.npz"))
+    ratios = []
+    for i in range(len(g["fstar"])):
+        nlp = setupNLP(int(g["xref"][i].shape[1] - 1), TS, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p0,
+                       Dynamic(**p0, device=0), ETHZ('optimal', True), device=0)
+        try:
+            _, fval, _, _ = nlp.solve(g["x0"][i], g["xref"][i], g["uprev"][i])
+        finally:
+            nlp.close()
+        ratios.append(fval / float(g["fstar"][i]))
+    return {"shape": "nlp_vs_slsqp", "fval_over_fstar": ratios, "max": float(max(ratios))}
+
+
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else None
     rows = [plan_case("c1_h20", 10000, 1, 20), plan_case("c1_h40", 10000, 1, 40), wide_case(), ctl_case(),
-            plan_case("c64_h20", 10000, 64, 20)]
+            nlp_case(), plan_case("c64_h20", 10000, 64, 20)]
     for r in rows:
         print(json.dumps(r), flush=True)
     if out:
