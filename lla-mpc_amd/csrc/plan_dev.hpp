@@ -281,30 +281,58 @@ __device__ __forceinline__ Tire load_tire(const double* p, int64_t ld, int64_t i
   return t;
 }
 
-// np.mean(window, axis=1) for one model: NumPy's pairwise order (8 partial sums) over the
-// ring read oldest -> newest, then / W.  W <= LLAMPC_WMAX (one pairwise block).
-__device__ __forceinline__ double window_mean(const double* ring, int64_t ld, int64_t n, int o,
-                                              int W) {
+// np.mean(window, axis=1) for one model (rt.py:358): NumPy's pairwise order (8 partial sums)
+// over the ring read oldest -> newest, then / W; W <= LLAMPC_WMAX (one pairwise block).
+// Split around the newest value (the ring slot this tick writes): every older
+// value is loaded and summed BEFORE the look-back's RK4 step — the loads' latency under the
+// step instead of after it — in that exact order, so finishing with the newest error
+// (win_finish) gives the mean's bits in that order.  Oldest -> newest is i = 0 .. W-1, the newest i = W-1:
+//   W < 8 or W % 8 != 0: the newest is the sequential tail's last add:  s = pre + e
+//   W % 8 == 0 (W >= 8):  it is r[7]'s last term (W = 8: r[7] itself), so
+//                          s = A + (B + (r6 + r7)),  A = (r0 + r1) + (r2 + r3),  B = r4 + r5
+struct WinPre {
+  double a, b, c, d;                    // pre | A, B, r6, r7 without the newest
+};
+__device__ __forceinline__ WinPre win_pre(const double* ring, int64_t ld, int64_t n, int o, int W) {
   auto at = [&](int i) {
     int s = o + i;
     if (s >= W) s -= W;
     return ring[(int64_t)s * ld + n];
   };
-  double s;
+  WinPre p{0.0, 0.0, 0.0, 0.0};
   if (W < 8) {
-    s = 0.0;
-    for (int i = 0; i < W; ++i) s += at(i);
+    for (int i = 0; i < W - 1; ++i) p.a += at(i);
+    return p;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = j < W - 1 ? at(j) : 0.0;
+  int i = 8;
+  const int full = W - (W % 8);
+  for (; i < full; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i + j < W - 1) r[j] += at(i + j);
+  }
+  if (W % 8 == 0) {
+    p.a = (r[0] + r[1]) + (r[2] + r[3]);
+    p.b = r[4] + r[5];
+    p.c = r[6];
+    p.d = r[7];                         // W = 8: unused (r[7] is the newest itself)
+    return p;
+  }
+  double s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < W - 1; ++i) s += at(i);
+  p.a = s;
+  return p;
+}
+__device__ __forceinline__ double win_finish(const WinPre& p, double e, int W) {
+  double s;
+  if (W >= 8 && W % 8 == 0) {
+    const double r7 = W == 8 ? e : p.d + e;
+    s = p.a + (p.b + (p.c + r7));
   } else {
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = at(j);
-    int i = 8;
-    for (; i < W - (W % 8); i += 8) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] += at(i + j);
-    }
-    s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < W; ++i) s += at(i);
+    s = p.a + e;
   }
   return s / W;
 }
@@ -476,6 +504,9 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
 #pragma unroll
     for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
     const Tire t = load_tire(a.params, a.n, n);
+    const int o = (a.slot + 1 == a.W) ? 0 : a.slot + 1;     // the window's oldest slot
+    WinPre wp{0.0, 0.0, 0.0, 0.0};
+    if (a.full) wp = win_pre(a.ring, a.n, n, o, a.W);      // launch-uniform; under the step
     // model.py:32-40, one RK4 step: the fast stage; a lane whose operands leave the fast
     // cores' domains redoes the step with the general functions (as the look-ahead does)
     const StageK sk = make_stage<1>(a.veh, t, 0);
@@ -497,8 +528,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     if (a.err_out) a.err_out[n] = err;
     a.ring[(int64_t)a.slot * a.n + n] = err;             // rt.py:352-353 without np.roll
     if (a.full) {
-      const int o = (a.slot + 1 == a.W) ? 0 : a.slot + 1;   // oldest slot
-      const double wm = window_mean(a.ring, a.n, n, o, a.W);   // rt.py:358
+      const double wm = win_finish(wp, err, a.W);          // rt.py:358
       if (a.R > 1 || a.wm_keep) a.wm_buf[n] = wm;         // launch-uniform
       if (r == 0) wm0 = wm;
     }

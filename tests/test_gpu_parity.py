@@ -124,10 +124,12 @@ def test_lookback_window_argmin_topk_vs_golden(nat):
         np.testing.assert_allclose(ring[:, 0], g["errors"][-int(g["W"])], rtol=RTOL_STEP)
 
 
-@pytest.mark.parametrize("N,W,K", [(1, 1, 1), (5, 3, 10), (257, 10, 10), (1000, 8, 32), (3001, 17, 7)])
+@pytest.mark.parametrize("N,W,K", [(1, 1, 1), (5, 3, 10), (257, 10, 10), (1000, 8, 32), (3001, 17, 7),
+                                   (700, 16, 5)])
 def test_lookback_edge_shapes(nat, N, W, K):
     """Ragged N (not a multiple of 256), N < K (padding with -1), W below/above 8 (both
-    pairwise-sum branches), K up to KMAX."""
+    pairwise-sum branches; W = 8 and 16: the newest error is the last term of the 8th partial
+    sum, the other W the sequential tail's last add — win_pre / win_finish), K up to KMAX."""
     from llampc.mpc import ModelBank, generate_bank
     d = golden("dyn_slice.npz")
     s, u = d["states"], d["inputs"]
