@@ -1366,3 +1366,39 @@ def test_lookahead_raceline_per_model_xref(nat, track_name, start):
                    return_costs=True, raceline_start=(s0, v0, scale))
     close(res.costs, cref, RTOL_ROLL)
     assert res.global_best[0] * C + res.global_best[1] == int(np.argmin(np.where(np.isnan(cref), np.inf, cref).ravel()))
+
+
+@pytest.mark.parametrize("C,gap", [(64, 1e-9), (64, 1e-12), (8, 1e-7)])
+def test_lookahead_argmin_near_ties(nat, C, gap):
+    """The look-ahead's candidate choice when candidates nearly tie: C candidates
+    that differ by `gap` (relative) in their steering, so many costs lie within the rollouts'
+    error bound of each other.  The choice must be exact where the oracle's best and second
+    best differ by more than twice RTOL_ROLL, and wherever they do not, the chosen candidate's
+    ORACLE cost must lie within 2 RTOL_ROLL of the minimum (a flip among costs the fp64 cores
+    cannot tell apart, never a worse control).  The flip count is reported."""
+    from llampc.mpc import ModelBank, generate_bank
+    N, H = 400, 20
+    p = generate_bank(N, seed=77)
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    x0 = s[:, 40]
+    base = u[:, 40:40 + H].T.copy()
+    U = np.repeat(base[None], C, axis=0)
+    U[:, :, 1] += (np.arange(C) * gap * 0.3)[:, None]
+    xref = np.vstack([s[0, 40:41 + H] + 0.01, s[1, 40:41 + H] - 0.02])
+    up = u[:, 39]
+    with ModelBank(p, device=0) as b:
+        r = b.lookahead(x0, U, xref, up, Ts=TS, return_costs=True, return_best_cand=True)
+    cref = O.mpc_cost(O.rollout_rk4(shared(), tuple(p), x0, U, TS), U, xref, up, np.eye(2), np.diag([5e-3, 1]),
+                      np.zeros((2, 2))).reshape(N, C)
+    close(r["costs"].ravel(), cref.ravel(), RTOL_ROLL)
+    cm = np.where(np.isnan(cref), np.inf, cref)
+    got = r["best_cand_per_model"]
+    srt = np.sort(cm, axis=1)
+    sep = (srt[:, 1] - srt[:, 0]) > 2 * RTOL_ROLL * np.abs(srt[:, 0])
+    want = np.argmin(cm, axis=1)
+    np.testing.assert_array_equal(got[sep], want[sep])
+    chosen = cm[np.arange(N), got]
+    assert np.all(chosen <= srt[:, 0] * (1 + 2 * RTOL_ROLL)), np.max(chosen / srt[:, 0])
+    flips = int(np.sum(got != want))
+    print(f"C={C} gap={gap}: {int(np.sum(~sep))} of {N} models near-tied, {flips} choices differ from the oracle's argmin")
