@@ -11,7 +11,9 @@ arithmetic order alone can produce is told apart from a wrong kernel).
   wide              the sigma = 2 bank (tests/golden/rollout_wide.npz): costs (plan) and final
                     states (llampc_integrate_batch, RK4) vs the reference's own x_final
 
-usage: python tools/diag/accuracy_headroom.py [out.json]   (GPU)"""
+  c2_scenario / c3_scenario  plan() on configs 2 / 3's own scenario states (llampc.mpc.scenarios)
+
+usage: python tools/diag/accuracy_headroom.py [out.json] [case,case,...]   (GPU)"""
 import json
 import os
 import sys
@@ -82,6 +84,36 @@ def plan_case(name, N, C, H, seed=0):
     return out
 
 
+def scenario_case(name, track, H, seed, N=10000, C=1, W=10, K=10):
+    """Configs 2 / 3 on their own scenario states (llampc.mpc.scenarios, the test's inputs):
+    every full-window tick's N costs."""
+    from llampc.mpc import ModelBank, generate_bank, plan
+    from llampc.mpc.scenarios import scenario_ticks, unpack
+    ticks = scenario_ticks(track, H, C, W + 3, device=0)
+    bank = generate_bank(N, seed=seed)
+    got, want, worst = [], [], None
+    with ModelBank(bank, W=W, device=0) as b:
+        for t, pk in enumerate(ticks):
+            f = unpack(pk, H, C)
+            last = t >= W - 1
+            res = plan(b, f["x_now"], f["u_prev"], f["x_prev"], f["xref"], f["U"], uprev=f["uprev"], Ts=TS, K=K,
+                       return_costs=last)
+            if not last:
+                continue
+            cref = O.mpc_cost(O.rollout_rk4(SHARED, tuple(bank), f["x_now"], f["U"], TS), f["U"], f["xref"],
+                              f["uprev"], Q, R, P)
+            r = relerr(res.costs.ravel(), cref)
+            if worst is None or r["max"] > worst[0]["max"]:
+                worst = (r, f)
+            got.append(res.costs.ravel())
+            want.append(cref)
+    out = {"shape": name, "N": N, "C": C, "H": H, "cost": relerr(np.concatenate(got), np.concatenate(want))}
+    r, f = worst
+    out["worst_conditioning"] = conditioning(bank, r["worst_index"], C, f["x_now"], f["U"], f["xref"], f["uprev"])
+    out["worst_conditioning"]["err"] = r["max"]
+    return out
+
+
 def ctl_case(N=10000, C=64, H=40, W=10, K=10, ticks=14):
     from llampc.mpc import LLAMPC, ModelBank, generate_bank
     from llampc.tracks import ETHZ
@@ -149,8 +181,13 @@ def nlp_case():
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else None
-    rows = [plan_case("c1_h20", 10000, 1, 20), plan_case("c1_h40", 10000, 1, 40), wide_case(), ctl_case(),
-            nlp_case(), plan_case("c64_h20", 10000, 64, 20)]
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+    cases = [("c2_scenario", lambda: scenario_case("c2_scenario", "ETHZ", 20, 0)),
+             ("c3_scenario", lambda: scenario_case("c3_scenario", "ETHZMobil", 40, 1)),
+             ("c1_h20", lambda: plan_case("c1_h20", 10000, 1, 20)), ("c1_h40", lambda: plan_case("c1_h40", 10000, 1, 40)),
+             ("wide", wide_case), ("ctl_h40", ctl_case), ("nlp", nlp_case),
+             ("c64_h20", lambda: plan_case("c64_h20", 10000, 64, 20))]
+    rows = [fn() for name, fn in cases if only is None or name in only]
     for r in rows:
         print(json.dumps(r), flush=True)
     if out:
