@@ -180,19 +180,20 @@ constexpr double kAtanR[10] = {
     -0.06649613695291669,  0.05736332165907643,  -0.04483334622272886,
     0.02275052699336167};
 constexpr double kTanPi8 = 0.41421356237309503;
-// Lean cores of the look-ahead rollouts (kLeanLA): 7-term atan (3.0e-12 relative on |t| <=
-// tan(pi/8)) and 7-term sin_wide (1.0e-11 absolute to |a| = 2, 3.9e-11 to 3), and the division
-// without its residual correction (<= 18 ulp): ~1e-11 relative on the tire forces against the
-// <= 4 ulp of the precise cores, which the look-back keeps (its errors are ranked).  Round 3
-// shipped 9 terms; round 4 went to 8 (12 fewer instructions per LPM-4 step, 24 per LPM-1 step;
-// profiles/r04/ab_lean8.log) and then 7 (another 12 / 32 with the LPM-1 lane's single
-// lower-bound record, dyn.hpp forces_fast): alternating A/B (profiles/r04/ab_lean7.log)
-// 26.75-26.91 -> 26.07-26.35 us per tick at C = 1 and 390-394 -> 372-373 us at C = 64.  The
-// rollout costs stay within 1e-6 of the NumPy restatement (the worst of the GPU tests' 10^6
-// costs: 1.2e-7, a tracking term's cancellation x - xref; north star: 1e-5).
-// -DLLAMPC_LEAN_TERMS=8 / 9 build the earlier cores (tools/fit_fastmath.py fits them).
+// Lean cores of the look-ahead rollouts (kLeanLA): 8-term atan (1.1e-13 relative on |t| <=
+// tan(pi/8)) and 8-term sin_wide (2.6e-13 absolute to |a| = 3), and the division without its
+// residual correction (<= 18 ulp), against the <= 4 ulp of the precise cores, which the
+// look-back keeps (its errors are ranked).  Round 3 shipped 9 terms, round 4 went to 8 and then
+// 7 (-12 / -32 instructions per LPM-4 / LPM-1 step, 26.3 -> 26.0 us per tick).  Round 5 measured
+// the cost of that on ill-conditioned rollouts (tools/diag/accuracy_headroom.py,
+// profiles/r05/accuracy_lean.txt): on config 3's own Mobil scenario states, where a ONE-ulp
+// change of x0 moves a cost by 1.5e-8 relative in NumPy itself, the 7-term cores
+// were 9.3e-5 off (6,400 ulp-equivalents: past the north star's 1e-5), 8 terms 6.8e-7 (47),
+// 9 terms 1.6e-8 (1.1); every well-conditioned shape stays within 1e-10 with 8 terms.  So 8
+// terms again (+0.2-0.4 us per tick at C = 1, +2 % at C = 64).
+// -DLLAMPC_LEAN_TERMS=7 / 9 build the other cores (tools/fit_fastmath.py fits them).
 #ifndef LLAMPC_LEAN_TERMS
-#define LLAMPC_LEAN_TERMS 7
+#define LLAMPC_LEAN_TERMS 8
 #endif
 constexpr int kLeanTerms = LLAMPC_LEAN_TERMS;
 #if LLAMPC_LEAN_TERMS == 7

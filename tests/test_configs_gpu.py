@@ -9,21 +9,22 @@
             full window the selection and every model's cost, against the oracle
   config 3  ETHZMobil, N = 10^4, H = 40, the sudden-drop scenario's synthetic Mobil states
             (track start, seed 3), same checks
-Tolerances: one integration step 1e-9 (the look-back), rollout costs RTOL_ROLL (the look-ahead's
-lean cores; DESIGN §4 has the measured bound), indices exact."""
+Tolerances: one integration step 1e-9 (the look-back); rollout costs RTOL_ROLL = 1e-7, or for
+an ill-conditioned rollout KAPPA_ULP times its own one-ulp sensitivity in the oracle
+(conftest.assert_costs_close; DESIGN §4 has the measured errors per shape); indices exact."""
 import os
 
 import numpy as np
 import pytest
 
-from conftest import REPO, golden
+from conftest import REPO, assert_costs_close, cost_sensitivity, golden
 from oracle import llampc_oracle as O
 
 pytestmark = pytest.mark.gpu
 
 TS = 0.02
 RTOL_STEP = 1e-9
-RTOL_ROLL = 1e-6
+RTOL_ROLL = 1e-7
 Q, R, P = np.eye(2), np.diag([5e-3, 1.0]), np.zeros((2, 2))
 
 
@@ -107,7 +108,7 @@ def test_config_scenario_ticks_vs_oracle(nat, track, H, seed):
         assert np.hypot(ticks[0][0] - tr.x_init, ticks[0][1] - tr.y_init) < 0.2
     p = generate_bank(N, seed=seed)
     win = O.LookbackWindow(N, W, K)
-    full_ticks = 0
+    full_ticks = conditioned = 0
     with ModelBank(p, W=W, device=0) as b:
         for t, pk in enumerate(ticks):
             f = unpack(pk, H, C)
@@ -126,7 +127,10 @@ def test_config_scenario_ticks_vs_oracle(nat, track, H, seed):
             np.testing.assert_array_equal(res.topk, win.best_k)
             cref = O.mpc_cost(O.rollout_rk4(shared(), tuple(p), f["x_now"], f["U"], TS), f["U"], f["xref"],
                               f["uprev"], Q, R, P)
-            close(res.costs.ravel(), cref, RTOL_ROLL)
-            np.testing.assert_allclose(res.cost, cref[win.current], rtol=RTOL_ROLL)
+            sens = lambda idx: cost_sensitivity(shared(), tuple(p[:, idx]), f["x_now"], f["U"], f["xref"],  # noqa: E731
+                                                f["uprev"], Q, R, P)
+            conditioned += assert_costs_close(res.costs.ravel(), cref, RTOL_ROLL, sens)
+            assert_costs_close([res.cost], [cref[win.current]], RTOL_ROLL, lambda idx: sens(np.array([win.current])))
             assert res.global_best[0] == int(np.argmin(np.where(np.isnan(cref), np.inf, cref)))
     assert full_ticks == 4
+    print(f"{track}: {conditioned} of {4 * N} costs held by their conditioning bound")

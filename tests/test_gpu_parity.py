@@ -1,7 +1,11 @@
 """GPU parity tests: the HIP path (through the C ABI) against the pinned oracle and the
 reference-generated golden vectors.  Tolerances: fp64 values 1e-9 relative for one
-integration step (ocml vs NumPy transcendentals differ by ulps), 1e-6 for H-step rollouts
-and their costs (the look-ahead's 7-term lean cores; north star bound: 1e-5); indices exact (tie-tolerant only where stated)."""
+integration step (the fast cores vs NumPy's libm differ by ulps), 1e-7 for H-step rollouts and
+their costs (the look-ahead's 8-term lean cores: the largest error measured on a well-conditioned
+shape is 1e-10, profiles/r05/accuracy_lean.txt; north star bound: 1e-5); indices exact
+(tie-tolerant only where stated).  Ill-conditioned rollouts (a one-ulp change of x0 moves the
+cost visibly in the oracle itself) are held to their conditioning (conftest.assert_costs_close)
+in tests/test_configs_gpu.py and tests/test_ctl_gpu.py."""
 import os
 
 import numpy as np
@@ -14,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 TS = 0.02
 RTOL_STEP = 1e-9
-RTOL_ROLL = 1e-6
+RTOL_ROLL = 1e-7
 
 
 @pytest.fixture(scope="module")
@@ -672,11 +676,10 @@ def test_fast_cores_ulp_on_domain(nat):
 
 
 def test_lean_cores_accuracy_on_domain(nat):
-    """The look-ahead's lean cores (math fn 10-12: 7-term atan and sin_wide, division without
-    its residual step) on the same domains vs NumPy: atan2 / atan within 2^16 ulp (~7e-12
-    relative; the fit's own error is 3.0e-12), sin_wide within 2^18 ulp for |a| <= 2 (1e-11
-    absolute) and 2^-33 absolute up to 3 (the fit: 3.9e-11) — far inside the 1e-6 rollout
-    tolerance and the north star's 1e-5."""
+    """The look-ahead's lean cores (math fn 10-12: 8-term atan and sin_wide, division without
+    its residual step) on the same domains vs NumPy: atan2 / atan within 2^11 ulp (~4.5e-13
+    relative; the fit's own error is 1.1e-13), sin_wide within 2^12 ulp for |a| <= 2 and 2^-40
+    absolute up to 3 (the fit: 2.6e-13)."""
     rng = np.random.RandomState(2)
     n = 1 << 20
     y = np.concatenate([rng.uniform(-3, 3, n), rng.standard_cauchy(n), [0.0, -0.0, 1.0, -1.0, 1e-300, 5.0]])
@@ -688,10 +691,10 @@ def test_lean_cores_accuracy_on_domain(nat):
     a = rng.uniform(-2, 2, n)
     u_s = _ulp(_math(nat, 12, a), np.sin(a))
     print(f"lean cores: atan2 {u_a2:.1f} ulp, atan {u_a:.1f} ulp, sin_wide |a|<=2 {u_s:.1f} ulp")
-    assert u_a2 <= 2 ** 16 and u_a <= 2 ** 16 and u_s <= 2 ** 18
+    assert u_a2 <= 2 ** 11 and u_a <= 2 ** 11 and u_s <= 2 ** 12
     a = np.concatenate([rng.uniform(-3, 3, n), [3.0, -3.0, 0.0, -0.0, 1e-300]])
     err = np.abs(_math(nat, 12, a) - np.sin(a))
-    assert np.all(err <= 16 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -33), err.max()
+    assert np.all(err <= 16 * np.spacing(np.abs(np.sin(a))) + 2.0 ** -40), err.max()
     # the paired cores of the LPM-1 look-ahead lane (math fn 13/14: front and rear division
     # through one reciprocal, partner = element n-1-i) on their domain (Dom::ok_paired:
     # atan2 divisors max(|y|, x) in [2^-500, 2^499], atan divisor products <= 2^499)
@@ -703,7 +706,7 @@ def test_lean_cores_accuracy_on_domain(nat):
     zz = z[np.abs(z) <= 2.0 ** 240]
     u_p = _ulp(_math(nat, 14, zz), np.arctan(zz))
     print(f"paired cores: atan2 {u_p2:.1f} ulp, atan {u_p:.1f} ulp")
-    assert u_p2 <= 2 ** 16 and u_p <= 2 ** 16
+    assert u_p2 <= 2 ** 11 and u_p <= 2 ** 11
 
 
 def test_lookahead_out_of_domain_fallback(nat):
