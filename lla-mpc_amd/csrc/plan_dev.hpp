@@ -513,6 +513,20 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     Dom dm;
     dm.init();
     step_fast<0, 1>(a.veh, t, sk, x, uf, a.Ts, K, dm);
+#ifdef LLAMPC_LB_TWICE
+    // diagnostic (stamps build only): the same step again, warm — its cycles against the first's
+    // split the first step's time into the code's cold fetch + the operands' loads vs the issue
+    if (r == 0) {
+      LB_STAMP(blk, 4);
+      double x2[6];
+      for (int j = 0; j < 6; ++j) x2[j] = a.x_prev[j];
+      Dom d2;
+      d2.init();
+      step_fast<0, 1>(a.veh, t, sk, x2, uf, a.Ts, K, d2);
+      asm volatile("" ::"v"(x2[0]), "v"(x2[1]), "v"(x2[2]), "v"(x2[3]));
+      LB_STAMP(blk, 5);
+    }
+#endif
     double s = sq_err4(x, a.x_now);                       // rt.py:349 mean over 4 states
     // the domain once per step; a NaN operand reaches x[0..3] (the stage-4 chains feed x[3])
     bool bad = (int)ubad | (int)!sk.sok | (int)!dm.ok() | (int)!(s <= __DBL_MAX__);
