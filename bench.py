@@ -849,8 +849,9 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
     try:                                    # the kernel time (their cost stays out of lat)
         nxt = time.perf_counter() + period
         for i in range(ticks + warm + ev_ticks):
-            if i == warm + ticks:
+            if i == warm + ticks:             # launched ticks: an armed launch's events hold its wait
                 for s in setups:
+                    s[1].set_prelaunch(False)
                     nat.check(lib.llampc_bank_timing(s[0].handle, 1, ev_ticks + 8))
             nxt = pace(nxt, period)
             t0 = time.perf_counter()
@@ -909,9 +910,10 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
             "kernel_us_avg": kern, "sel_models": sel, "projidx": laps, **extra_ctl,
             "host_split_us_p50": {"begin": float(np.median([a for a, _ in split[warm:warm + ticks]]) * 1e6),
                                   "end": float(np.median([b for _, b in split[warm:warm + ticks]]) * 1e6)},
-            "note": "LLAMPC.tick (device mode, llampc_ctl_tick_async/wait: one launch per track per step) for "
-                    "two tracks concurrently, paced at 1 ms; kernel_us_avg = per-launch HIP events of each "
-                    "bank's controller launch over 100 further steps (the timed steps carry no events)"}
+            "note": "LLAMPC.tick (device mode, llampc_ctl_tick_async/wait: one launch per track per step, armed "
+                    "during the previous step and rung with x_t — llampc_ctl_set_prelaunch) for two tracks "
+                    "concurrently, paced at 1 ms; kernel_us_avg = per-launch HIP events of each bank's "
+                    "controller launch over 100 further LAUNCHED steps (the timed steps carry no events)"}
 
 
 def solve_latency(args, n=200, warm=10, H=20):

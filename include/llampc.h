@@ -353,6 +353,16 @@ int llampc_ctl_tick(llampc_ctl* ctl, const double* x_t, llampc_ctl_out* out);
  * controllers of different banks (e.g. two tracks) overlap on the device. */
 int llampc_ctl_tick_async(llampc_ctl* ctl, const double* x_t);
 int llampc_ctl_wait(llampc_ctl* ctl, llampc_ctl_out* out);
+/* on = 1: every tick also enqueues the NEXT tick's launch behind itself ("armed"): it runs the
+ * part of the tick that does not need x_t (the raceline tables, the state, the variates) and
+ * then waits on a doorbell in pinned host memory; the next llampc_ctl_tick_async stores x_t and
+ * rings it instead of launching, so the launch call and the dispatch leave the control step's
+ * latency (rt.py:269-366's step starts when x_t is known).  Results are those of unarmed ticks.
+ * While armed, the bank's stream holds that launch: every other call on the bank or the
+ * controller cancels it first (it exits untouched; the next tick launches normally and re-arms),
+ * as does a tick more than 0.5 s after the arming; an armed launch never rung exits after 2 s.
+ * Not with llampc_ctl_set_exchange.  on = 0 cancels. */
+int llampc_ctl_set_prelaunch(llampc_ctl* ctl, int32_t on);
 /* ConstantSpeed (planner.py:12-67) alone on the device with the controller's tables and Ts:
  * x0 [2], v0, horizon H (<= LLAMPC_HMAX), projidx, curr_mu, scale -> xref [2][H+1], the new
  * projidx (no lap wrap) and vr.  Blocking; leaves the controller state alone. */

@@ -193,7 +193,15 @@ struct llampc_bank {
   uint64_t async_seq = 0;          // the outstanding llampc_plan_async tick's tag (0: copy path)
   int64_t launches = 0;            // plan-kernel launches enqueued on this bank (llampc_bank_launches)
   uint64_t* d_wq = nullptr;        // work-queue unit counter (0 between launches; launch_plan's WQ layout)
+  // the controller whose armed launch waits on this bank's stream (llampc_ctl_set_prelaunch):
+  // every other call that enqueues on the stream cancels it first (bank_disarm)
+  llampc_ctl* armed = nullptr;
 };
+
+// Cancels the armed controller launch waiting on the bank's stream, if any (defined with the
+// controller below): the launch exits without touching anything, and work enqueued after it
+// runs once it has.
+static void bank_disarm(llampc_bank* b);
 
 namespace {
 
@@ -671,6 +679,7 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
 
 int llampc_bank_destroy(llampc_bank* b) {
   if (!b) return LLAMPC_OK;
+  bank_disarm(b);
   {
     DeviceGuard g(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
@@ -711,6 +720,7 @@ int llampc_bank_launches(const llampc_bank* b, int64_t* launches) {
 int llampc_bank_reset(llampc_bank* b) {
   if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   DeviceGuard g(b->device);
   HIP_TRY(hipMemsetAsync(b->d_ring, 0, (size_t)b->W * b->n * sizeof(double), b->stream));
   HIP_TRY(hipMemsetAsync(b->d_tickets, 0, 2 * sizeof(unsigned), b->stream));
@@ -724,6 +734,7 @@ int llampc_bank_reset(llampc_bank* b) {
 int llampc_bank_window(llampc_bank* b, double* ring, int32_t* window_count) {
   if (!b || !ring) return fail(LLAMPC_E_ARG, "bank/ring is NULL");
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   DeviceGuard g(b->device);
   std::vector<double> raw((size_t)b->W * b->n);
   HIP_TRY(hipStreamSynchronize(b->stream));
@@ -755,6 +766,7 @@ int llampc_bank_set_concurrency(llampc_bank* b, int32_t banks) {
   if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
   if (banks < 1 || banks > 64) return fail(LLAMPC_E_ARG, "banks=%d outside [1, 64]", banks);
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   b->share = banks;
   if (banks > 1 && !b->dedicated) {      // concurrent banks: a hardware queue of its own (bank_stream)
     b->dedicated = true;
@@ -773,6 +785,7 @@ int llampc_bank_set_concurrency(llampc_bank* b, int32_t banks) {
 int llampc_bank_set_stream(llampc_bank* b, void* stream) {
   if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   DeviceGuard g(b->device);
   HIP_TRY(hipStreamSynchronize(b->stream));
   if (b->own_stream) (void)hipStreamDestroy(b->stream);
@@ -832,6 +845,7 @@ int llampc_plan(llampc_bank* b, const llampc_plan_in* in, llampc_plan_out* out, 
   int rc = check_plan_in(b, in);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
   DeviceGuard g(b->device);
   hipStream_t s = b->stream;
@@ -880,6 +894,7 @@ int llampc_bank_set_raceline(llampc_bank* b, const double* knots, int32_t n, con
   for (int32_t i = 1; i < M; ++i)
     if (!(mus[i] >= mus[i - 1])) return fail(LLAMPC_E_ARG, "mus must be ascending (at %d)", i);
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   DeviceGuard g(b->device);
   HIP_TRY(hipStreamSynchronize(b->stream));
   const size_t m = (size_t)n - 1;
@@ -909,6 +924,7 @@ int llampc_plan_async(llampc_bank* b, const llampc_plan_in* in) {
   int rc = check_plan_in(b, in);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
   DeviceGuard g(b->device);
   hipStream_t s = b->stream;
@@ -954,6 +970,7 @@ int llampc_plan_device(llampc_bank* b, const llampc_plan_in* in, void* d_out, do
   int rc = check_plan_in(b, in);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   // an outstanding async tick shares the tickets, tags, ring slot and window count
   if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
   DeviceGuard g(b->device);
@@ -1162,6 +1179,7 @@ int llampc_plan_exchange(llampc_bank* b, const llampc_plan_in* in, void* d_local
   int rc = check_plan_in(b, in);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding: call llampc_plan_wait");
   DeviceGuard g(b->device);
   hipStream_t s = pick_stream(b, stream);
@@ -1235,14 +1253,56 @@ struct llampc_ctl {
   llampc_mailbox* mb = nullptr;
   double* d_gparams = nullptr;           // [6][n_global]
   int64_t n_global = 0;
+  // armed launches (llampc_ctl_set_prelaunch): the next tick's launch is enqueued behind this
+  // one and waits for x_t on the doorbell (CtlLaunch.door)
+  bool prelaunch = false;
+  bool armed = false;
+  bool arm_next = false;                 // arm the next tick in llampc_ctl_wait (before its spin)
+  uint64_t* h_door = nullptr;            // pinned: kCtlDoorWords tagged words (CtlLaunch.door)
+  uint64_t* d_door = nullptr;            //   its device alias
+  uint64_t* d_door_dev = nullptr;        // block 0's device copy (CtlLaunch.door_dev)
+  uint32_t door_ctr = 0;                 // never reused: a cancelled word cannot match a later launch
+  std::chrono::steady_clock::time_point arm_t{};
+  struct Prep {                          // a prepared tick: its launch and what it commits
+    CtlLaunch L{};
+    int lpm = 4;
+    size_t lds = 0;
+    uint64_t hs = 0;
+    uint32_t seq = 0, px_seq = 0;
+    int64_t t = 0;
+    bool do_lb = false;
+    int32_t count = 0;
+  } arm;
   std::mutex mu;
 };
+
+// An armed launch waits at most kArmBound for its doorbell; the host fires it only while it is
+// younger than kArmFresh (else cancels it and launches the tick normally), so the launch
+// cannot expire between the host's check and its store short of a ~1 s stall of that thread.
+constexpr double kArmBoundS = 2.0;
+constexpr double kArmFreshS = 0.5;
+
+static void ctl_cancel(llampc_ctl* c) {
+  if (!c || !c->armed) return;
+  __atomic_store_n(&c->h_door[kCtlDoorWords - 1], ((uint64_t)c->arm.L.door_seq << 32) | kCtlDoorCancel,
+                   __ATOMIC_RELEASE);
+  // its completion number is spent: a launch that expired before the cancel has stored it
+  // (with kCtlTagExpired) into the tag the next tick's wait reads
+  c->hseq = c->arm.hs;
+  c->armed = false;
+  if (c->b && c->b->armed == c) c->b->armed = nullptr;
+}
+
+static void bank_disarm(llampc_bank* b) {
+  if (b && b->armed) ctl_cancel(b->armed);
+}
 
 // A failed controller tick (a wait that gave up, or a completion that never arrived): once the
 // stream has drained, the look-back ticket is zeroed so the next launch's ticket_last counts
 // from 0.  The tick still consumed its step on the device (the window slot, the tick number);
 // the Python controller refuses further ticks until it is rebuilt (LLAMPC.tick).
 static int ctl_recover(llampc_ctl* c) {
+  ctl_cancel(c);                         // an armed launch behind the failed one exits at once
   HIP_TRY(hipStreamSynchronize(c->b->stream));
   HIP_TRY(hipMemsetAsync(c->d_tickets, 0, sizeof(unsigned), c->b->stream));
   HIP_TRY(hipStreamSynchronize(c->b->stream));
@@ -1253,15 +1313,17 @@ extern "C" {
 
 int llampc_ctl_destroy(llampc_ctl* c) {
   if (!c) return LLAMPC_OK;
+  ctl_cancel(c);
   {
     DeviceGuard g(c->b ? c->b->device : 0);
     if (c->b && c->b->stream) (void)hipStreamSynchronize(c->b->stream);
     void* d[] = {c->d_st, c->d_pts, c->d_sel_tag, c->d_slot_tag, c->d_tickets, c->d_dbg, c->d_znoise, c->d_ztag,
-                 c->d_gparams};
+                 c->d_gparams, c->d_door_dev};
     for (void* p : d)
       if (p) (void)hipFree(p);
     if (c->h_out) (void)hipHostFree(c->h_out);
     if (c->h_tag) (void)hipHostFree(c->h_tag);
+    if (c->h_door) (void)hipHostFree(c->h_door);
   }
   delete c;
   return LLAMPC_OK;
@@ -1301,16 +1363,20 @@ int llampc_ctl_create(llampc_bank* b, const llampc_ctl_cfg* cfg, const double* p
   if ((rc = dev_alloc(&c->d_st, 1)) || (rc = dev_alloc(&c->d_pts, 3 * (size_t)np - 1)) ||
       (rc = dev_alloc(&c->d_sel_tag, kCtlSlotsMax)) || (rc = dev_alloc(&c->d_slot_tag, 4 * (size_t)kCtlSlotsMax)) ||
       (rc = dev_alloc(&c->d_tickets, 1)) || (rc = dev_alloc(&c->d_znoise, 4 * (size_t)k.C * k.H)) ||
-      (rc = dev_alloc(&c->d_ztag, 2)))
+      (rc = dev_alloc(&c->d_ztag, 2)) || (rc = dev_alloc(&c->d_door_dev, 16)))
     return cleanup(rc);
   if (k.debug_inputs && (rc = dev_alloc(&c->d_dbg, 2 * (size_t)(k.H + 1) + 2 * (size_t)k.C * k.H))) return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&c->h_out), sizeof(llampc_ctl_out),
                     hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&c->h_tag), 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_tag), 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_door), 16 * sizeof(uint64_t),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
     return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(controller record) failed"));
   *c->h_tag = 0;
+  for (int j = 0; j < 16; ++j) c->h_door[j] = 0;
   if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_out), c->h_out, 0) != hipSuccess ||
-      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_tag), c->h_tag, 0) != hipSuccess)
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_tag), c->h_tag, 0) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_door), c->h_door, 0) != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "hipHostGetDevicePointer(controller record) failed"));
   CtlState st{};
   st.mu_pred = std::nan("");
@@ -1321,20 +1387,19 @@ int llampc_ctl_create(llampc_bank* b, const llampc_ctl_cfg* cfg, const double* p
       hipMemset(c->d_sel_tag, 0, kCtlSlotsMax * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->d_slot_tag, 0, 4 * kCtlSlotsMax * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->d_tickets, 0, sizeof(unsigned)) != hipSuccess ||
-      hipMemset(c->d_ztag, 0, 2 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      hipMemset(c->d_ztag, 0, 2 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->d_door_dev, 0, 16 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "controller upload failed"));
   *out = c;
   return LLAMPC_OK;
 }
 
-int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
-  if (!c || !x_t) return fail(LLAMPC_E_ARG, "controller/x_t is NULL");
-  std::lock_guard<std::mutex> lc(c->mu);
-  if (c->pending) return fail(LLAMPC_E_STATE, "a controller tick is outstanding: call llampc_ctl_wait");
+}  // extern "C"
+
+// The launch of tick c->t (x_t null: armed — the doorbell carries x_t) and what it commits
+// (ctl_commit), from the host's copy of the controller and bank state.
+static int ctl_prepare(llampc_ctl* c, const double* x_t, llampc_ctl::Prep& P) {
   llampc_bank* b = c->b;
-  std::lock_guard<std::mutex> lk(b->mu);
-  if (b->async_pending) return fail(LLAMPC_E_STATE, "an async plan tick is outstanding on the bank");
-  DeviceGuard g(b->device);
   const llampc_ctl_cfg& k = c->cfg;
   const int64_t t = c->t;
   const int32_t W = b->W;
@@ -1427,7 +1492,7 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   L.tick = (uint64_t)t;
   L.seed = k.seed;
   for (int j = 0; j < 6; ++j) {
-    L.x_t[j] = x_t[j];
+    L.x_t[j] = x_t ? x_t[j] : 0.0;      // armed (x_t null): the doorbell carries it
     L.nominal[j] = k.nominal[j];
   }
   const double sqrt3 = std::sqrt(3.0);
@@ -1451,7 +1516,13 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   L.do_lb = do_lb;
   L.warm = warm;
   L.use_mu = t > W + 1;                  // rt.py:278
-  if (!c->hint_ok) {                     // after a failed wait: the state itself
+  if (!x_t) {                            // armed: the launch reads projidx / mu-hat from the state
+    L.door = c->d_door;
+    L.door_dev = c->d_door_dev;
+    c->door_ctr = c->door_ctr == 0xFFFFFFFFu ? 1u : c->door_ctr + 1u;
+    L.door_seq = c->door_ctr;
+    L.door_bound = (uint32_t)(kArmBoundS * 1e8 / 65536.0) + 1;
+  } else if (!c->hint_ok) {              // after a failed wait: the state itself
     CtlState hs{};
     HIP_TRY(hipStreamSynchronize(b->stream));
     HIP_TRY(hipMemcpy(&hs, c->d_st, sizeof hs, hipMemcpyDeviceToHost));
@@ -1459,8 +1530,10 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
     c->hint_mu = hs.mu_pred;
     c->hint_ok = true;
   }
-  L.p0_walk = c->hint_p0;
-  L.br_walk = mu_bracket(b->rl_mus.data(), b->rl_M, L.use_mu ? c->hint_mu : L.mu_fixed);   // rt.py:278-282
+  if (x_t) {
+    L.p0_walk = c->hint_p0;
+    L.br_walk = mu_bracket(b->rl_mus.data(), b->rl_M, L.use_mu ? c->hint_mu : L.mu_fixed);   // rt.py:278-282
+  }
   L.full = full;
   L.nslots = warm ? 1 : k.K + 1;
   L.G = lookahead_group(k.C);
@@ -1474,11 +1547,9 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   // sharded: the exchange runs on every tick whose window is full (the same ticks on every
   // rank); the selection is global, the look-ahead reads the replicated global table
   L.sel_goff = b->goff;
-  std::unique_lock<std::mutex> lm;
   uint32_t px_seq = 0;
-  if (c->mb) {
+  if (c->mb) {                           // (the caller holds mb->mu)
     llampc_mailbox* mb = c->mb;
-    lm = std::unique_lock<std::mutex>(mb->mu);
     if (!mb->box_synced) {
       HIP_TRY(hipMemcpy(mb->d_box, mb->box, kPeerMax * sizeof(uint64_t*), hipMemcpyHostToDevice));
       mb->box_synced = true;
@@ -1506,21 +1577,90 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   if (lds > 160 * 1024) return fail(LLAMPC_E_ARG, "controller tick needs %zu B of LDS (> 160 KiB)", lds);
   if (L.s4) L.poll_off = poll_s4;
   lds = std::max<size_t>(lds, 82 * 1024); // one block per CU, as the plan launch (sc1 hand-offs)
+  P.L = L;
+  P.lpm = lpm;
+  P.lds = lds;
+  P.hs = hs;
+  P.seq = seq;
+  P.px_seq = px_seq;
+  P.t = t;
+  P.do_lb = do_lb;
+  P.count = count;
+  return LLAMPC_OK;
+}
+
+// The host state after tick P.t was enqueued (or its armed launch fired).
+static void ctl_commit(llampc_ctl* c, const llampc_ctl::Prep& P) {
+  llampc_bank* b = c->b;
+  c->hseq = P.hs;
+  c->seq = P.seq;
+  if (P.L.px_G) c->mb->seq = P.px_seq;   // committed after the launch was enqueued (next_seq)
+  c->t = P.t + 1;
+  c->pending = true;
+  c->pend_seq = P.hs;
+  b->launches++;
+  if (P.do_lb) {
+    b->slot = (b->slot + 1) % b->W;
+    b->count = P.count;
+  }
+}
+
+// Enqueues tick c->t's launch armed (llampc_ctl_set_prelaunch): it runs behind the tick in
+// flight and waits for the doorbell.  Not with a sharded exchange.
+static int ctl_arm(llampc_ctl* c) {
+  if (c->armed || c->mb) return LLAMPC_OK;
+  llampc_ctl::Prep P;
+  int rc = ctl_prepare(c, nullptr, P);
+  if (rc) return rc;
+  HIP_TRY(launch_ctl(P.L, P.lpm, P.lds, c->b->stream));
+  c->arm = P;
+  c->armed = true;
+  c->arm_t = std::chrono::steady_clock::now();
+  c->b->armed = c;
+  return LLAMPC_OK;
+}
+
+extern "C" {
+
+int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
+  if (!c || !x_t) return fail(LLAMPC_E_ARG, "controller/x_t is NULL");
+  std::lock_guard<std::mutex> lc(c->mu);
+  if (c->pending) return fail(LLAMPC_E_STATE, "a controller tick is outstanding: call llampc_ctl_wait");
+  llampc_bank* b = c->b;
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (b->async_pending) return fail(LLAMPC_E_STATE, "an async plan tick is outstanding on the bank");
+  DeviceGuard g(b->device);
+  if (c->armed) {
+    const double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - c->arm_t).count();
+    if (age < kArmFreshS && c->arm.t == c->t) {
+      // fire: every word tagged (block 0 polls until all carry the tag: no order needed)
+      const uint64_t tg = (uint64_t)c->arm.L.door_seq << 32;
+      for (int j = 0; j < 6; ++j) {
+        uint64_t w;
+        std::memcpy(&w, &x_t[j], 8);
+        __atomic_store_n(&c->h_door[2 * j], tg | (w >> 32), __ATOMIC_RELAXED);
+        __atomic_store_n(&c->h_door[2 * j + 1], tg | (w & 0xFFFFFFFFull), __ATOMIC_RELAXED);
+      }
+      __atomic_store_n(&c->h_door[kCtlDoorWords - 1], tg | kCtlDoorFire, __ATOMIC_RELEASE);
+      c->armed = false;
+      b->armed = nullptr;
+      ctl_commit(c, c->arm);
+      c->arm_next = c->prelaunch;
+      return LLAMPC_OK;
+    }
+    ctl_cancel(c);                       // stale: this tick launches normally
+  }
+  std::unique_lock<std::mutex> lm;
+  if (c->mb) lm = std::unique_lock<std::mutex>(c->mb->mu);
+  llampc_ctl::Prep P;
+  int rc = ctl_prepare(c, x_t, P);
+  if (rc) return rc;
   {
     TimedLaunch tl(b, 0, b->stream);
-    HIP_TRY(launch_ctl(L, lpm, lds, b->stream));
+    HIP_TRY(launch_ctl(P.L, P.lpm, P.lds, b->stream));
   }
-  c->hseq = hs;
-  c->seq = seq;
-  if (L.px_G) c->mb->seq = px_seq;      // committed after the launch was enqueued (next_seq)
-  c->t = t + 1;
-  c->pending = true;
-  c->pend_seq = hs;
-  b->launches++;
-  if (do_lb) {
-    b->slot = (b->slot + 1) % W;
-    b->count = count;
-  }
+  ctl_commit(c, P);
+  c->arm_next = c->prelaunch;
   return LLAMPC_OK;
 }
 
@@ -1531,11 +1671,26 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
   c->pending = false;
   c->hint_ok = false;                    // until this tick's record is read
   DeviceGuard g(c->b->device);
+  if (c->arm_next) {
+    // the next tick's launch, armed behind this one — here rather than in tick_async, so that
+    // several controllers' ticks (two tracks) are all rung before any launch call; the launch
+    // call overlaps this tick's device time.  A failed arm only turns prelaunch off.
+    c->arm_next = false;
+    std::lock_guard<std::mutex> lk(c->b->mu);
+    if (!c->b->async_pending && ctl_arm(c) != LLAMPC_OK) c->prelaunch = false;
+  }
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t spins = 0;
-  while (__atomic_load_n(c->h_tag, __ATOMIC_ACQUIRE) != c->pend_seq) {
+  uint64_t tag;
+  while ((tag = __atomic_load_n(c->h_tag, __ATOMIC_ACQUIRE)) != c->pend_seq) {
     __builtin_ia32_pause();
+    if (tag == (c->pend_seq | kCtlTagExpired)) {   // an armed launch that never saw its doorbell
+      (void)ctl_recover(c);
+      return fail(LLAMPC_E_DEVICE, "controller tick %llu: the armed launch expired before its doorbell",
+                  (unsigned long long)c->pend_seq);
+    }
     if ((++spins & 0xFFF) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      ctl_cancel(c);
       HIP_TRY(hipStreamSynchronize(c->b->stream));
       if (__atomic_load_n(c->h_tag, __ATOMIC_ACQUIRE) == c->pend_seq) break;
       (void)ctl_recover(c);
@@ -1553,6 +1708,24 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
   return LLAMPC_OK;
 }
 
+int llampc_ctl_set_prelaunch(llampc_ctl* c, int32_t on) {
+  if (!c) return fail(LLAMPC_E_ARG, "controller is NULL");
+  std::lock_guard<std::mutex> lc(c->mu);
+  if (on && c->mb) return fail(LLAMPC_E_STATE, "prelaunch is not available with a sharded exchange");
+  llampc_bank* b = c->b;
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  c->prelaunch = on != 0;
+  c->arm_next = c->prelaunch && c->pending;   // a tick in flight: armed by its wait
+  if (!c->prelaunch) {
+    ctl_cancel(c);
+    return LLAMPC_OK;
+  }
+  if (c->pending || b->async_pending) return LLAMPC_OK;
+  bank_disarm(b);                         // another controller's launch on this bank
+  return ctl_arm(c);
+}
+
 int llampc_ctl_tick(llampc_ctl* c, const double* x_t, llampc_ctl_out* out) {
   if (!out) return fail(LLAMPC_E_ARG, "out is NULL");
   int rc = llampc_ctl_tick_async(c, x_t);
@@ -1567,6 +1740,7 @@ int llampc_ctl_reference(llampc_ctl* c, const double* x0, double v0, int32_t H, 
   std::lock_guard<std::mutex> lc(c->mu);
   llampc_bank* b = c->b;
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   DeviceGuard g(b->device);
   const size_t n = 2 * (size_t)(H + 1) + 2;
   double* d = nullptr;
@@ -1618,6 +1792,8 @@ int llampc_ctl_set_exchange(llampc_ctl* c, llampc_mailbox* mb, const double* gpa
   std::lock_guard<std::mutex> lc(c->mu);
   if (c->pending) return fail(LLAMPC_E_STATE, "a controller tick is outstanding");
   if (c->t != 0) return fail(LLAMPC_E_STATE, "set the exchange before the first tick");
+  ctl_cancel(c);                         // no armed launches with an exchange
+  c->prelaunch = false;
   DeviceGuard g(b->device);
   double* d = nullptr;
   if (int rc = dev_alloc(&d, 6 * (size_t)n_global)) return rc;
@@ -1668,6 +1844,7 @@ int llampc_ctl_inputs(llampc_ctl* c, double* xref, double* U) {
   if (!c->d_dbg) return fail(LLAMPC_E_STATE, "controller created without debug_inputs");
   std::lock_guard<std::mutex> lc(c->mu);
   DeviceGuard g(c->b->device);
+  ctl_cancel(c);                         // an armed launch would hold the stream (re-armed next tick)
   HIP_TRY(hipStreamSynchronize(c->b->stream));
   const size_t nx = 2 * (size_t)(c->cfg.H + 1), nu = 2 * (size_t)c->cfg.C * c->cfg.H;
   HIP_TRY(hipMemcpy(xref, c->d_dbg, nx * sizeof(double), hipMemcpyDeviceToHost));
@@ -1780,6 +1957,7 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   std::lock_guard<std::mutex> lp(p->mu);
   llampc_bank* b = p->b;
   std::lock_guard<std::mutex> lk(b->mu);
+  bank_disarm(b);
   if (b->async_pending) return fail(LLAMPC_E_STATE, "an async tick is outstanding on the bank");
   DeviceGuard g(b->device);
   const llampc_nlp_cfg& k = p->cfg;

@@ -80,8 +80,8 @@ static_assert(offsetof(llampc_ctl_out, tick) == sizeof(llampc_plan_out) &&
 // barrier, 3 selection, 4 rolled out, 5 published; look-back blocks: 0 entry, 6 scored,
 // 7 lb_final done (ticket winner), 8 slots polled, 12 top-K / sequence stores issued, 13 the
 // record words computed, 11 record stores issued, 9 record written; look-ahead prologue: 14 the
-// mu bracket known, 15 the tables' LDS stores issued.
-static __device__ unsigned long long g_ctl_ph[64][16];
+// mu bracket known, 15 the tables' LDS stores issued; 16 an armed launch's doorbell seen.
+static __device__ unsigned long long g_ctl_ph[64][24];
 #define CTL_STAMP(blk, slot)                                                                   \
   do {                                                                                         \
     if (threadIdx.x == 0 && (blk) < 64) g_ctl_ph[blk][slot] = __builtin_amdgcn_s_memrealtime(); \
@@ -99,6 +99,57 @@ namespace {
 
 __device__ __forceinline__ bool ctl_late(uint64_t t0, uint32_t poll) {
   return __builtin_amdgcn_s_memrealtime() - t0 > ((uint64_t)poll << 16);
+}
+
+// An armed launch's doorbell (CtlLaunch.door): thread 0 polls the kCtlDoorWords tagged words —
+// block 0 the pinned host copy (system-scope loads), every other block the device copy block 0
+// makes — until the status word carries door_seq (and, to fire, every x_t half does).  Returns,
+// block-uniform after the barrier: kCtlDoorFire (x_t in xl), kCtlDoorCancel, kCtlDoorExpired.
+__device__ __forceinline__ int ctl_door(const CtlLaunch& c, double* xl, int* res) {
+  if (threadIdx.x == 0) {
+    const bool host = blockIdx.x == 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t w[kCtlDoorWords];
+    int r;
+    for (;;) {
+      if (host) {
+#pragma unroll
+        for (int q = 0; q < kCtlDoorWords; ++q)
+          w[q] = __hip_atomic_load(&c.door[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+#pragma unroll
+        for (int q = 0; q < kCtlDoorWords; ++q) w[q] = ld_wt(&c.door_dev[q]);
+      }
+      const uint64_t sw = w[kCtlDoorWords - 1];
+      if (tag_ok(sw, c.door_seq)) {
+        r = (int)(uint32_t)sw;
+        if (r != (int)kCtlDoorFire) break;
+        int all = 1;
+#pragma unroll
+        for (int q = 0; q < kCtlDoorWords - 1; ++q) all &= (int)tag_ok(w[q], c.door_seq);
+        if (all) break;
+      }
+      // block 0 gives up at the bound; the others wait twice as long for its verdict
+      if (ctl_late(t0, host ? c.door_bound : 2 * c.door_bound)) {
+        r = (int)kCtlDoorExpired;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (host) {                         // the verdict for the other blocks
+      if (r == (int)kCtlDoorExpired) w[kCtlDoorWords - 1] = tag_word(c.door_seq, kCtlDoorExpired);
+#pragma unroll
+      for (int q = 0; q < kCtlDoorWords; ++q) st_wt(&c.door_dev[q], w[q]);
+    }
+    if (r == (int)kCtlDoorFire) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) xl[j] = __longlong_as_double((long long)join_words(w[2 * j], w[2 * j + 1]));
+    }
+    *res = r;
+  }
+  CTL_STAMP(blockIdx.x, 16);
+  __syncthreads();
+  return *res;
 }
 
 // The raw candidates [C][H][2] (before the rate clip) by threads t0 + i stride, i >= 0: from
@@ -154,7 +205,8 @@ __device__ __forceinline__ void ctl_draw_next(const CtlLaunch& c, int t0, int st
 // ------------------------------------------------------------------------------------
 // The completing block (after lb_final<true>, or alone on ticks without a look-back).
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* smem, const CtlSel& cs) {
+__device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* smem, const CtlSel& cs,
+                                             const double* xt) {
 #pragma clang fp contract(off)
   const int tid = threadIdx.x;
   const int H = c.la.H, C = c.la.C;
@@ -176,7 +228,7 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   const int p0 = st->projidx;
   const int segs = ctl_segments(p0, c.np);
   if (tid < kCtlSegs && tid < segs)                                // track.py:155-157
-    pdist[tid] = ref_project_dist(c.x_t[0], c.x_t[1], c.pts[p0 + tid], c.pts[c.np + p0 + tid],
+    pdist[tid] = ref_project_dist(xt[0], xt[1], c.pts[p0 + tid], c.pts[c.np + p0 + tid],
                                   c.pts[p0 + tid + 1], c.pts[c.np + p0 + tid + 1]);
   const double up0 = st->u_prev[0], up1 = st->u_prev[1];
   {
@@ -223,9 +275,9 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   // the current model (this block writes it after the poll): loaded now, off the tail
   const int64_t cur_model = (tid < 64 && warm) ? st->current_model : 0;
   // x_prev: every look-back block has read it (this block holds the last ticket) and the
-  // look-ahead blocks never do — stored now, so no load of x_t (kernel argument, global)
-  // sits behind the record's host stores after the poll
-  if (tid < 6) st->x_prev[tid] = c.x_t[tid];
+  // look-ahead blocks never do — stored now, so no load of x_t sits behind the record's host
+  // stores after the poll
+  if (tid < 6) st->x_prev[tid] = xt[tid];
   // the record's scalar kernel arguments, loaded (and kept) before the poll: the tail used
   // to wait for them one by one after it
   int32_t a_wc = c.fin.window_count, a_full = c.fin.full, a_K = c.K, a_warm = c.warm, a_lap = c.lap_projidx;
@@ -713,17 +765,21 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   double* x0 = reinterpret_cast<double*>(smem + L.misc + 640);            // [6] x_t (no kernarg address taken)
   int* arrived = reinterpret_cast<int*>(smem + L.misc + 688);              // waves 1-3 (ctl_group_sync)
   double* s4 = reinterpret_cast<double*>(smem + L.s4);                      // s4: the staged inputs
+  int* door_res = reinterpret_cast<int*>(smem + L.misc + 720);
   CTL_STAMP(blockIdx.x, 0);
-  if (tid < 6) x0[tid] = c.x_t[0 + tid];
+  const bool armed = c.door != nullptr;
+  if (!armed && tid < 6) x0[tid] = c.x_t[0 + tid];
   if (tid == 0) *arrived = 0;
   const CtlState* st = c.st;
   const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
   // rt.py:278-282: projidx and the mu bracket (mu-hat or the fixed mu) come from the host's
   // copy of the state (CtlLaunch.p0_walk / br_walk): the tables' loads follow the kernel
-  // arguments directly (profiles/r04/s4/ctl_phases_prologue.txt: 2.5 us to the bracket before)
-  const int p0 = c.p0_walk;
+  // arguments directly (profiles/r04/s4/ctl_phases_prologue.txt: 2.5 us to the bracket before).
+  // An armed launch reads the state itself: the previous tick ended before it started, and
+  // the loads sit before the doorbell.
+  const int p0 = armed ? st->projidx : c.p0_walk;
   const double scale = c.use_mu ? c.v_factor : c.scale_fixed;
-  const MuBracket br = c.br_walk;
+  const MuBracket br = armed ? mu_bracket(rl.mus, rl.M, c.use_mu ? st->mu_pred : c.mu_fixed) : c.br_walk;
   CTL_STAMP(blockIdx.x, 14);
   // waves 1-3: this tick's candidate variates (the previous tick's completion drew them) are
   // loaded now, their latency under the tables' (used only when their tag matches: ctl_draw)
@@ -745,7 +801,18 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   //     project_fast of x_t on raceline[:, p0 : p0 + 10] (track.py:147-160)
   cs_stage(rl, br, kn, spd);
   CTL_STAMP(blockIdx.x, 15);
-  const int segs = cs_project(c.pts, c.np, p0, c.x_t[0], c.x_t[1], dist);
+  double px = 0.0, py = 0.0, pv = 0.0;
+  if (armed) {                          // x_t: the doorbell (x0 in LDS after its barrier)
+    if (ctl_door(c, x0, door_res) != (int)kCtlDoorFire) return;
+    px = x0[0];
+    py = x0[1];
+    pv = x0[3];
+  } else {
+    px = c.x_t[0];
+    py = c.x_t[1];
+    pv = c.x_t[3];
+  }
+  const int segs = cs_project(c.pts, c.np, p0, px, py, dist);
   __syncthreads();
   CTL_STAMP(blockIdx.x, 1);
   // (c) wave 0 walks ConstantSpeed from the projection (planner.py:24-65) while waves 1-3
@@ -753,8 +820,7 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   const double up0 = st->u_prev[0], up1 = st->u_prev[1];
   if (tid < 64) {
     double vr;
-    (void)cs_walk_wave(rl, br, kn, spd, c.prefix, dist, segs, p0, c.x_t[0], c.x_t[1], c.x_t[3], scale, c.la.Ts, H,
-                       sx, &vr);
+    (void)cs_walk_wave(rl, br, kn, spd, c.prefix, dist, segs, p0, px, py, pv, scale, c.la.Ts, H, sx, &vr);
     CTL_STAMP(blockIdx.x, 10);
   } else {
     if (zfit && c.ztag[(int)(c.tick & 1)] == c.tick + 1) {          // launch-uniform
@@ -993,16 +1059,28 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
             reinterpret_cast<double*>(pl + 2624), reinterpret_cast<double*>(pl + 3200),
             reinterpret_cast<int32_t*>(pl + 3520)};
   if (threadIdx.x == 0) *cs.xlate = 0;
+  // x_t through LDS (pointing into the kernel argument itself would make the compiler copy the
+  // whole argument to scratch): the kernel argument, or an armed launch's doorbell — after the
+  // look-back's step, which needs only the state (lookback_block<ARMED>)
+  double* xl = reinterpret_cast<double*>(pl + 3072);
+  auto door = [&]() -> const double* {
+    if (c.door) {
+      const int r = ctl_door(c, xl, reinterpret_cast<int*>(pl + 3584));
+      if (r != (int)kCtlDoorFire) {     // cancelled or expired: nothing touched
+        if (r == (int)kCtlDoorExpired && blk == 0 && threadIdx.x == 0)
+          __hip_atomic_store(c.host_tag, c.host_seq | kCtlTagExpired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return nullptr;
+      }
+    } else {
+      if (threadIdx.x < 6) xl[threadIdx.x] = c.x_t[0 + threadIdx.x];
+      __syncthreads();
+    }
+    return xl;
+  };
   if (c.do_lb) {
-    // x_now: this tick's x_t through LDS (pointing into the kernel argument itself would make
-    // the compiler copy the whole argument to scratch)
-    double* xl = reinterpret_cast<double*>(pl + 3072);
-    if (threadIdx.x < 6) xl[threadIdx.x] = c.x_t[0 + threadIdx.x];
-    __syncthreads();
     LookbackLaunch lb = c.lb;           // x_prev / u_prev: the state
-    lb.x_now = xl;
     CTL_STAMP(blk, 0);
-    lookback_block(lb, blk, sc);
+    if (!lookback_block<true>(lb, blk, sc, door)) return;
     CTL_STAMP(blk, 6);
     if (!ticket_last(&c.tickets[0], (unsigned)c.nb_lb, flag)) return;
     if (c.full) {
@@ -1016,8 +1094,10 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
     }
     CTL_STAMP(blk, 7);
     __syncthreads();
+  } else if (!door()) {                 // ticks without a look-back: block 0 only completes
+    return;
   }
-  ctl_complete(c, smem, cs);
+  ctl_complete(c, smem, cs, xl);
 }
 
 // llampc_ctl_reference: ConstantSpeed alone (one block), into out = xref [2][H+1], projidx,

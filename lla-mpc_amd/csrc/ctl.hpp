@@ -338,7 +338,21 @@ struct CtlLaunch {
   int32_t px_G, px_rank;
   uint32_t px_seq;            // the mailbox's tick number of this exchange
   uint32_t px_bound;          // the peers' wait bound, units of 2^16 s_memrealtime ticks
+  // armed launch (door != null, llampc_ctl_set_prelaunch): enqueued behind the previous tick,
+  // it runs its x_t-independent prologue and then waits for the host's doorbell: kCtlDoorWords
+  // tagged words (tag door_seq) in pinned memory — x_t as 12 32-bit halves, then the status
+  // (kCtlDoorFire / kCtlDoorCancel).  Block 0 alone polls the pinned words (many blocks reading
+  // host memory queue behind each other on PCIe) and copies them to door_dev in device memory,
+  // which the other blocks poll.  Block 0 gives up after door_bound (2^16 s_memrealtime units):
+  // it then posts kCtlDoorExpired, stores host_seq | kCtlTagExpired, and every block exits
+  // untouched.  projidx and the mu bracket then come from the state.
+  const uint64_t* door;
+  uint64_t* door_dev;
+  uint32_t door_seq, door_bound;
 };
+constexpr int kCtlDoorWords = 13;
+constexpr uint32_t kCtlDoorFire = 1, kCtlDoorCancel = 2, kCtlDoorExpired = 3;
+constexpr uint64_t kCtlTagExpired = 1ull << 62;
 
 // llampc_ctl_reference's launch: ConstantSpeed alone (planner.py:12-67) on the device.
 struct CsLaunch {

@@ -490,52 +490,96 @@ __device__ __forceinline__ void wave_topk_rank(const LookbackLaunch& a, double w
 // RK4 step from (x_{t-1}, u_{t-1}), 4-state MSE against x_t, in-place ring write, window
 // mean in NumPy's pairwise order; then the block's argmin and its SORTED top-K list.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk, const Scratch& sc) {
+// ARMED (the controller, ctl.hip): x_t comes from door() — the LDS copy of x_t, or null when
+// the launch is cancelled (lookback_block then returns false) — and with one model per lane
+// the RK4 step runs BEFORE it: the step needs only the state's (x_{t-1}, u_{t-1}), x_t enters
+// with the error, so an armed launch has the step done when its doorbell rings.
+template <bool ARMED = false, typename Door = int>
+__device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk, const Scratch& sc, Door door = 0) {
   LB_STAMP(blk, 0);
   const int64_t base = (int64_t)blk * kBlock * a.R;
   const fm::FmK K = fm::FmK::load();
   bool ubad = false;
   const Input uf = make_input_fast(a.u_prev[0], a.u_prev[1], K, ubad);
   double wm0 = 0.0;                     // R == 1 keeps the window mean in a register
+  const double* x_now = a.x_now;
+  double xp[4] = {0.0, 0.0, 0.0, 0.0};  // ARMED, R == 1: the step before the doorbell
+  Tire tp{};
+  WinPre wpp{0.0, 0.0, 0.0, 0.0};
+  bool bp = false, pre = false;
+  if constexpr (ARMED) {
+    if (a.R == 1) {                     // launch-uniform
+      const int64_t n = base + threadIdx.x;
+      if (n < a.n) {
+        double x[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
+        tp = load_tire(a.params, a.n, n);
+        const int o = (a.slot + 1 == a.W) ? 0 : a.slot + 1;
+        if (a.full) wpp = win_pre(a.ring, a.n, n, o, a.W);
+        const StageK sk = make_stage<1>(a.veh, tp, 0);
+        Dom dm;
+        dm.init();
+        step_fast<0, 1>(a.veh, tp, sk, x, uf, a.Ts, K, dm);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xp[j] = x[j];
+        bp = (int)ubad | (int)!sk.sok | (int)!dm.ok();
+      }
+      pre = true;
+    }
+    x_now = door();
+    if (!x_now) return false;
+  }
   for (int r = 0; r < a.R; ++r) {
     const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
     if (n >= a.n) break;
     double x[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
-    const Tire t = load_tire(a.params, a.n, n);
-    const int o = (a.slot + 1 == a.W) ? 0 : a.slot + 1;     // the window's oldest slot
+    Tire t;
     WinPre wp{0.0, 0.0, 0.0, 0.0};
-    if (a.full) wp = win_pre(a.ring, a.n, n, o, a.W);      // launch-uniform; under the step
-    // model.py:32-40, one RK4 step: the fast stage; a lane whose operands leave the fast
-    // cores' domains redoes the step with the general functions (as the look-ahead does)
-    const StageK sk = make_stage<1>(a.veh, t, 0);
-    Dom dm;
-    dm.init();
-    step_fast<0, 1>(a.veh, t, sk, x, uf, a.Ts, K, dm);
+    bool bad;
+    if (ARMED && pre) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = xp[j];
+      t = tp;
+      wp = wpp;
+      bad = bp;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
+      t = load_tire(a.params, a.n, n);
+      const int o = (a.slot + 1 == a.W) ? 0 : a.slot + 1;     // the window's oldest slot
+      if (a.full) wp = win_pre(a.ring, a.n, n, o, a.W);      // launch-uniform; under the step
+      // model.py:32-40, one RK4 step: the fast stage; a lane whose operands leave the fast
+      // cores' domains redoes the step with the general functions (as the look-ahead does)
+      const StageK sk = make_stage<1>(a.veh, t, 0);
+      Dom dm;
+      dm.init();
+      step_fast<0, 1>(a.veh, t, sk, x, uf, a.Ts, K, dm);
 #ifdef LLAMPC_LB_TWICE
-    // diagnostic (stamps build only): the same step again, warm — its cycles against the first's
-    // split the first step's time into the code's cold fetch + the operands' loads vs the issue
-    if (r == 0) {
-      LB_STAMP(blk, 4);
-      double x2[6];
-      for (int j = 0; j < 6; ++j) x2[j] = a.x_prev[j];
-      Dom d2;
-      d2.init();
-      step_fast<0, 1>(a.veh, t, sk, x2, uf, a.Ts, K, d2);
-      asm volatile("" ::"v"(x2[0]), "v"(x2[1]), "v"(x2[2]), "v"(x2[3]));
-      LB_STAMP(blk, 5);
-    }
+      // diagnostic (stamps build only): the same step again, warm — its cycles against the first's
+      // split the first step's time into the code's cold fetch + the operands' loads vs the issue
+      if (r == 0) {
+        LB_STAMP(blk, 4);
+        double x2[6];
+        for (int j = 0; j < 6; ++j) x2[j] = a.x_prev[j];
+        Dom d2;
+        d2.init();
+        step_fast<0, 1>(a.veh, t, sk, x2, uf, a.Ts, K, d2);
+        asm volatile("" ::"v"(x2[0]), "v"(x2[1]), "v"(x2[2]), "v"(x2[3]));
+        LB_STAMP(blk, 5);
+      }
 #endif
-    double s = sq_err4(x, a.x_now);                       // rt.py:349 mean over 4 states
+      bad = (int)ubad | (int)!sk.sok | (int)!dm.ok();
+    }
+    double s = sq_err4(x, x_now);                         // rt.py:349 mean over 4 states
     // the domain once per step; a NaN operand reaches x[0..3] (the stage-4 chains feed x[3])
-    bool bad = (int)ubad | (int)!sk.sok | (int)!dm.ok() | (int)!(s <= __DBL_MAX__);
+    bad = (int)bad | (int)!(s <= __DBL_MAX__);
     if (__builtin_expect(__any(bad), 0)) {
       if (bad) {
 #pragma unroll
         for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
         rk4_step(a.veh, t, x, make_input(a.u_prev[0], a.u_prev[1]), a.Ts);
-        s = sq_err4(x, a.x_now);
+        s = sq_err4(x, x_now);
       }
     }
     const double err = s / 4;
@@ -548,7 +592,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     }
   }
   LB_STAMP(blk, 1);
-  if (!a.full) return;  // launch-uniform
+  if (!a.full) return true;  // launch-uniform
 
   // per WAVE (a list): the argmin (rt.py:359 semantics) and the sorted top-K (rt.py:360
   // argsort order) of its 64*R models with branch-free wave picks — no LDS round trip, no
@@ -581,7 +625,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
     __syncthreads();
     block_topk_merge(a, blk, wl);
     LB_STAMP(blk, 3);
-    return;
+    return true;
   }
   // R > 1: K rounds of "next key after the previous pick" (NaN last, ties -> lower index)
   double lv = 0.0;
@@ -610,6 +654,7 @@ __device__ __forceinline__ void lookback_block(const LookbackLaunch& a, int blk,
   __syncthreads();
   block_topk_merge(a, blk, wl);
   LB_STAMP(blk, 3);
+  return true;
 }
 
 // Input-rate term du' R du of one step (nmpc.py:65-68, 111) and the bounds / rate
@@ -1982,6 +2027,10 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
     lookback_block(lb, lb_blk, sc);
     if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
     if (fin.full) {
+#ifdef LLAMPC_LBF_TWICE                       // diagnostic: the stamps then time a warm lb_final
+      lb_final(fin, smem);
+      __syncthreads();
+#endif
       lb_final(fin, smem);
       // host completion: lb_final's record stores are performed before any later hand-off
       // (the final block, possibly another one, publishes the host tag after them)

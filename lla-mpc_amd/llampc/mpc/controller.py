@@ -18,7 +18,10 @@ Host logic restated from the reference driver (llampc/mpc/run_nmpc_orca_llampc_r
                              candidates (Philox sampling), look-back + selection, the
                              look-ahead of the selected model and the top-K, mu-hat and the
                              controller state all on the GPU; the host passes x_t and reads
-                             the record.
+                             the record.  prelaunch=True (default): each tick's launch is
+                             enqueued during the previous tick and waits for x_t on a
+                             doorbell, having done the look-back's RK4 step (it needs only the
+                             state) — the tick rings it (llampc_ctl_set_prelaunch).
     mode="host":             the round-3 loop: host ConstantSpeed + host CandidateGenerator
                              around the fused plan launch, every (model, candidate) rolled out.
 """
@@ -159,7 +162,7 @@ class DeviceController:
 
     def __init__(self, bank: ModelBank, track, H=20, C=64, K=10, Ts=0.02, v_factor=0.9, mu_init=1.0, S=20,
                  sigma=(0.05, 0.02), seed=2, nominal6=None, cost=None, nan_policy=nat.NAN_FIRST,
-                 debug_inputs=False, lap_projidx=None):
+                 debug_inputs=False, lap_projidx=None, prelaunch=False):
         if getattr(bank, "raceline", None) is not track:
             bank.set_raceline(track)
         self.bank, self.track, self.H, self.C = bank, track, int(H), int(C)
@@ -186,6 +189,17 @@ class DeviceController:
         lib = nat.load()
         self._xp = self._x.ctypes.data
         self._f_async, self._f_wait = lib.llampc_ctl_tick_async, lib.llampc_ctl_wait
+        self.prelaunch = False
+        if prelaunch:
+            self.set_prelaunch(True)
+
+    def set_prelaunch(self, on=True):
+        """Arm every next tick (llampc_ctl_set_prelaunch): its launch is enqueued behind the
+        current one and waits for x_t on a doorbell, so the next ``tick`` only rings it — the
+        launch call and the dispatch leave the step's latency.  Any other call on the bank or
+        this controller cancels the armed launch first (the tick after it launches normally)."""
+        nat.check(nat.load().llampc_ctl_set_prelaunch(self._h, int(bool(on))))
+        self.prelaunch = bool(on)
 
     def tick(self, x_t, out=None) -> "nat.CtlOut":
         """One blocking step; ``out`` (a CtlOut) is filled and returned (a new one if None)."""
@@ -317,12 +331,13 @@ class LLAMPC:
     """Stateful LLA-MPC tick loop over a ``ModelBank`` (rt.py:269-366 without IPOPT).
 
     ``nominal``: the Pacejka parameters the warm-up ticks plan with (default ORCA(),
-    the reference's true_model / params at setup, rt.py:78-79, 207)."""
+    the reference's true_model / params at setup, rt.py:78-79, 207).  ``prelaunch``: device
+    mode's armed ticks (module docstring); results are those of launched ticks."""
 
     def __init__(self, bank: ModelBank, track, H=20, Ts=0.02, K=10, C=64, v_factor=0.9,
                  mu_init=1.0, S=20, alpha=0.08, cost=None, integrator="rk4", seed=2,
                  nan_policy=nat.NAN_FIRST, nominal: dict | None = None, mode="device",
-                 sigma=(0.05, 0.02), debug_inputs=False):
+                 sigma=(0.05, 0.02), debug_inputs=False, prelaunch=True):
         from llampc.params import ORCA
         if mode not in ("device", "host"):
             raise ValueError(f"mode={mode!r}: 'device' or 'host'")
@@ -349,6 +364,8 @@ class LLAMPC:
                                          nan_policy=nan_policy, debug_inputs=debug_inputs)
             if sharded is not None and sharded.exchange:
                 self._ctl.set_exchange(sharded)
+            elif prelaunch:
+                self._ctl.set_prelaunch(True)
         else:
             # a one-model bank: the warm-up look-ahead runs the same kernel on the nominal model
             self.nominal_bank = ModelBank(col, shared=bank.shared, W=1, device=bank.device)
@@ -370,6 +387,11 @@ class LLAMPC:
         self.u_prev = None
         self.u_seq = None
         self.last_topk = None
+
+    def set_prelaunch(self, on=True):
+        """Device mode: arm every next tick (the default; DeviceController.set_prelaunch) or not."""
+        if self._ctl is not None and not (self.sharded is not None and self.sharded.exchange):
+            self._ctl.set_prelaunch(on)
 
     def tick(self, x_t) -> PlanResult:
         """One control tick.  After the warm-up (t > W) it is ONE fused launch on the bank:

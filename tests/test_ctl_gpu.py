@@ -257,3 +257,105 @@ def test_ctl_staged_inputs_equal_unstaged(nat, monkeypatch):
     for a, c in zip(*recs):
         for va, vc in zip(a, c):
             np.testing.assert_array_equal(np.asarray(va), np.asarray(vc))
+
+
+def _ctl_words(o, H):
+    """A controller record as comparable values: the whole plan record's bytes, the
+    controller's words and the chosen sequence [H][2]."""
+    return (bytes(o.plan), o.tick, o.projidx, o.warm, o.mu_used, o.scale_used, o.mu_pred, o.dr_mean, o.df_mean,
+            np.ctypeslib.as_array(o.u_seq)[:H].copy())
+
+
+def _same_words(a, b):
+    assert a[0] == b[0]
+    for va, vb in zip(a[1:], b[1:]):
+        np.testing.assert_array_equal(np.asarray(va), np.asarray(vb))
+
+
+def test_ctl_prelaunch_equals_launched(nat):
+    """Armed ticks (llampc_ctl_set_prelaunch: each tick's launch enqueued behind the previous
+    one, x_t through the doorbell, projidx / mu-hat from the device state) against launched
+    ticks: the same records bitwise over the warm-up and the selection, with the armed launch
+    cancelled on the way — by a bank call (llampc_bank_window), by a tick more than 0.5 s after
+    the arming (launched instead) and by switching prelaunch off and on — and the closed loop
+    continuing through each."""
+    import time
+    from llampc.mpc import DeviceController, ModelBank, generate_bank
+    from llampc.params import ORCA
+    nominal = [ORCA()[k] for k in ("Bf", "Cf", "Df", "Br", "Cr", "Dr")]
+    tr, _ = tracks("ETHZ")
+    p = generate_bank(2000, seed=5)
+    x_start = start_state("ETHZ", tr)
+    H, T = 40, 16
+    recs = []
+    for armed in (False, True):
+        b = ModelBank(p, W=5, device=0)
+        ctl = DeviceController(b, tr, H=H, C=64, K=10, nominal6=nominal, prelaunch=armed)
+        x = x_start.copy()
+        plant = O.Vehicle.from_params(O.orca_params())
+        got = []
+        try:
+            for t in range(T):
+                if armed and t == 4:
+                    b.window()                       # a bank call cancels the armed launch
+                if armed and t == 8:
+                    time.sleep(0.6)                  # stale: cancelled, this tick launched
+                if armed and t == 11:
+                    ctl.set_prelaunch(False)
+                if armed and t == 12:
+                    ctl.set_prelaunch(True)
+                o = ctl.tick(x)
+                got.append(_ctl_words(o, H))
+                xn, _ = O.sim_continuous(plant, x, np.array(o.u_seq[0][:]).reshape(2, 1), [0, TS])
+                x = xn[:, -1]
+            assert b.launches == T
+        finally:
+            ctl.close()
+            b.close()
+        recs.append(got)
+    for a, c in zip(*recs):
+        _same_words(a, c)
+
+
+def test_ctl_prelaunch_two_tracks_and_plan_between(nat):
+    """Two armed controllers ticked concurrently (config 5's shape) equal two launched ones, and
+    a plan() call on a third bank between ticks leaves them alone; after the loop a plan() on an
+    armed controller's own bank (which cancels its armed launch) returns normally."""
+    from llampc.mpc import DeviceController, ModelBank, generate_bank
+    from llampc.params import ORCA
+    nominal = [ORCA()[k] for k in ("Bf", "Cf", "Df", "Br", "Cr", "Dr")]
+    setups = []
+    for seed, name in ((0, "ETHZ"), (1, "ETHZMobil")):
+        tr, _ = tracks(name)
+        setups.append((generate_bank(2000, seed=seed), tr, start_state(name, tr)))
+    d = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))
+    s, u = d["states"], d["inputs"]
+
+    def run(armed):
+        banks = [ModelBank(q, W=5, device=0) for q, _, _ in setups]
+        other = ModelBank(generate_bank(500, seed=9), W=5, device=0)
+        ctls = [DeviceController(bk, tr, H=40, C=64, K=10, nominal6=nominal, prelaunch=armed)
+                for bk, (_, tr, _) in zip(banks, setups)]
+        xs = [x.copy() for _, _, x in setups]
+        plant = O.Vehicle.from_params(O.orca_params())
+        recs = []
+        try:
+            for t in range(10):
+                for c, x in zip(ctls, xs):
+                    c.tick_async(x)
+                outs = [c.wait() for c in ctls]
+                other.plan_raw(s[:, t], u[:, t], s[:, t + 1], np.tile(u[:, t], (20, 1))[None], s[:2, :21], u[:, t])
+                for i, o in enumerate(outs):
+                    recs.append(_ctl_words(o, 40))
+                    xn, _ = O.sim_continuous(plant, xs[i], np.array(o.u_seq[0][:]).reshape(2, 1), [0, TS])
+                    xs[i] = xn[:, -1]
+            banks[0].plan_raw(s[:, 0], u[:, 0], s[:, 1], np.tile(u[:, 0], (20, 1))[None], s[:2, :21], u[:, 0])
+        finally:
+            for c in ctls:
+                c.close()
+            for bk in banks + [other]:
+                bk.close()
+        return recs
+
+    for a, c in zip(run(False), run(True)):
+        _same_words(a, c)

@@ -6,7 +6,8 @@ s_memrealtime at 100 MHz): look-ahead blocks — staged (tables + candidates), w
 — scored, lb_final done, slots polled, record stores issued (thread 0), record
 written (after the system fence) — plus the host's own split of the
 tick (tick_begin, the wait, the result).  Paced at 1 ms and back to back.
-usage: python tools/diag/ctl_phases.py [N] [ticks]"""
+"prelaunch": armed ticks (llampc_ctl_set_prelaunch), times from the first block's doorbell.
+usage: python tools/diag/ctl_phases.py [N] [ticks] [prelaunch]"""
 import ctypes
 import os
 import sys
@@ -25,15 +26,16 @@ from llampc.tracks import ETHZ  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+PRE = "prelaunch" in sys.argv[3:]
 lib = nat.load()
 lib.llampc_debug_ctl_stamps.argtypes = [ctypes.c_void_p]
 tr = ETHZ('optimal', True)
 b = ModelBank(generate_bank(N, seed=0), W=10, device=0)
-ctl = LLAMPC(b, tr, H=40, C=64, K=10, mode="device")
+ctl = LLAMPC(b, tr, H=40, C=64, K=10, mode="device", prelaunch=PRE)
 plant = Dynamic(**ORCA(), device=0)
 x = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))["states"][:, 0].copy()
 nb_lb = None
-NAMES = {0: "entry", 14: "bracket", 15: "tables", 1: "staged", 10: "walked", 2: "walk-bar", 3: "selected", 4: "rolled", 5: "published"}
+NAMES = {16: "door", 0: "entry", 14: "bracket", 15: "tables", 1: "staged", 10: "walked", 2: "walk-bar", 3: "selected", 4: "rolled", 5: "published"}
 
 
 def step(paced_until=None):
@@ -55,16 +57,16 @@ def step(paced_until=None):
 
 for i in range(40):
     step()
-buf = (ctypes.c_ulonglong * (64 * 16))()
+buf = (ctypes.c_ulonglong * (64 * 24))()
 for mode in ("paced", "back-to-back"):
     nxt = time.perf_counter()
     for i in range(T):
         nxt += 1e-3
         hb, hw, hr = step(nxt if mode == "paced" else None)
         lib.llampc_debug_ctl_stamps(buf)
-        Z = np.frombuffer(buf, dtype=np.uint64).reshape(64, 16).astype(np.int64)
+        Z = np.frombuffer(buf, dtype=np.uint64).reshape(64, 24).astype(np.int64)
         live = Z[:, 0] > 0
-        base = Z[live, 0].min()
+        base = Z[live, 16].min() if PRE else Z[live, 0].min()
         us = lambda v: (v - base) / 100.0  # noqa: E731
         win = int(np.argmax(np.where(live, Z[:, 9], 0)))      # the completing block
         la = [k for k in range(64) if live[k] and Z[k, 5] >= base and Z[k, 1] >= base]
@@ -72,7 +74,7 @@ for mode in ("paced", "back-to-back"):
         parts.append(f"lb(block {win}): scored {us(Z[win, 6]):.1f} lb_final {us(Z[win, 7]):.1f} "
                      f"polled {us(Z[win, 8]):.1f} seq {us(Z[win, 12]):.1f} words {us(Z[win, 13]):.1f} "
                      f"stored {us(Z[win, 11]):.1f} record {us(Z[win, 9]):.1f} |")
-        for slot in (0, 14, 15, 1, 10, 2, 3, 4, 5):
+        for slot in ((16, 0, 14, 15, 1, 10, 2, 3, 4, 5) if PRE else (0, 14, 15, 1, 10, 2, 3, 4, 5)):
             v = np.array([us(Z[k, slot]) for k in la])
             parts.append(f"{NAMES[slot]} {v.min():.1f}/{v.max():.1f}")
         print(" ".join(parts), flush=True)

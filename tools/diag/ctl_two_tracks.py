@@ -1,7 +1,8 @@
 """Diagnostic: the bench's two-track controller step (ETHZ + ETHZMobil, H = 40, C = 64, N models
 each, tick_begin on both then tick_end) for a kernel trace: do the two controllers' launches
 overlap on the GPU?  Prints the host split per step; run under rocprofv3 --kernel-trace and
-read the trace with tools/diag/trace_overlap.py.  usage: python tools/diag/ctl_two_tracks.py [N] [ticks] [timing] [plant]"""
+read the trace with tools/diag/trace_overlap.py.  "prelaunch": armed ticks (llampc_ctl_set_prelaunch).
+usage: python tools/diag/ctl_two_tracks.py [N] [ticks] [timing] [plant] [prelaunch]"""
 import os
 import sys
 import time
@@ -17,6 +18,7 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 TIMING = "timing" in sys.argv[3:]
 PLANT = "plant" in sys.argv[3:]
+PRE = "prelaunch" in sys.argv[3:]
 EXTRA = int(next((a[8:] for a in sys.argv[3:] if a.startswith("streams=")), "0"))
 import torch  # noqa: E402
 _extra = [torch.cuda.Stream(device=0) for _ in range(EXTRA)]   # other streams created first
@@ -28,7 +30,7 @@ setups = []
 for seed, tr in ((0, ETHZ('optimal', True)), (1, ETHZMobil('optimal', True))):
     b = ModelBank(generate_bank(N, seed=seed), W=10, device=0)
     b.set_concurrency(2)            # the two controllers' banks: a hardware queue each
-    ctl = LLAMPC(b, tr, H=40, C=64, K=10, mode="device")
+    ctl = LLAMPC(b, tr, H=40, C=64, K=10, mode="device", prelaunch=PRE)
     if tr.name == "ETHZ":
         x = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))["states"][:, 0].copy()
     else:
@@ -52,7 +54,7 @@ for i in range(T):
             xn, _ = plant.sim_continuous(s[2], r.u_seq[:, 0].reshape(2, 1), [0, 0.02])
             s[2] = xn[:, -1]
 lat = np.array(lat[20:]) * 1e6
-print(f"timing={TIMING} plant={PLANT} extra streams={EXTRA}: two-track step us p50 {np.median(lat):.1f} p99 {np.percentile(lat, 99):.1f}")
+print(f"timing={TIMING} plant={PLANT} prelaunch={PRE} extra streams={EXTRA}: two-track step us p50 {np.median(lat):.1f} p99 {np.percentile(lat, 99):.1f}")
 for s in setups:
     s[1].close()
     s[0].close()
