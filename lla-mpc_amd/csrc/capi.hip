@@ -1261,6 +1261,15 @@ struct llampc_ctl {
   uint64_t* h_door = nullptr;            // pinned: kCtlDoorWords tagged words (CtlLaunch.door)
   uint64_t* d_door = nullptr;            //   its device alias
   uint64_t* d_door_dev = nullptr;        // block 0's device copy (CtlLaunch.door_dev)
+  // the speculative look-ahead of armed ticks (CtlLaunch.n_spec; LLAMPC_CTL_NO_SPEC=1: never)
+  bool no_spec = false;
+  int32_t spec_cap = kCtlSpecMax;        // LLAMPC_CTL_SPEC_N (tests: few spec models, more misses)
+  int32_t spec_nb = 0;                   // look-back blocks the lists were sized for
+  double* d_spec_val = nullptr;          // [spec_nb][kCtlSpecMax]
+  int64_t* d_spec_idx = nullptr;
+  uint64_t* d_spec_tag = nullptr;        // [kCtlSpecMax]
+  uint64_t* d_spec_res = nullptr;        // [kCtlSpecMax][4]
+  uint64_t* d_xref_tag = nullptr;        // [2 (HMAX + 1)][2]
   uint32_t door_ctr = 0;                 // never reused: a cancelled word cannot match a later launch
   std::chrono::steady_clock::time_point arm_t{};
   struct Prep {                          // a prepared tick: its launch and what it commits
@@ -1304,7 +1313,7 @@ static void bank_disarm(llampc_bank* b) {
 static int ctl_recover(llampc_ctl* c) {
   ctl_cancel(c);                         // an armed launch behind the failed one exits at once
   HIP_TRY(hipStreamSynchronize(c->b->stream));
-  HIP_TRY(hipMemsetAsync(c->d_tickets, 0, sizeof(unsigned), c->b->stream));
+  HIP_TRY(hipMemsetAsync(c->d_tickets, 0, 2 * sizeof(unsigned), c->b->stream));
   HIP_TRY(hipStreamSynchronize(c->b->stream));
   return LLAMPC_OK;
 }
@@ -1318,7 +1327,8 @@ int llampc_ctl_destroy(llampc_ctl* c) {
     DeviceGuard g(c->b ? c->b->device : 0);
     if (c->b && c->b->stream) (void)hipStreamSynchronize(c->b->stream);
     void* d[] = {c->d_st, c->d_pts, c->d_sel_tag, c->d_slot_tag, c->d_tickets, c->d_dbg, c->d_znoise, c->d_ztag,
-                 c->d_gparams, c->d_door_dev};
+                 c->d_gparams, c->d_door_dev, c->d_spec_val, c->d_spec_idx, c->d_spec_tag, c->d_spec_res,
+                 c->d_xref_tag};
     for (void* p : d)
       if (p) (void)hipFree(p);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1362,9 +1372,15 @@ int llampc_ctl_create(llampc_bank* b, const llampc_ctl_cfg* cfg, const double* p
   int rc;
   if ((rc = dev_alloc(&c->d_st, 1)) || (rc = dev_alloc(&c->d_pts, 3 * (size_t)np - 1)) ||
       (rc = dev_alloc(&c->d_sel_tag, kCtlSlotsMax)) || (rc = dev_alloc(&c->d_slot_tag, 4 * (size_t)kCtlSlotsMax)) ||
-      (rc = dev_alloc(&c->d_tickets, 1)) || (rc = dev_alloc(&c->d_znoise, 4 * (size_t)k.C * k.H)) ||
-      (rc = dev_alloc(&c->d_ztag, 2)) || (rc = dev_alloc(&c->d_door_dev, 16)))
+      (rc = dev_alloc(&c->d_tickets, 2)) || (rc = dev_alloc(&c->d_znoise, 4 * (size_t)k.C * k.H)) ||
+      (rc = dev_alloc(&c->d_ztag, 2)) || (rc = dev_alloc(&c->d_door_dev, 16)) ||
+      (rc = dev_alloc(&c->d_spec_val, (size_t)nb_lb * kCtlSpecMax)) ||
+      (rc = dev_alloc(&c->d_spec_idx, (size_t)nb_lb * kCtlSpecMax)) || (rc = dev_alloc(&c->d_spec_tag, kCtlSpecMax)) ||
+      (rc = dev_alloc(&c->d_spec_res, 4 * (size_t)kCtlSpecMax)) || (rc = dev_alloc(&c->d_xref_tag, 4 * (size_t)(LLAMPC_HMAX + 1))))
     return cleanup(rc);
+  c->spec_nb = nb_lb;
+  if (const char* e = std::getenv("LLAMPC_CTL_NO_SPEC")) c->no_spec = e[0] == '1';
+  if (const char* e = std::getenv("LLAMPC_CTL_SPEC_N")) c->spec_cap = std::max(1, std::min(kCtlSpecMax, std::atoi(e)));
   if (k.debug_inputs && (rc = dev_alloc(&c->d_dbg, 2 * (size_t)(k.H + 1) + 2 * (size_t)k.C * k.H))) return cleanup(rc);
   if (hipHostMalloc(reinterpret_cast<void**>(&c->h_out), sizeof(llampc_ctl_out),
                     hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
@@ -1386,7 +1402,10 @@ int llampc_ctl_create(llampc_bank* b, const llampc_ctl_cfg* cfg, const double* p
       hipMemcpy(c->d_pts + 2 * (size_t)np, prefix, ((size_t)np - 1) * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(c->d_sel_tag, 0, kCtlSlotsMax * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->d_slot_tag, 0, 4 * kCtlSlotsMax * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->d_tickets, 0, sizeof(unsigned)) != hipSuccess ||
+      hipMemset(c->d_tickets, 0, 2 * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(c->d_spec_tag, 0, kCtlSpecMax * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->d_spec_res, 0, 4 * kCtlSpecMax * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->d_xref_tag, 0, 4 * (LLAMPC_HMAX + 1) * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->d_ztag, 0, 2 * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->d_door_dev, 0, 16 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "controller upload failed"));
@@ -1576,6 +1595,28 @@ static int ctl_prepare(llampc_ctl* c, const double* x_t, llampc_ctl::Prep& P) {
   size_t lds = L.s4 ? lds_s4 : ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &L.poll_off, false, L.px_G);
   if (lds > 160 * 1024) return fail(LLAMPC_E_ARG, "controller tick needs %zu B of LDS (> 160 KiB)", lds);
   if (L.s4) L.poll_off = poll_s4;
+  // the speculative look-ahead (CtlLaunch.n_spec): armed ticks past the warm-up whose rollouts
+  // are one model per block in fused quads with diagonal Q / P (the spec blocks' layout)
+  {
+    const llampc_cost& cq = k.cost;
+    const bool diag = cq.Q[1] == 0.0 && cq.Q[2] == 0.0 && cq.P[1] == 0.0 && cq.P[2] == 0.0;
+    if (!x_t && !c->no_spec && !warm && full && R == 1 && L.s4 && lpm == 4 && L.cpl == 1 && L.G == k.C && diag &&
+        !c->mb && L.nb_lb <= c->spec_nb) {
+      size_t poll_sp = 0;
+      const int ns = (int)std::min<int64_t>(c->spec_cap, b->n);
+      const size_t lds_sp = ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &poll_sp, true, 0, ns);
+      if (lds_sp <= 160 * 1024) {
+        L.n_spec = ns;
+        L.spec_val = c->d_spec_val;
+        L.spec_idx = c->d_spec_idx;
+        L.spec_tag = c->d_spec_tag;
+        L.spec_res = c->d_spec_res;
+        L.xref_tag = c->d_xref_tag;
+        L.poll_off = poll_sp;
+        lds = lds_sp;
+      }
+    }
+  }
   lds = std::max<size_t>(lds, 82 * 1024); // one block per CU, as the plan launch (sc1 hand-offs)
   P.L = L;
   P.lpm = lpm;

@@ -54,6 +54,29 @@ __host__ __device__ __forceinline__ CtlLds ctl_lds(int H, int C, int n, bool s4 
   L.end = o + 1024;
   return L;
 }
+// A spec block (ctl_spec): xref [H+1][2] (from the walker) | U [C][H][2] | the staged terms
+// (s4) | the deferred positions [C][2][H] (X, Y of each candidate per step) | the quads' unused
+// lanes' sink | misc (x_t, the doorbell's verdict, the model).
+struct SpecLds {
+  size_t sx, ul, s4, pos, junk, misc, end;
+};
+__host__ __device__ __forceinline__ SpecLds spec_lds(int H, int C) {
+  SpecLds L;
+  size_t o = kScratchBytes;
+  L.sx = o;
+  o = align16(o + 16 * (size_t)(H + 1));
+  L.ul = o;
+  o = align16(o + 16 * (size_t)C * H);
+  L.s4 = o;
+  o = align16(o + 16 * (size_t)C * H + 16 * (size_t)C);
+  L.pos = o;
+  o = align16(o + 16 * (size_t)C * H);
+  L.junk = o;
+  o += 8 * 64;
+  L.misc = o;
+  L.end = o + 256;
+  return L;
+}
 constexpr size_t kCtlPollBytes = 4096;   // ctl_complete's area (layout there)
 // ctl_complete's record words (one 8-byte word per lane of wave 0)
 static_assert(offsetof(llampc_plan_out, window_full) == 4 && offsetof(llampc_plan_out, K) == 8 &&
@@ -80,7 +103,8 @@ static_assert(offsetof(llampc_ctl_out, tick) == sizeof(llampc_plan_out) &&
 // barrier, 3 selection, 4 rolled out, 5 published; look-back blocks: 0 entry, 6 scored,
 // 7 lb_final done (ticket winner), 8 slots polled, 12 top-K / sequence stores issued, 13 the
 // record words computed, 11 record stores issued, 9 record written; look-ahead prologue: 14 the
-// mu bracket known, 15 the tables' LDS stores issued; 16 an armed launch's doorbell seen.
+// mu bracket known, 15 the tables' LDS stores issued; 16 an armed launch's doorbell seen; the
+// walk (cs_walk_wave): 17 its loop entered, 18 its loop done (then x/y).
 static __device__ unsigned long long g_ctl_ph[64][24];
 #define CTL_STAMP(blk, slot)                                                                   \
   do {                                                                                         \
@@ -96,6 +120,15 @@ extern "C" int llampc_debug_ctl_stamps(unsigned long long* out) {
 #endif
 
 namespace {
+
+// x_t[i] of the kernel argument by constant indices (a dynamic index into the argument's array
+// makes the compiler copy the whole argument to scratch)
+__device__ __forceinline__ double ctl_xt(const CtlLaunch& c, int i) {
+  double v = c.x_t[0];
+#pragma unroll
+  for (int j = 1; j < 6; ++j) v = i == j ? c.x_t[j] : v;
+  return v;
+}
 
 __device__ __forceinline__ bool ctl_late(uint64_t t0, uint32_t poll) {
   return __builtin_amdgcn_s_memrealtime() - t0 > ((uint64_t)poll << 16);
@@ -150,6 +183,65 @@ __device__ __forceinline__ int ctl_door(const CtlLaunch& c, double* xl, int* res
   CTL_STAMP(blockIdx.x, 16);
   __syncthreads();
   return *res;
+}
+
+// ---- the speculative look-ahead (CtlLaunch.n_spec; ctl.hpp) --------------------------------
+// The n_spec best of the look-back blocks' sorted lists: a tree merge in LDS (the cross-shard
+// merge's), published as tagged words (local model index; kNoLocal: none).
+__device__ __forceinline__ void ctl_spec_merge(const CtlLaunch& c, unsigned char* smem) {
+  const int L = c.nb_lb, M = c.n_spec, tid = threadIdx.x;
+  Ent* b0 = reinterpret_cast<Ent*>(smem + kScratchBytes);
+  Ent* b1 = b0 + (size_t)L * M;
+  for (int e = tid; e < L * M; e += kBlock) b0[e] = Ent{ld_wt(&c.spec_val[e]), ld_wt(&c.spec_idx[e])};
+  __syncthreads();
+  const Ent* top = tree_merge(b0, b1, L, M);
+  if (tid < M) {
+    const int64_t i = top[tid].i;
+    st_wt(&c.spec_tag[tid], tag_word(c.seq, i == kNoIndex ? kNoLocal : (uint32_t)i));
+  }
+}
+
+// A look-back block's part, before the doorbell: its models ranked by the window mean without
+// x_t (pred; NaN last, ties to the lower index — lb_final's order), the n_spec best stored
+// sorted; the last block (ticket 1, reset at once: every block has drawn) merges the lists.
+__device__ __forceinline__ void ctl_spec_lists(const CtlLaunch& c, int blk, double pred, bool valid, int64_t n,
+                                               unsigned char* smem, int* flag) {
+  const int tid = threadIdx.x, M = c.n_spec;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem + kScratchBytes);
+  uint32_t* ids = reinterpret_cast<uint32_t*>(keys + kBlock);
+  const uint64_t key = valid ? order_key(pred) : ~0ull;
+  const uint32_t id = valid ? (uint32_t)n : kNoModelId + (uint32_t)tid;
+  keys[tid] = key;
+  ids[tid] = id;
+  __syncthreads();
+  int r = 0;
+#pragma unroll 16
+  for (int j = 0; j < kBlock; ++j) r += (int)(keys[j] < key) | ((int)(keys[j] == key) & (int)(ids[j] < id));
+  if (r < M) {
+    st_wt(&c.spec_val[(int64_t)blk * M + r], valid ? pred : __builtin_nan(""));
+    st_wt(&c.spec_idx[(int64_t)blk * M + r], valid ? n : kNoIndex);
+  }
+  if (!ticket_last(&c.tickets[1], (unsigned)c.nb_lb, flag)) return;
+  if (tid == 0) __hip_atomic_store(&c.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ctl_spec_merge(c, smem);
+}
+
+// The deferred tracking cost (rollout<DEFER>): the split rollout's epilogue with the reference
+// known — the same terms in the same order, so J equals the undeferred rollout's bitwise.
+__device__ __forceinline__ double defer_cost(const double* dpos, int dstride, const double* sx, int H, int pc,
+                                             double Qd, double Pd, const DeferOut& d, bool sok, bool& bad) {
+  double track = 0.0, xr0 = 0.0;
+  for (int k = 0; k < H; ++k) {
+    xr0 = sx[2 * (k + 1) + pc];
+    const double e = dpos[k * dstride] - xr0;
+    track = track + e * (Qd * e);
+  }
+  const double e = d.xl - xr0;
+  const double jl = e * (Pd * e) + track;
+  double J = (dpp_bcast<kQuad0>(jl) + dpp_bcast<kQuad1>(jl)) + d.act;
+  bad = (int)bad | (int)!sok | (int)!d.dok | (int)!(fabs(J) <= __DBL_MAX__) | (int)(d.feas_s != d.feas_s);
+  if (!(d.feas_s != 0.0)) J = __builtin_inf();
+  return J;
 }
 
 // The raw candidates [C][H][2] (before the rate clip) by threads t0 + i stride, i >= 0: from
@@ -221,6 +313,22 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   unsigned char* late_w = smem + kLateOff;
   CtlState* st = c.st;
   const bool warm = c.warm != 0;
+  // the spec list (CtlLaunch.n_spec): a slot whose model is on it reads the spec block's words
+  uint32_t* spec_ids = reinterpret_cast<uint32_t*>(pl + 3648);    // [kCtlSpecMax]
+  if (tid < c.n_spec) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t v = kNoLocal;
+    for (;;) {
+      const uint64_t w = ld_wt(&c.spec_tag[tid]);
+      if (tag_ok(w, c.seq)) {
+        v = (uint32_t)w;
+        break;
+      }
+      if (ctl_late(t0, c.poll)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    spec_ids[tid] = v;
+  }
   // Before the poll (the look-ahead blocks' rollouts take most of the launch) everything that
   // does not need their results: the projection, mu-hat and every candidate after its rate
   // clip (the look-ahead blocks' generator), so the chosen sequence is a copy after the poll.
@@ -280,9 +388,17 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   if (tid < 6) st->x_prev[tid] = xt[tid];
   // the record's scalar kernel arguments, loaded (and kept) before the poll: the tail used
   // to wait for them one by one after it
-  int32_t a_wc = c.fin.window_count, a_full = c.fin.full, a_K = c.K, a_warm = c.warm, a_lap = c.lap_projidx;
-  int64_t a_goff = c.sel_goff, a_tick = (int64_t)c.tick;
-  double a_scale = c.use_mu ? c.v_factor : c.scale_fixed;
+  // (readfirstlane: launch-uniform values in SGPRs whatever the argument's copy)
+  auto rfl = [](int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane(v); };
+  auto rfl64 = [](int64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  int32_t a_wc = rfl(c.fin.window_count), a_full = rfl(c.fin.full), a_K = rfl(c.K), a_warm = rfl(c.warm),
+          a_lap = rfl(c.lap_projidx);
+  int64_t a_goff = rfl64(c.sel_goff), a_tick = rfl64((int64_t)c.tick);
+  double a_scale = __longlong_as_double((long long)rfl64(__double_as_longlong(c.use_mu ? c.v_factor : c.scale_fixed)));
   asm volatile("" : "+s"(a_wc), "+s"(a_full), "+s"(a_K), "+s"(a_warm), "+s"(a_lap));
   asm volatile("" : "+s"(a_goff), "+s"(a_tick), "+s"(a_scale));
   // waves 1-3 draw the next tick's variates while wave 0 polls (off every critical path)
@@ -291,10 +407,16 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   int late = 0;
   if (tid < c.nslots) {
     uint64_t w[4];
+    const uint64_t* src = c.slot_tag + 4 * (size_t)tid;
+    if (c.n_spec && !warm) {
+      const uint32_t id = cs.ids[tid];
+      for (int p = 0; p < c.n_spec; ++p)
+        if (id != kNoLocal && spec_ids[p] == id) src = c.spec_res + 4 * (size_t)p;
+    }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = ld_wt(&c.slot_tag[4 * tid + q]);
+      for (int q = 0; q < 4; ++q) w[q] = ld_wt(&src[q]);
       if ((int)tag_ok(w[0], c.seq) & (int)tag_ok(w[1], c.seq) & (int)tag_ok(w[2], c.seq) & (int)tag_ok(w[3], c.seq))
         break;
       if (ctl_late(t0, c.poll)) {
@@ -606,15 +728,22 @@ __device__ __forceinline__ double spline4(const double* c, double dx) {
 // ConstantSpeed's walk (planner.py:24-65) by ONE WAVE (all 64 lanes call it, uniform control
 // flow): projidx = p0 + argmin (:26-27), the start arc length from the prefix table (:29-36),
 // then H <= 64 steps of :40-62 into sx [H+1][2]; returns projidx and, in lane 0, vr (:63-64).
-// RaceRef::step's walk with the step's candidate segments evaluated speculatively: lane
-// l <= kAhead reads knot seg + l and that segment's two speed cubics (five LDS reads, all
-// addressed by the step's start segment) and evaluates v there; the count of knots <= t over
-// lanes 1..kAhead (a ballot: RaceRef::step's advance) picks the lane whose v holds.  So the
-// chain of a step is one LDS round trip, the cubic and one division chain; x/y are not on it:
-// lane k keeps step k's (segment, dx) and evaluates :43 after the walk.  (The serial walker
-// read the knots, then the chosen segment's coefficients, ~0.7 us a step; a first wave version
-// with x/y in the loop 0.45 us.)  v = (v_lo wa) / den + (v_hi wb) / den (:58-60), the
-// divisions by div_by.
+// RaceRef::step's walk over a window of 64 consecutive segments held in registers — lane j
+// segment w0 + j: its knot (+inf past the last) and the two speed cubics' coefficients — so a
+// step reads no memory: every lane evaluates its segment's v at t, the count of knots <= t over
+// the kWalkAhead lanes past the current segment (a ballot: RaceRef::step's advance) picks the
+// lane whose v holds, and readlane takes v, the knot and dx from it.  The chain of a step is
+// the cubic and one division chain.  The window moves (64 lanes' LDS reads) when the
+// candidates would leave it — about once per walk; x/y are not on the chain: lane k keeps step
+// k's (segment, dx) and evaluates :43 after the walk.  (Before: each step read its candidate
+// segments from LDS — one LDS round trip on the chain, ~0.3 us a step; the serial walker
+// ~0.7 us.)  v = (v_lo wa) / den + (v_hi wb) / den (:58-60), the divisions by div_by, the cubic
+// spline_at's expression (spline4's): the same roundings as before.
+constexpr int kWalkAhead = 16;
+__device__ __forceinline__ double cubic4(double a, double b, double c, double d, double dx) {
+  const double dx2 = dx * dx;
+  return a + b * dx + c * dx2 + d * (dx2 * dx);
+}
 __device__ __forceinline__ int cs_walk_wave(const RacelineK& rl, const MuBracket& br, const double* kn,
                                             const double* spd, const double* prefix, const double* dist, int segs,
                                             int p0, double px, double py, double v0, double scale, double Ts, int H,
@@ -634,7 +763,27 @@ __device__ __forceinline__ int cs_walk_wave(const RacelineK& rl, const MuBracket
   // a single profile (mu outside the table) has wa = 1, wb = 0, den = 1: v = v_lo exactly
   // (both rows hold it), so no branch keeps the second cubic's reads behind the first
   const double wa = br.wa, wb = br.wb, den = br.den, rden = 1.0 / den;
-  const int l = lane < kAhead ? lane : kAhead;                      // lanes > kAhead repeat kAhead
+  // the register window: lane j <- segment w0 + j (cubics of min(w0 + j, m - 1), as before)
+  int w0 = 0;
+  double wk, c0, c1, c2, c3, c4, c5, c6, c7;
+  auto load_win = [&](int base) {
+    w0 = base;
+    const int sj = base + lane;
+    wk = sj <= m ? kn[sj] : __builtin_inf();
+    const int sl = sj < m - 1 ? sj : m - 1;
+    const double2* c = reinterpret_cast<const double2*>(spd + 8 * (size_t)sl);
+    const double2 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3];
+    c0 = q0.x;
+    c1 = q0.y;
+    c2 = q1.x;
+    c3 = q1.y;
+    c4 = q2.x;
+    c5 = q2.y;
+    c6 = q3.x;
+    c7 = q3.y;
+  };
+  load_win(seg);
+  CTL_STAMP(blockIdx.x, 17);
   int myseg = 0;                                                    // lane k: step k's segment, dx
   double mydx = 0.0, v1 = 0.0;
   for (int k = 0; k < H; ++k) {
@@ -649,27 +798,25 @@ __device__ __forceinline__ int cs_walk_wave(const RacelineK& rl, const MuBracket
       seg = 0;
       kseg = kn[0];
     }
-    // lane l: knot seg + l (+inf past the last: never counted, since t < L = kn[m]) and the
-    // segment's cubics at t (coefficient reads clamped into the table; unused lanes discard)
-    const int sl = seg + l < m - 1 ? seg + l : m - 1;
-    const double kl = kn[seg + l];
-    const double* cl = spd + 8 * (size_t)sl;
-    double dl = t - kl;
-    const double vb = spline4(cl, dl);
-    const double va = spline4(cl + 4, dl);
+    int rel = seg - w0;
+    if (rel < 0 || rel + kWalkAhead > 63) {                         // wave-uniform: move the window
+      load_win(seg);
+      rel = 0;
+    }
+    double dl = t - wk;
+    const double vb = cubic4(c0, c1, c2, c3, dl);
+    const double va = cubic4(c4, c5, c6, c7, dl);
     double vl = div_by(vb * wa, den, rden) + div_by(va * wb, den, rden);
-    // every lane's v before the advance is known: the compiler would otherwise sink the
-    // cubics' reads below the ballot's branch — a second LDS round trip on the chain
-    asm volatile("" : "+v"(vl), "+v"(dl));
-    const int adv = __popcll(__ballot(lane >= 1 && lane <= kAhead && kl <= t));
+    const int adv = __popcll(__ballot(lane > rel && lane <= rel + kWalkAhead && wk <= t));
     double dx;
-    if (__builtin_expect(adv < kAhead, 1)) {                        // wave-uniform
-      v = readlane_d(vl, adv);
-      kseg = readlane_d(kl, adv);
-      dx = readlane_d(dl, adv);
+    if (__builtin_expect(adv < kWalkAhead, 1)) {                    // wave-uniform
+      const int ch = rel + adv;
+      v = readlane_d(vl, ch);
+      kseg = readlane_d(wk, ch);
+      dx = readlane_d(dl, ch);
       seg += adv;
-    } else {                                                        // past a full window: serial
-      int sg = seg + kAhead;
+    } else {                                                        // past the candidates: serial
+      int sg = seg + kWalkAhead;
       while (sg < m - 1 && kn[sg + 1] <= t) ++sg;
       kseg = kn[sg];
       dx = t - kseg;
@@ -685,6 +832,7 @@ __device__ __forceinline__ int cs_walk_wave(const RacelineK& rl, const MuBracket
     }
     if (k == 0) v1 = v;
   }
+  CTL_STAMP(blockIdx.x, 18);
   if (lane == 0) {
     sx[0] = px;                                                     // planner.py:33
     sx[1] = py;
@@ -722,7 +870,8 @@ __device__ __forceinline__ void ctl_stage(const CtlLaunch& c, const double* Ul, 
   constexpr int kThreads = kBlock - 64;
   const int ns = C < kThreads / 2 ? C : kThreads / 2;                 // threads summing per candidate
   if (t < ns) {
-    const CostK& q = c.la.cost;
+    const CostK q = c.la.cost;          // a copy: a reference into the kernel argument made
+                                        // the compiler copy the whole argument to scratch
     for (int cc = t; cc < C; cc += ns) {
       const double* u = Ul + 2 * (size_t)cc * H;
       double act = 0.0, p0 = up0, p1 = up1;
@@ -768,7 +917,7 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   int* door_res = reinterpret_cast<int*>(smem + L.misc + 720);
   CTL_STAMP(blockIdx.x, 0);
   const bool armed = c.door != nullptr;
-  if (!armed && tid < 6) x0[tid] = c.x_t[0 + tid];
+  if (!armed && tid < 6) x0[tid] = ctl_xt(c, tid);
   if (tid == 0) *arrived = 0;
   const CtlState* st = c.st;
   const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
@@ -777,9 +926,19 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   // arguments directly (profiles/r04/s4/ctl_phases_prologue.txt: 2.5 us to the bracket before).
   // An armed launch reads the state itself: the previous tick ended before it started, and
   // the loads sit before the doorbell.
-  const int p0 = armed ? st->projidx : c.p0_walk;
+  // (values, not pointers, are selected — the empty asm keeps the compiler from loading through a
+  // select of the state's and the kernel argument's addresses, which copies the whole argument
+  // to scratch)
+  int p0 = c.p0_walk;
+  double mu_k = c.mu_fixed;
+  asm volatile("" : "+s"(p0));
+  asm volatile("" : "+v"(mu_k));
+  if (armed) {
+    p0 = st->projidx;
+    if (c.use_mu) mu_k = st->mu_pred;
+  }
   const double scale = c.use_mu ? c.v_factor : c.scale_fixed;
-  const MuBracket br = armed ? mu_bracket(rl.mus, rl.M, c.use_mu ? st->mu_pred : c.mu_fixed) : c.br_walk;
+  const MuBracket br = armed ? mu_bracket(rl.mus, rl.M, mu_k) : c.br_walk;
   CTL_STAMP(blockIdx.x, 14);
   // waves 1-3: this tick's candidate variates (the previous tick's completion drew them) are
   // loaded now, their latency under the tables' (used only when their tag matches: ctl_draw)
@@ -811,6 +970,7 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
     px = c.x_t[0];
     py = c.x_t[1];
     pv = c.x_t[3];
+    asm volatile("" : "+v"(px), "+v"(py), "+v"(pv));
   }
   const int segs = cs_project(c.pts, c.np, p0, px, py, dist);
   __syncthreads();
@@ -848,6 +1008,31 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   }
   __syncthreads();
   CTL_STAMP(blockIdx.x, 2);
+  // speculative look-ahead (c.n_spec): the first block publishes the reference for the spec
+  // blocks' deferred costs, and wave 1 of every block loads the spec list (its models' results
+  // come from the spec blocks)
+  uint32_t* spec_ids = reinterpret_cast<uint32_t*>(smem + L.misc + 768);   // [kCtlSpecMax]
+  if (c.n_spec) {
+    if (blk == 0 && tid < 2 * (H + 1)) {
+      const uint64_t v = (uint64_t)__double_as_longlong(sx[tid]);
+      st_wt(&c.xref_tag[2 * tid], tag_word(c.seq, (uint32_t)(v >> 32)));
+      st_wt(&c.xref_tag[2 * tid + 1], tag_word(c.seq, (uint32_t)v));
+    }
+    if (tid >= 64 && tid < 64 + c.n_spec) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t v = kNoLocal;
+      for (;;) {
+        const uint64_t w = ld_wt(&c.spec_tag[tid - 64]);
+        if (tag_ok(w, c.seq)) {
+          v = (uint32_t)w;
+          break;
+        }
+        if (ctl_late(t0, c.poll)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      spec_ids[tid - 64] = v;
+    }
+  }
   // (d) waves 1-3 clip the candidates' rates; meanwhile (e) wave 0 takes this block's slots:
   //     the selection (tagged words of the look-back ticket winner), or the nominal model
   //     while the window fills
@@ -885,6 +1070,17 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
     sel_late[tid] = late;
   }
   __syncthreads();
+  if (c.n_spec) {                       // launch-uniform: a slot whose model a spec block rolls out: bit 1
+    if (tid < 64) {
+      const int lane = tid;
+      for (int q = 0; q < mpb; ++q) {
+        const uint32_t sid = slot_id[q];
+        const bool hit = __ballot(lane < c.n_spec && sid != kNoLocal && spec_ids[lane] == sid) != 0;
+        if (lane == 0 && hit) sel_late[q] |= 2;
+      }
+    }
+    __syncthreads();
+  }
   CTL_STAMP(blockIdx.x, 3);
   if (c.dbg && blk == 0) {              // tests: this tick's reference and candidates
     for (int e = tid; e < 2 * (H + 1); e += kBlock) {
@@ -899,7 +1095,8 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   const int sub = tid % LPM, cl = tid / LPM, g = cl & (G - 1), si = cl / G;
   const int slot = blk * mpb + si;
   const uint32_t id = si < mpb ? slot_id[si] : kNoLocal;
-  const bool live = slot < c.nslots && id != kNoLocal;
+  const bool spec_hit = si < mpb && (sel_late[si] & 2);
+  const bool live = slot < c.nslots && id != kNoLocal && !spec_hit;
   Tire t{};
   if (live) {
     if (c.warm) {
@@ -1028,9 +1225,9 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
     }
   }
   // (h) publish: cost (hi, lo), candidate, non-finite count | late << 31 (tagged words)
-  if (g == 0 && sub == 0 && si < mpb && slot < c.nslots) {
+  if (g == 0 && sub == 0 && si < mpb && slot < c.nslots && !spec_hit) {
     const uint64_t vb = (uint64_t)__double_as_longlong(bv);
-    const uint32_t nfw = (uint32_t)nf | ((uint32_t)sel_late[si] << 31);
+    const uint32_t nfw = (uint32_t)nf | ((uint32_t)(sel_late[si] & 1) << 31);
     uint64_t* w = c.slot_tag + 4 * (size_t)slot;
     st_wt(&w[0], tag_word(c.seq, (uint32_t)(vb >> 32)));
     st_wt(&w[1], tag_word(c.seq, (uint32_t)vb));
@@ -1040,16 +1237,200 @@ __device__ __forceinline__ void ctl_lookahead(const CtlLaunch& c, int blk, unsig
   CTL_STAMP(blockIdx.x, 5);
 }
 
+// A spec block: model spec_tag[j] x the C candidates from the doorbell on (ctl.hpp
+// CtlLaunch.n_spec).  Before the doorbell: the candidates (the look-ahead blocks' generator, so
+// the same sequences), the rate clip, the staged terms, the model.  Then the rollouts with the
+// tracking cost deferred (rollout<DEFER>), the reference from the first look-ahead block's walk
+// (xref_tag), defer_cost, and the block's best candidate as ctl_lookahead publishes a slot.
+// LPM 4 with diagonal Q / P only (the host enables spec blocks for that layout).
+template <int LPM>
+__device__ __forceinline__ void ctl_spec(const CtlLaunch& c, int j, unsigned char* smem, const Scratch& sc) {
+  if constexpr (LPM != 4) {
+    return;
+  } else {
+    const int tid = threadIdx.x;
+    const int H = c.la.H, C = c.la.C;
+    const SpecLds S = spec_lds(H, C);
+    double* sx = reinterpret_cast<double*>(smem + S.sx);
+    double* Ul = reinterpret_cast<double*>(smem + S.ul);
+    double* s4 = reinterpret_cast<double*>(smem + S.s4);
+    double* pos = reinterpret_cast<double*>(smem + S.pos);
+    double* junk = reinterpret_cast<double*>(smem + S.junk);
+    double* x0 = reinterpret_cast<double*>(smem + S.misc);            // [6]
+    int* door_res = reinterpret_cast<int*>(smem + S.misc + 64);
+    uint32_t* sid = reinterpret_cast<uint32_t*>(smem + S.misc + 80);
+    const CtlState* st = c.st;
+    const double* prev_seq = st->has_seq ? &st->useq[0][0] : nullptr;
+    const double up0 = st->u_prev[0], up1 = st->u_prev[1];
+    ctl_draw(c, prev_seq, up0, up1, Ul, tid, kBlock);
+    __syncthreads();
+    for (int t = tid; t < 2 * C; t += kBlock) {
+      const int jj = t & 1;
+      ctl_rate_chain(Ul + 2 * (size_t)(t >> 1) * H + jj, H, jj ? up1 : up0, jj ? c.rate[1] : c.rate[0]);
+    }
+    __syncthreads();
+    if (tid >= 64) ctl_stage(c, Ul, s4, tid - 64, up0, up1);      // waves 1-3, as the look-ahead blocks
+    if (tid == 0) {                     // the model (the spec merge publishes before the doorbell)
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t id = kNoLocal;
+      for (;;) {
+        const uint64_t w = ld_wt(&c.spec_tag[j]);
+        if (tag_ok(w, c.seq)) {
+          id = (uint32_t)w;
+          break;
+        }
+        if (ctl_late(t0, 2 * c.door_bound)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      *sid = id;
+    }
+    __syncthreads();
+    const uint32_t id = *sid;
+    if (id == kNoLocal) return;         // block-uniform: fewer models than spec blocks
+    const Tire t = load_tire(c.la.params, c.la.n, id);
+    if (ctl_door(c, x0, door_res) != (int)kCtlDoorFire) return;
+    CTL_STAMP(blockIdx.x, 19);
+    const int G = c.G, cpl = c.cpl;
+    const int sub = tid % LPM, cl = tid / LPM, g = cl & (G - 1);
+    CostK q = c.la.cost;
+    VehK veh = c.la.veh;
+    double Ts = c.la.Ts;
+    for (int m = 0; m < 4; ++m) {
+      pin_vgpr(q.Q[m]);
+      pin_vgpr(q.R[m]);
+      pin_vgpr(q.P[m]);
+    }
+    pin_vgpr(veh.lf);
+    pin_vgpr(veh.lr);
+    pin_vgpr(veh.mass);
+    pin_vgpr(veh.inv_mass);
+    pin_vgpr(veh.inv_Iz);
+    pin_vgpr(veh.Cm1);
+    pin_vgpr(veh.Cm2);
+    pin_vgpr(veh.Cr0);
+    pin_vgpr(veh.Cr2);
+    pin_vgpr(Ts);
+    constexpr bool kScaled = scaled_yaw(LPM);
+    StageK sk = make_stage<LPM>(veh, t, sub, Ts);
+    if (kScaled) sk.ch[0].lw = sk.ch[0].lw / Ts;
+    if (kScaled && sub >= 2) {          // lanes 2/3: zero-operand chains (plan kernel)
+      sk.ch[0].lw = 0.0;
+      sk.ch[0].sg = 0.0;
+      sk.ch[0].B = 0.0;
+      sk.ch[0].nsB = 0.0;
+    }
+    const FusedK fq = make_fused(veh, sk, Ts, kScaled);
+    const fm::FmK K = fm::FmK::load<kLeanLA>();
+    const double Qd = sk.pc ? q.Q[3] : q.Q[0], Pd = sk.pc ? q.P[3] : q.P[0];
+    // cpl == 1 with G == C (the host's layout for spec blocks): candidate g in quad g
+    const int cc = g;
+    double* dp = sub < 2 ? pos + (size_t)(2 * cc + sub) * H : junk + (tid & 63);
+    const int ds = sub < 2 ? 1 : 0;
+    bool bad = false;
+    DeferOut d{};
+    (void)cpl;
+    (void)rollout<0, false, LPM, 0, true, true, true, false, true, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts,
+                                                                         up0, up1, K, fq, bad, nullptr, s4, dp, ds,
+                                                                         &d);
+    CTL_STAMP(blockIdx.x, 20);
+    // the reference: the walker's tagged halves (its walk ended long before these rollouts)
+    {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (int e = tid; e < 2 * (H + 1); e += kBlock) {
+        uint64_t hi, lo;
+        for (;;) {
+          hi = ld_wt(&c.xref_tag[2 * e]);
+          lo = ld_wt(&c.xref_tag[2 * e + 1]);
+          if ((int)tag_ok(hi, c.seq) & (int)tag_ok(lo, c.seq)) break;
+          if (ctl_late(t0, c.poll)) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        sx[e] = __longlong_as_double((long long)join_words(hi, lo));
+      }
+    }
+    __syncthreads();
+    double J = defer_cost(dp, ds, sx, H, sk.pc, Qd, Pd, d, sk.sok, bad);
+    {
+      int bi = bad;
+      bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX1, 0xF, 0xF, false);
+      bi |= __builtin_amdgcn_mov_dpp(bi, kQuadX2, 0xF, 0xF, false);
+      bad = bi;
+    }
+    if (__builtin_expect(__any(bad), 0)) {
+      bool unused = false;
+      if (bad)
+        J = rollout<0, false, LPM, 0, false, false, true>(c.la, cc, 0, x0, sx, Ul, veh, t, sk, q, Ts, up0, up1, K, fq,
+                                                         unused);
+    }
+    double bv = __builtin_nan("");
+    int64_t bc = kNoIndex;
+    int nf = 0;
+    if (sub == 0) nf += !isfinite(J);
+    if (less_nan_last(J, cc, bv, bc)) {
+      bv = J;
+      bc = cc;
+    }
+    // the block's argmin over its C candidates and non-finite count (ctl_lookahead's (g))
+    const int span = G * LPM;
+    for (int off = (span < 64 ? span : 64) >> 1; off >= LPM; off >>= 1) {
+      const double ov = __shfl_xor(bv, off, 64);
+      const int64_t oc = __shfl_xor(bc, off, 64);
+      nf += __shfl_xor(nf, off, 64);
+      if (less_nan_last(ov, oc, bv, bc)) {
+        bv = ov;
+        bc = oc;
+      }
+    }
+    if (span > 64) {                    // block-uniform
+      if ((tid & 63) == 0) {
+        sc.sv[tid >> 6] = bv;
+        sc.si[tid >> 6] = bc;
+        sc.sn[tid >> 6] = nf;
+      }
+      __syncthreads();
+      const int w0 = (tid / span) * (span / 64);
+      bv = sc.sv[w0];
+      bc = sc.si[w0];
+      nf = sc.sn[w0];
+      for (int k = 1; k < span / 64; ++k) {
+        nf += sc.sn[w0 + k];
+        if (less_nan_last(sc.sv[w0 + k], sc.si[w0 + k], bv, bc)) {
+          bv = sc.sv[w0 + k];
+          bc = sc.si[w0 + k];
+        }
+      }
+    }
+    if (tid == 0) {
+      const uint64_t vb = (uint64_t)__double_as_longlong(bv);
+      uint64_t* w = c.spec_res + 4 * (size_t)j;
+      st_wt(&w[0], tag_word(c.seq, (uint32_t)(vb >> 32)));
+      st_wt(&w[1], tag_word(c.seq, (uint32_t)vb));
+      st_wt(&w[2], tag_word(c.seq, (uint32_t)(int32_t)bc));
+      st_wt(&w[3], tag_word(c.seq, (uint32_t)nf));
+    }
+    CTL_STAMP(blockIdx.x, 21);
+  }
+}
+
 }  // namespace
 
 // PX: the sharded controller (ctl_exchange after the shard's lb_final) — its own
 // instantiation, so the unsharded tick's code is unchanged
 template <int LPM, bool PX>
-__global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
+__global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch arg) {
+  // the argument read in place from the kernarg segment (it is the launch's first and only
+  // explicit argument): referencing the by-value parameter itself made the compiler copy all
+  // 1.4 KB of it to scratch once the kernel grew
+  (void)arg;
+  const CtlLaunch& c = *(const CtlLaunch*)__builtin_amdgcn_kernarg_segment_ptr();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Scratch sc(smem);
   int* flag = reinterpret_cast<int*>(smem + kFlagOff);
   const int blk = (int)blockIdx.x;
+  if (blk >= c.nb_lb + c.nb_la) {       // spec blocks (CtlLaunch.n_spec), last in the grid
+    ctl_spec<LPM>(c, blk - c.nb_lb - c.nb_la, smem, sc);
+    return;
+  }
   if (blk >= c.nb_lb) {
     ctl_lookahead<LPM>(c, blk - c.nb_lb, smem, sc);
     return;
@@ -1063,7 +1444,9 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
   // whole argument to scratch): the kernel argument, or an armed launch's doorbell — after the
   // look-back's step, which needs only the state (lookback_block<ARMED>)
   double* xl = reinterpret_cast<double*>(pl + 3072);
-  auto door = [&]() -> const double* {
+  auto door = [&](double pred, bool pvalid, int64_t pn) -> const double* {
+    // the speculative look-ahead's ranking first: it needs only the window (before x_t)
+    if (c.n_spec) ctl_spec_lists(c, blk, pred, pvalid, pn, smem, flag);
     if (c.door) {
       const int r = ctl_door(c, xl, reinterpret_cast<int*>(pl + 3584));
       if (r != (int)kCtlDoorFire) {     // cancelled or expired: nothing touched
@@ -1072,7 +1455,7 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
         return nullptr;
       }
     } else {
-      if (threadIdx.x < 6) xl[threadIdx.x] = c.x_t[0 + threadIdx.x];
+      if (threadIdx.x < 6) xl[threadIdx.x] = ctl_xt(c, (int)threadIdx.x);
       __syncthreads();
     }
     return xl;
@@ -1094,7 +1477,7 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch c) {
     }
     CTL_STAMP(blk, 7);
     __syncthreads();
-  } else if (!door()) {                 // ticks without a look-back: block 0 only completes
+  } else if (!door(0.0, false, 0)) {    // ticks without a look-back: block 0 only completes
     return;
   }
   ctl_complete(c, smem, cs, xl);
@@ -1136,13 +1519,18 @@ hipError_t launch_constant_speed(const CsLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4, int px_G) {
+size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4, int px_G, int n_spec) {
   const CtlLds L = ctl_lds(H, C, n, s4);
   const size_t M = (size_t)nb_lb * K, Lb = nb_lb;    // lb_final's region (launch_plan's formula)
   const size_t lbf = kScratchBytes + 8 * (3 * M + Lb) + sizeof(Ent) * Lb * kWaves + 4 * (3 * M + Lb + LLAMPC_KMAX + 2) + 8 + 16;
   const size_t rank = kScratchBytes + (size_t)kWaves * kRankBytes + kBlockMergeBytes;
   const size_t px = px_G ? kScratchBytes + ctl_px_bytes(px_G, K) : 0;   // ctl_exchange's region
-  size_t off = std::max(std::max(L.end, px), std::max(lbf, rank));
+  // the speculative look-ahead: a spec block's layout, the look-back blocks' ranking and the
+  // spec merge's two list buffers
+  const size_t spec = n_spec ? std::max(spec_lds(H, C).end,
+                                        kScratchBytes + std::max<size_t>(12 * kBlock, 2 * sizeof(Ent) * Lb * n_spec))
+                             : 0;
+  size_t off = std::max(std::max(std::max(L.end, px), std::max(lbf, rank)), spec);
   off = align16(off);
   *poll_off = off;
   return off + kCtlPollBytes;
@@ -1150,7 +1538,7 @@ size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bo
 
 template <bool PX>
 static void launch_ctl_px(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s) {
-  const dim3 grid(c.nb_lb + c.nb_la), block(kBlock);
+  const dim3 grid(c.nb_lb + c.nb_la + c.n_spec), block(kBlock);
   if (lpm == 4) {
     allow_lds(ctl_kernel<4, PX>);
     hipLaunchKernelGGL((ctl_kernel<4, PX>), grid, block, lds, s, c);

@@ -349,7 +349,25 @@ struct CtlLaunch {
   const uint64_t* door;
   uint64_t* door_dev;
   uint32_t door_seq, door_bound;
+  // speculative look-ahead (n_spec > 0: an armed tick with a full window): before the doorbell
+  // each look-back block ranks its models by their window mean without x_t — the W - 1 entries
+  // that stay (win_pre) — and stores its sorted n_spec best at spec_val / spec_idx[blk]; the
+  // last of them (ticket 1) merges the lists and publishes the n_spec best as tagged words
+  // spec_tag[j] (local index; kNoLocal: none).  Spec block j (after the look-ahead blocks in the
+  // grid) rolls model spec_tag[j] out from the doorbell on — the tracking cost deferred until
+  // the reference arrives (xref_tag: the first look-ahead block's walk, tagged halves) — and
+  // publishes its best candidate at spec_res[4 j] (ctl_lookahead's slot words).  A selected
+  // model among them is not rolled out again: the look-ahead blocks skip it and the completion
+  // reads spec_res (profiles/r05/spec_topm.json: the selection falls inside the 64 best by this
+  // predictor on ~90 % of the closed loop's ticks).
+  int32_t n_spec;
+  double* spec_val;           // [nb_lb][n_spec]
+  int64_t* spec_idx;
+  uint64_t* spec_tag;         // [kCtlSpecMax]
+  uint64_t* spec_res;         // [kCtlSpecMax][4]
+  uint64_t* xref_tag;         // [2 (H + 1)][2]
 };
+constexpr int kCtlSpecMax = 64;
 constexpr int kCtlDoorWords = 13;
 constexpr uint32_t kCtlDoorFire = 1, kCtlDoorCancel = 2, kCtlDoorExpired = 3;
 constexpr uint64_t kCtlTagExpired = 1ull << 62;
@@ -367,7 +385,8 @@ hipError_t launch_constant_speed(const CsLaunch& a, hipStream_t s);
 
 // LDS bytes of the controller launch and the completing block's area offset (ctl.hip); s4:
 // with the staged input terms (CtlLaunch.s4).
-size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4 = false, int px_G = 0);
+size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bool s4 = false, int px_G = 0,
+                     int n_spec = 0);
 hipError_t launch_ctl(const CtlLaunch& c, int lpm, size_t lds, hipStream_t s);
 
 }  // namespace llampc

@@ -490,10 +490,12 @@ __device__ __forceinline__ void wave_topk_rank(const LookbackLaunch& a, double w
 // RK4 step from (x_{t-1}, u_{t-1}), 4-state MSE against x_t, in-place ring write, window
 // mean in NumPy's pairwise order; then the block's argmin and its SORTED top-K list.
 // ------------------------------------------------------------------------------------
-// ARMED (the controller, ctl.hip): x_t comes from door() — the LDS copy of x_t, or null when
-// the launch is cancelled (lookback_block then returns false) — and with one model per lane
-// the RK4 step runs BEFORE it: the step needs only the state's (x_{t-1}, u_{t-1}), x_t enters
-// with the error, so an armed launch has the step done when its doorbell rings.
+// ARMED (the controller, ctl.hip): x_t comes from door(pred, valid, n) — the LDS copy of x_t,
+// or null when the launch is cancelled (lookback_block then returns false) — and with one
+// model per lane the RK4 step runs BEFORE it: the step needs only the state's (x_{t-1},
+// u_{t-1}), x_t enters with the error, so an armed launch has the step done when its doorbell
+// rings.  door() also gets the lane's model n (valid: n < N) and its window mean without x_t
+// (pred: the W - 1 entries that stay, over W; the speculative look-ahead's ranking).
 template <bool ARMED = false, typename Door = int>
 __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk, const Scratch& sc, Door door = 0) {
   LB_STAMP(blk, 0);
@@ -508,9 +510,14 @@ __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk,
   WinPre wpp{0.0, 0.0, 0.0, 0.0};
   bool bp = false, pre = false;
   if constexpr (ARMED) {
+    double pred = 0.0;
+    bool pvalid = false;
+    int64_t pn = 0;
     if (a.R == 1) {                     // launch-uniform
       const int64_t n = base + threadIdx.x;
       if (n < a.n) {
+        pvalid = true;
+        pn = n;
         double x[6];
 #pragma unroll
         for (int j = 0; j < 6; ++j) x[j] = a.x_prev[j];
@@ -524,10 +531,11 @@ __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk,
 #pragma unroll
         for (int j = 0; j < 4; ++j) xp[j] = x[j];
         bp = (int)ubad | (int)!sk.sok | (int)!dm.ok();
+        if (a.full) pred = win_finish(wpp, 0.0, a.W);
       }
       pre = true;
     }
-    x_now = door();
+    x_now = door(pred, pvalid, pn);
     if (!x_now) return false;
   }
   for (int r = 0; r < a.R; ++r) {
@@ -684,14 +692,25 @@ __device__ __forceinline__ bool input_feasible(const CostK& q, double ua, double
 // feasibility (1 / 0; NaN: a steering outside sincos_fast's domain, so the rollout re-runs in
 // the general evaluation) at s4 + 2CH [C][2] (LDS; ctl.hip ctl_stage) — the step reads two
 // values instead of forming them, with the same values and roundings.
+// DEFER (with SPLIT and S4: the controller's speculative look-ahead, ctl.hip ctl_spec): the
+// reference is not known yet — the lane stores its position component after step k at
+// dpos[k dstride] instead of accumulating the tracking term, and returns its last position,
+// the summed input-rate cost, the feasibility and the domain flag in *dout (J: defer_cost,
+// the same terms in the same order once the reference is known).
+struct DeferOut {
+  double xl, act, feas_s;
+  bool dok;
+};
 template <int INTEG, bool STAGE, int LPM, int XM, bool FAST, bool SPLIT = false, bool ULDS = false, bool TRAJ = false,
-          bool S4 = false>
+          bool S4 = false, bool DEFER = false>
 __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64_t n,
                                           const double* x0, const double* sx, const double* su, const VehK& veh,
                                           const Tire& t, const StageK& sk, const CostK& q,
                                           double Ts, double up0, double up1, const fm::FmK& K,
                                           const FusedK& fq, bool& bad, double* traj = nullptr,
-                                          const double* s4 = nullptr) {
+                                          const double* s4 = nullptr, double* dpos = nullptr, int dstride = 0,
+                                          DeferOut* dout = nullptr) {
+  static_assert(!DEFER || (SPLIT && S4), "deferred tracking cost: the controller's split, staged rollout");
   static_assert(!TRAJ || (INTEG != 0 && !SPLIT), "trajectory output: unscaled, unsplit state");
   static_assert(!S4 || (ULDS && FAST && !STAGE), "staged sincos / cost terms: the controller's fast rollout");
   static_assert(!SPLIT || (FAST && INTEG == 0 && LPM == 4), "position split: fused RK4 quads only");
@@ -760,7 +779,9 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     else if (FAST && INTEG == 0) step_fused<LPM, SPLIT>(sk, fq, x, u, K, dm);
     else if (FAST) step_fast<INTEG, LPM>(veh, t, sk, x, u, Ts, K, dm);
     else step<INTEG>(veh, t, x, u, Ts);
-    if (SPLIT) {                        // this lane's component of the reference and term
+    if (DEFER) {                        // the position component, for defer_cost
+      dpos[k * dstride] = x[0];
+    } else if (SPLIT) {                 // this lane's component of the reference and term
       xr0 = XM ? xpm[2 * k + sk.pc] : sx[2 * (k + 1) + sk.pc];
       const double e = x[0] - xr0;
       track = track + e * (Qd * e);
@@ -787,6 +808,13 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     const double2 af = *reinterpret_cast<const double2*>(s4 + 2 * (int64_t)C * H + 2 * c);
     act = af.x;
     feas_s = af.y;
+  }
+  if constexpr (DEFER) {
+    (void)track;
+    (void)Qd;
+    (void)Pd;
+    *dout = DeferOut{x[0], act, feas_s, dm.ok()};
+    return 0.0;
   }
   double J;
   if (SPLIT) {                                                    // nmpc.py:48, :111

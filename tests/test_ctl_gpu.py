@@ -78,9 +78,10 @@ def test_ctl_reference_matches_reference_planner(nat, name):
 
 @pytest.mark.parametrize("name", ["ETHZ", "ETHZMobil"])
 def test_ctl_reference_fast_starts_and_lap_end(nat, name):
-    """The walk's branches off the common path: a first step past kAhead segments (v0 up to
-    25 m/s: the serial continuation after the wave's window), and starts just before the lap
-    end (the mod-L wrap, then the restart at segment 0) — against host ConstantSpeed, 1e-10."""
+    """The walk's branches off the common path: a first step past the walker's kWalkAhead = 16
+    candidate segments (v0 = 25 m/s: ~21 segments of ~0.023 m; the serial continuation), the
+    register window moving several times per walk, and starts just before the lap end (the
+    mod-L wrap, then the restart at segment 0) — against host ConstantSpeed, 1e-10."""
     from llampc.mpc import DeviceController, ModelBank, generate_bank
     from llampc.mpc.planner import ConstantSpeed
     tr, _ = tracks(name)
@@ -272,14 +273,21 @@ def _same_words(a, b):
         np.testing.assert_array_equal(np.asarray(va), np.asarray(vb))
 
 
-def test_ctl_prelaunch_equals_launched(nat):
+@pytest.mark.parametrize("spec", ["64", "3", "off"])
+def test_ctl_prelaunch_equals_launched(nat, monkeypatch, spec):
     """Armed ticks (llampc_ctl_set_prelaunch: each tick's launch enqueued behind the previous
     one, x_t through the doorbell, projidx / mu-hat from the device state) against launched
     ticks: the same records bitwise over the warm-up and the selection, with the armed launch
     cancelled on the way — by a bank call (llampc_bank_window), by a tick more than 0.5 s after
     the arming (launched instead) and by switching prelaunch off and on — and the closed loop
-    continuing through each."""
+    continuing through each.  spec: the armed ticks' speculative look-ahead (CtlLaunch.n_spec)
+    with 64 models (mostly hits), 3 (mostly misses: the look-ahead blocks roll the rest out) or
+    none (LLAMPC_CTL_NO_SPEC)."""
     import time
+    if spec == "off":
+        monkeypatch.setenv("LLAMPC_CTL_NO_SPEC", "1")
+    else:
+        monkeypatch.setenv("LLAMPC_CTL_SPEC_N", spec)
     from llampc.mpc import DeviceController, ModelBank, generate_bank
     from llampc.params import ORCA
     nominal = [ORCA()[k] for k in ("Bf", "Cf", "Df", "Br", "Cr", "Dr")]

@@ -35,7 +35,7 @@ ctl = LLAMPC(b, tr, H=40, C=64, K=10, mode="device", prelaunch=PRE)
 plant = Dynamic(**ORCA(), device=0)
 x = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))["states"][:, 0].copy()
 nb_lb = None
-NAMES = {16: "door", 0: "entry", 14: "bracket", 15: "tables", 1: "staged", 10: "walked", 2: "walk-bar", 3: "selected", 4: "rolled", 5: "published"}
+NAMES = {17: "walk-loop", 18: "walk-loop-end", 16: "door", 0: "entry", 14: "bracket", 15: "tables", 1: "staged", 10: "walked", 2: "walk-bar", 3: "selected", 4: "rolled", 5: "published"}
 
 
 def step(paced_until=None):
@@ -74,7 +74,7 @@ for mode in ("paced", "back-to-back"):
         parts.append(f"lb(block {win}): scored {us(Z[win, 6]):.1f} lb_final {us(Z[win, 7]):.1f} "
                      f"polled {us(Z[win, 8]):.1f} seq {us(Z[win, 12]):.1f} words {us(Z[win, 13]):.1f} "
                      f"stored {us(Z[win, 11]):.1f} record {us(Z[win, 9]):.1f} |")
-        for slot in ((16, 0, 14, 15, 1, 10, 2, 3, 4, 5) if PRE else (0, 14, 15, 1, 10, 2, 3, 4, 5)):
+        for slot in ((16, 0, 14, 15, 1, 17, 18, 10, 2, 3, 4, 5) if PRE else (0, 14, 15, 1, 17, 18, 10, 2, 3, 4, 5)):
             v = np.array([us(Z[k, slot]) for k in la])
             parts.append(f"{NAMES[slot]} {v.min():.1f}/{v.max():.1f}")
         print(" ".join(parts), flush=True)
