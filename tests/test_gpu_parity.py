@@ -1313,10 +1313,12 @@ def test_setupnlp_cem_shapes_equal_oracle(nat, samples, elite, iters, H):
         nlp.close()
 
 
-def test_setupnlp_within_5pct_of_local_optimum(nat):
+def test_setupnlp_within_1pct_of_local_optimum(nat):
     """Solution quality of the setupNLP drop-in: on three DYN-slice ticks its fval is within
-    5 % of a local optimum of the same restated NLP found by scipy's SLSQP
-    (tests/golden/nlp_optimum.npz, gen_nlp_optimum.py).  IPOPT's own optimum stays unpinned."""
+    1 % of a local optimum of the same restated NLP found by scipy's SLSQP
+    (tests/golden/nlp_optimum.npz, gen_nlp_optimum.py) — measured 1.0013, 1.0023, 1.0079 (the
+    search is deterministic: bitwise the oracle's, test_setupnlp_cem_equals_oracle).
+    IPOPT's own optimum stays unpinned."""
     g = golden("nlp_optimum.npz")
     for i in range(len(g["fstar"])):
         nlp, _ = _nlp()
@@ -1324,7 +1326,7 @@ def test_setupnlp_within_5pct_of_local_optimum(nat):
             umpc, fval, _, _ = nlp.solve(g["x0"][i], g["xref"][i], g["uprev"][i])
         finally:
             nlp.close()
-        assert fval <= 1.05 * g["fstar"][i], (int(g["tick"][i]), fval, g["fstar"][i])
+        assert fval <= 1.01 * g["fstar"][i], (int(g["tick"][i]), fval, g["fstar"][i])
 
 
 @pytest.mark.parametrize("track_name,start", [("ETHZ", "projected"), ("ETHZ", "lap_end"), ("ETHZMobil", "projected")])
