@@ -1306,6 +1306,21 @@ static void bank_disarm(llampc_bank* b) {
   if (b && b->armed) ctl_cancel(b->armed);
 }
 
+// Controllers whose tick was rung and whose next launch is still to be armed (arm_next).  The
+// first llampc_ctl_wait of a step arms them ALL before it spins: with two tracks (tick_async on
+// both, then wait on both) the second controller's launch call would otherwise sit between the
+// first's result and its own (~5 us on the two-track step).
+static std::mutex g_arm_mu;
+static std::vector<llampc_ctl*> g_arm_list;
+static void arm_list_add(llampc_ctl* c) {
+  std::lock_guard<std::mutex> g(g_arm_mu);
+  g_arm_list.push_back(c);
+}
+static void arm_list_remove(llampc_ctl* c) {
+  std::lock_guard<std::mutex> g(g_arm_mu);
+  g_arm_list.erase(std::remove(g_arm_list.begin(), g_arm_list.end(), c), g_arm_list.end());
+}
+
 // A failed controller tick (a wait that gave up, or a completion that never arrived): once the
 // stream has drained, the look-back ticket is zeroed so the next launch's ticket_last counts
 // from 0.  The tick still consumed its step on the device (the window slot, the tick number);
@@ -1322,6 +1337,7 @@ extern "C" {
 
 int llampc_ctl_destroy(llampc_ctl* c) {
   if (!c) return LLAMPC_OK;
+  arm_list_remove(c);
   ctl_cancel(c);
   {
     DeviceGuard g(c->b ? c->b->device : 0);
@@ -1687,6 +1703,7 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
       b->armed = nullptr;
       ctl_commit(c, c->arm);
       c->arm_next = c->prelaunch;
+      if (c->arm_next) arm_list_add(c);
       return LLAMPC_OK;
     }
     ctl_cancel(c);                       // stale: this tick launches normally
@@ -1702,6 +1719,7 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   }
   ctl_commit(c, P);
   c->arm_next = c->prelaunch;
+  if (c->arm_next) arm_list_add(c);
   return LLAMPC_OK;
 }
 
@@ -1712,13 +1730,40 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
   c->pending = false;
   c->hint_ok = false;                    // until this tick's record is read
   DeviceGuard g(c->b->device);
-  if (c->arm_next) {
-    // the next tick's launch, armed behind this one — here rather than in tick_async, so that
-    // several controllers' ticks (two tracks) are all rung before any launch call; the launch
-    // call overlaps this tick's device time.  A failed arm only turns prelaunch off.
-    c->arm_next = false;
-    std::lock_guard<std::mutex> lk(c->b->mu);
-    if (!c->b->async_pending && ctl_arm(c) != LLAMPC_OK) c->prelaunch = false;
+  {
+    // the next ticks' launches, armed behind the ones in flight — here rather than in
+    // tick_async, so that several controllers' ticks (two tracks) are all rung before any
+    // launch call, and for every rung controller at once (g_arm_list); the launch calls overlap
+    // the device time.  Another controller is armed only if its locks are free (else its own
+    // wait arms it).  A failed arm only turns prelaunch off.
+    std::vector<llampc_ctl*> todo;
+    {
+      std::lock_guard<std::mutex> g(g_arm_mu);
+      todo.swap(g_arm_list);
+    }
+    std::vector<llampc_ctl*> keep;
+    for (llampc_ctl* x : todo) {
+      const bool self = x == c;
+      if (!self && !x->mu.try_lock()) {
+        keep.push_back(x);
+        continue;
+      }
+      if (x->arm_next) {
+        if (x->b->mu.try_lock()) {
+          x->arm_next = false;
+          DeviceGuard gx(x->b->device);
+          if (!x->b->async_pending && ctl_arm(x) != LLAMPC_OK) x->prelaunch = false;
+          x->b->mu.unlock();
+        } else {
+          keep.push_back(x);
+        }
+      }
+      if (!self) x->mu.unlock();
+    }
+    if (!keep.empty()) {
+      std::lock_guard<std::mutex> g(g_arm_mu);
+      g_arm_list.insert(g_arm_list.end(), keep.begin(), keep.end());
+    }
   }
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t spins = 0;
@@ -1758,6 +1803,7 @@ int llampc_ctl_set_prelaunch(llampc_ctl* c, int32_t on) {
   DeviceGuard g(b->device);
   c->prelaunch = on != 0;
   c->arm_next = c->prelaunch && c->pending;   // a tick in flight: armed by its wait
+  if (c->arm_next) arm_list_add(c);
   if (!c->prelaunch) {
     ctl_cancel(c);
     return LLAMPC_OK;

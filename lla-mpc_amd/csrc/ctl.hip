@@ -134,29 +134,38 @@ __device__ __forceinline__ bool ctl_late(uint64_t t0, uint32_t poll) {
   return __builtin_amdgcn_s_memrealtime() - t0 > ((uint64_t)poll << 16);
 }
 
-// An armed launch's doorbell (CtlLaunch.door): thread 0 polls the kCtlDoorWords tagged words —
-// block 0 the pinned host copy (system-scope loads), every other block the device copy block 0
-// makes — until the status word carries door_seq (and, to fire, every x_t half does).  Returns,
-// block-uniform after the barrier: kCtlDoorFire (x_t in xl), kCtlDoorCancel, kCtlDoorExpired.
+// An armed launch's doorbell (CtlLaunch.door): thread 0 of block 0 polls the pinned host copy
+// (system-scope loads, all 13 words a round), every other block the device copy block 0 makes:
+// its STATUS word alone, and once that carries door_seq the 12 x_t halves (block 0 drains their
+// stores before it stores the status); every word's tag is checked.  One word per round on the
+// device side: 13 words a round from 64 blocks made the relay 2.9 us instead of 1.1
+// (tools/diag/doorbell_lat.hip, mode 3).  Returns, block-uniform after
+// the barrier: kCtlDoorFire (x_t in xl), kCtlDoorCancel, kCtlDoorExpired.
 __device__ __forceinline__ int ctl_door(const CtlLaunch& c, double* xl, int* res) {
   if (threadIdx.x == 0) {
     const bool host = blockIdx.x == 0;
+    auto ld = [&](int q) {
+      return host ? __hip_atomic_load(&c.door[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : ld_wt(&c.door_dev[q]);
+    };
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t w[kCtlDoorWords];
     int r;
     for (;;) {
+      // block 0 reads every word each round (the PCIe reads overlap; a second round trip for
+      // the x_t halves after the status would add ~1 us), the others the status word first
       if (host) {
 #pragma unroll
-        for (int q = 0; q < kCtlDoorWords; ++q)
-          w[q] = __hip_atomic_load(&c.door[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      } else {
-#pragma unroll
-        for (int q = 0; q < kCtlDoorWords; ++q) w[q] = ld_wt(&c.door_dev[q]);
+        for (int q = 0; q < kCtlDoorWords - 1; ++q) w[q] = ld(q);
       }
-      const uint64_t sw = w[kCtlDoorWords - 1];
+      const uint64_t sw = ld(kCtlDoorWords - 1);
       if (tag_ok(sw, c.door_seq)) {
+        w[kCtlDoorWords - 1] = sw;
         r = (int)(uint32_t)sw;
         if (r != (int)kCtlDoorFire) break;
+        if (!host) {
+#pragma unroll
+          for (int q = 0; q < kCtlDoorWords - 1; ++q) w[q] = ld(q);
+        }
         int all = 1;
 #pragma unroll
         for (int q = 0; q < kCtlDoorWords - 1; ++q) all &= (int)tag_ok(w[q], c.door_seq);
@@ -169,10 +178,14 @@ __device__ __forceinline__ int ctl_door(const CtlLaunch& c, double* xl, int* res
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (host) {                         // the verdict for the other blocks
-      if (r == (int)kCtlDoorExpired) w[kCtlDoorWords - 1] = tag_word(c.door_seq, kCtlDoorExpired);
+    if (host) {                         // the verdict for the other blocks: x_t, drained, then the status
+      if (r == (int)kCtlDoorFire) {
 #pragma unroll
-      for (int q = 0; q < kCtlDoorWords; ++q) st_wt(&c.door_dev[q], w[q]);
+        for (int q = 0; q < kCtlDoorWords - 1; ++q) st_wt(&c.door_dev[q], w[q]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      st_wt(&c.door_dev[kCtlDoorWords - 1], r == (int)kCtlDoorExpired ? tag_word(c.door_seq, kCtlDoorExpired)
+                                                                       : w[kCtlDoorWords - 1]);
     }
     if (r == (int)kCtlDoorFire) {
 #pragma unroll

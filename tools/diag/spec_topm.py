@@ -6,6 +6,7 @@ friction decay, the controller's own controls), whether the rolled-out set top-K
 lies inside the M best models of a predictor known before x_t:
   prev      the previous tick's window means (its argsort)
   partial   the sum of the W - 1 window entries that stay (the one dropping out removed)
+  partial+last  that sum plus the newest entry again (the coming error's estimate)
 for M in a range; also the mean and max rank of the needed models under each predictor.  CPU
 only (the oracle).  usage: python tools/diag/spec_topm.py [N] [ticks] [out.json]"""
 import json
@@ -40,8 +41,8 @@ def run(name, seed, x0, H=40, C=64, K=10, W=10):
                              H=H, C=C, K=K, W=W)
     plant = O.Vehicle.from_params(p)
     x = np.asarray(x0, dtype=np.float64)
-    hits = {"prev": {m: 0 for m in MS}, "partial": {m: 0 for m in MS}}
-    maxrank = {"prev": [], "partial": []}
+    hits = {k: {m: 0 for m in MS} for k in ("prev", "partial", "partial+last")}
+    maxrank = {k: [] for k in ("prev", "partial", "partial+last")}
     compared = 0
     for t in range(T):
         win = orc.win
@@ -50,7 +51,9 @@ def run(name, seed, x0, H=40, C=64, K=10, W=10):
             prev_order = np.lexsort((np.arange(N), win.avg, np.isnan(win.avg)))
             part = win.win[:, 1:].sum(axis=1)     # the entries that stay after the roll
             part_order = np.lexsort((np.arange(N), part, np.isnan(part)))
-            pre = {"prev": prev_order, "partial": part_order}
+            last = part + win.win[:, -1]          # ... plus the newest error again, as the next one's estimate
+            last_order = np.lexsort((np.arange(N), last, np.isnan(last)))
+            pre = {"prev": prev_order, "partial": part_order, "partial+last": last_order}
         o = orc.tick(x)
         if not o["warm"] and pre is not None:
             needed = np.unique(np.append(np.asarray(o["topk"], dtype=np.int64), int(o["best_model"])))
