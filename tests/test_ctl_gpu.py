@@ -307,7 +307,9 @@ def test_ctl_prelaunch_equals_launched(nat, monkeypatch, spec):
                 if armed and t == 4:
                     b.window()                       # a bank call cancels the armed launch
                 if armed and t == 8:
-                    time.sleep(0.6)                  # stale: cancelled, this tick launched
+                    # stale: cancelled, this tick launched; with spec 64 past the armed launch's
+                    # 2 s bound, so it has expired (marked its completion number) before the cancel
+                    time.sleep(2.3 if spec == "64" else 0.6)
                 if armed and t == 11:
                     ctl.set_prelaunch(False)
                 if armed and t == 12:
