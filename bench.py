@@ -585,10 +585,13 @@ def extras(args, sb, stream, world, rank=0):
         out["paced_plan_latency_us"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                         "max": float(lat.max()), "ticks": int(lat.size), "period_us": period * 1e6,
                                         "note": "sync_plan_latency's call, one tick per 1 ms period (busy-wait pacing)"}
-        out["config5"] = concurrent_tracks(args)
-        out["config3"] = config3(args)
-        out["controller_tick_us"] = controller_ticks(args)
-        out["solve_us"] = solve_latency(args)
+        # (one process: an extra that fails is reported in the line, not fatal to the headline)
+        for key, fn in (("config5", concurrent_tracks), ("config3", config3), ("controller_tick_us", controller_ticks),
+                        ("solve_us", solve_latency)):
+            try:
+                out[key] = fn(args)
+            except Exception as e:          # noqa: BLE001
+                out[key] = {"error": f"{type(e).__name__}: {e}"}
     else:
         out["config5"] = concurrent_tracks_sharded(args, world, rank, sb.device)
         out["controller_tick_us"] = controller_ticks_sharded(args, world, rank, sb.device)
