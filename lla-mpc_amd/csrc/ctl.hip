@@ -455,8 +455,11 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
   llampc_ctl_out* o = c.out;
   llampc_plan_out* po = &o->plan;
   const double nan = __builtin_nan("");
-  if (tid < LLAMPC_KMAX) {
-    const int k = tid;
+  // the top-K's candidates (wave 1) and the chosen sequence (waves 2-3) while wave 0 forms the
+  // record's words: every wave issues its own stores into the pinned record (one wave issuing
+  // them all in turn put ~1 us before the words, profiles/r05/spec2/phases_armed.txt)
+  if (tid >= 64 && tid < 64 + LLAMPC_KMAX) {
+    const int k = tid - 64;
     const bool have = !warm && k < c.K;
     if (warm) {                         // no look-back selection yet (lb_final did not run)
       po->topk[k] = -1;
@@ -465,11 +468,12 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     po->topk_cand[k] = have ? pcand[k] : -1;
     po->topk_cost[k] = have ? pcost[k] : nan;
   }
-  if (tid < 2 * H) {                    // the chosen sequence: candidate sel_cand
-    const double v = cu[2 * (size_t)scand * H + tid];
-    (&o->u_seq[0][0])[tid] = v;
-    (&st->useq[0][0])[tid] = v;
-    if (tid < 2) st->u_prev[tid] = v;
+  if (tid >= 128 && tid < 128 + 2 * H) {   // the chosen sequence: candidate sel_cand
+    const int e = tid - 128;
+    const double v = cu[2 * (size_t)scand * H + e];
+    (&o->u_seq[0][0])[e] = v;
+    (&st->useq[0][0])[e] = v;
+    if (e < 2) st->u_prev[e] = v;
   }
   CTL_STAMP(blockIdx.x, 12);
   if (tid < 64) {

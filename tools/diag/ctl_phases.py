@@ -74,6 +74,13 @@ for mode in ("paced", "back-to-back"):
         parts.append(f"lb(block {win}): scored {us(Z[win, 6]):.1f} lb_final {us(Z[win, 7]):.1f} "
                      f"polled {us(Z[win, 8]):.1f} seq {us(Z[win, 12]):.1f} words {us(Z[win, 13]):.1f} "
                      f"stored {us(Z[win, 11]):.1f} record {us(Z[win, 9]):.1f} |")
+        # spec blocks (armed ticks, CtlLaunch.n_spec): 19 doorbell seen, 20 rolled out, 21 published
+        sp = [k for k in range(64) if Z[k, 21] >= base and Z[k, 19] >= base]
+        if PRE and sp:
+            for slot, nm in ((19, "spec-door"), (20, "spec-rolled"), (21, "spec-published")):
+                v = np.array([us(Z[k, slot]) for k in sp])
+                parts.append(f"{nm} {v.min():.1f}/{v.max():.1f}")
+            parts.append("|")
         for slot in ((16, 0, 14, 15, 1, 17, 18, 10, 2, 3, 4, 5) if PRE else (0, 14, 15, 1, 17, 18, 10, 2, 3, 4, 5)):
             v = np.array([us(Z[k, slot]) for k in la])
             parts.append(f"{NAMES[slot]} {v.min():.1f}/{v.max():.1f}")
