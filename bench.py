@@ -903,9 +903,9 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
                          f"{LOOKBACK_INSTR_PER_MODEL} (look-back, upper bound) over the mean launch; pmc: "
                          "SQ_INSTS_VALU x 64 of the committed PMC pass over the same launch time"}
     extra_ctl = {"rollout_steps_per_tick": steps_tick,
-                 "spec_models": 64,
-                 "spec_note": "armed ticks also roll out the 64 best models by the window mean without x_t from the "
-                              "doorbell on (CtlLaunch.n_spec; 64 C H further steps per tick, not counted above): the "
+                 "spec_models": 32,
+                 "spec_note": "armed ticks also roll out the 32 best models by the window mean without x_t from the "
+                              "doorbell on (CtlLaunch.n_spec; 32 C H further steps per tick, not counted above): the "
                               "selected ones are not rolled out again",
                  "rollout_steps_per_s_at_p50": 2 * steps_tick / (q["p50"] * 1e-6),
                  "bytes_per_launch": ctl_bytes,

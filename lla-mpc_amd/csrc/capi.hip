@@ -1263,7 +1263,10 @@ struct llampc_ctl {
   uint64_t* d_door_dev = nullptr;        // block 0's device copy (CtlLaunch.door_dev)
   // the speculative look-ahead of armed ticks (CtlLaunch.n_spec; LLAMPC_CTL_NO_SPEC=1: never)
   bool no_spec = false;
-  int32_t spec_cap = kCtlSpecMax;        // LLAMPC_CTL_SPEC_N (tests: few spec models, more misses)
+  // spec models per armed tick: 32 (LLAMPC_CTL_SPEC_N, <= kCtlSpecMax).  The paced two-track step
+  // measured p50 56.1 / 55.9 us with 32, 57.8 / 58.0 with 64, 57.9 with 96 (profiles/r05/specn/):
+  // fewer busy CUs outweigh the 2-3 % more misses (profiles/r05/spec_topm.json)
+  int32_t spec_cap = 32;
   int32_t spec_nb = 0;                   // look-back blocks the lists were sized for
   double* d_spec_val = nullptr;          // [spec_nb][kCtlSpecMax]
   int64_t* d_spec_idx = nullptr;

@@ -358,8 +358,8 @@ struct CtlLaunch {
   // the reference arrives (xref_tag: the first look-ahead block's walk, tagged halves) — and
   // publishes its best candidate at spec_res[4 j] (ctl_lookahead's slot words).  A selected
   // model among them is not rolled out again: the look-ahead blocks skip it and the completion
-  // reads spec_res (profiles/r05/spec_topm.json: the selection falls inside the 64 best by this
-  // predictor on ~90 % of the closed loop's ticks).
+  // reads spec_res (profiles/r05/spec_topm.json: the selection falls inside the 32 best by this
+  // predictor on 86-88 % of the closed loop's ticks, the 64 best on ~90 %; 32 by default, capi.hip).
   int32_t n_spec;
   double* spec_val;           // [nb_lb][n_spec]
   int64_t* spec_idx;
