@@ -846,7 +846,7 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
         else:
             x = np.array([tr.x_init, tr.y_init, tr.psi_init, 1.0, 0.0, 0.0])
         setups.append([b, ctl, plant, x])
-    lat, kern, split = [], [], []
+    lat, kern, split, devt = [], [], [], []
     lib = nat.load()
     ev_ticks = 100                          # after the timed steps: per-launch event pairs for
     try:                                    # the kernel time (their cost stays out of lat)
@@ -865,6 +865,7 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
             t2 = time.perf_counter()
             lat.append(t2 - t0)
             split.append((t1 - t0, t2 - t1))
+            devt.append([s[1].device_us() for s in setups])
             for s, r in zip(setups, res):     # the plant (outside the timed step)
                 pl = s[2]
                 pl.Df -= pl.Df / 2600.
@@ -883,6 +884,14 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
             s[1].close()
             s[0].close()
     q = pctl(np.array(lat[warm:warm + ticks]) * 1e6)
+    dv = np.array(devt, dtype=np.float64)
+    def dpct(a):
+        a = a[np.isfinite(a)]
+        return {"p50": float(np.percentile(a, 50)), "p99": float(np.percentile(a, 99)), "max": float(a.max())} if a.size else None
+    device_us = {"armed": dpct(dv[warm:warm + ticks].ravel()), "launched": dpct(dv[warm + ticks + 8:].ravel()),
+                 "note": "llampc_ctl_device_us per tick and track: x_t on the device (armed: block 0 sees the "
+                         "doorbell; launched: block 0 starts) to the record's stores issued, by the GPU's 100 MHz "
+                         "clock; armed = the timed steps, launched = the event-timed steps after them"}
     N, K, W = args.n_per_gpu, args.K, args.W
     steps_tick = N + (K + 1) * C * H              # look-back steps + the (K+1) x C rollouts' steps
     # algorithmic HBM bytes of one controller launch: the look-back's params + ring read/write per
@@ -914,7 +923,7 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
     return {"p50": q["p50"], "p99": q["p99"], "max": q["max"], "ticks": q["ticks"], "period_us": period * 1e6,
             "budget_us": 1000.0, "met": q["p99"] < 1000.0, "tracks": ["ETHZ", "ETHZMobil"],
             "N_per_track": args.n_per_gpu, "H": H, "C": C, "K": args.K, "W": args.W,
-            "kernel_us_avg": kern, "sel_models": sel, "projidx": laps, **extra_ctl,
+            "kernel_us_avg": kern, "device_us": device_us, "sel_models": sel, "projidx": laps, **extra_ctl,
             "host_split_us_p50": {"begin": float(np.median([a for a, _ in split[warm:warm + ticks]]) * 1e6),
                                   "end": float(np.median([b for _, b in split[warm:warm + ticks]]) * 1e6)},
             "note": "LLAMPC.tick (device mode, llampc_ctl_tick_async/wait: one launch per track per step, armed "

@@ -363,6 +363,11 @@ int llampc_ctl_wait(llampc_ctl* ctl, llampc_ctl_out* out);
  * as does a tick more than 0.5 s after the arming; an armed launch never rung exits after 2 s.
  * Not with llampc_ctl_set_exchange.  on = 0 cancels. */
 int llampc_ctl_set_prelaunch(llampc_ctl* ctl, int32_t on);
+/* The last completed tick's device time in microseconds: from x_t reaching the device (an armed
+ * launch's block 0 seeing the doorbell; else block 0 starting) to the record's stores issued, by
+ * the GPU's 100 MHz clock (s_memrealtime).  NaN before the first tick.  Not the step latency:
+ * that adds the doorbell / launch and the record's path to the host. */
+int llampc_ctl_device_us(llampc_ctl* ctl, double* us);
 /* ConstantSpeed (planner.py:12-67) alone on the device with the controller's tables and Ts:
  * x0 [2], v0, horizon H (<= LLAMPC_HMAX), projidx, curr_mu, scale -> xref [2][H+1], the new
  * projidx (no lap wrap) and vr.  Blocking; leaves the controller state alone. */

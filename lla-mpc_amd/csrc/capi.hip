@@ -1274,6 +1274,7 @@ struct llampc_ctl {
   uint64_t* d_spec_res = nullptr;        // [kCtlSpecMax][4]
   uint64_t* d_xref_tag = nullptr;        // [2 (HMAX + 1)][2]
   uint32_t door_ctr = 0;                 // never reused: a cancelled word cannot match a later launch
+  uint64_t dev_ticks = 0;                // the last completed tick's device time (llampc_ctl_device_us)
   std::chrono::steady_clock::time_point arm_t{};
   struct Prep {                          // a prepared tick: its launch and what it commits
     CtlLaunch L{};
@@ -1554,9 +1555,9 @@ static int ctl_prepare(llampc_ctl* c, const double* x_t, llampc_ctl::Prep& P) {
   L.do_lb = do_lb;
   L.warm = warm;
   L.use_mu = t > W + 1;                  // rt.py:278
+  L.door_dev = c->d_door_dev;            // every launch: its x_t time (kCtlTimeWord)
   if (!x_t) {                            // armed: the launch reads projidx / mu-hat from the state
     L.door = c->d_door;
-    L.door_dev = c->d_door_dev;
     c->door_ctr = c->door_ctr == 0xFFFFFFFFu ? 1u : c->door_ctr + 1u;
     L.door_seq = c->door_ctr;
     L.door_bound = (uint32_t)(kArmBoundS * 1e8 / 65536.0) + 1;
@@ -1787,6 +1788,7 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
     }
   }
   std::memcpy(out, const_cast<const llampc_ctl_out*>(c->h_out), sizeof(llampc_ctl_out));
+  c->dev_ticks = __atomic_load_n(c->h_tag + 1, __ATOMIC_RELAXED);
   if (out->plan.status) {
     (void)ctl_recover(c);
     return fail(LLAMPC_E_DEVICE, "controller tick record status %d (an in-launch wait timed out)", out->plan.status);
@@ -1794,6 +1796,13 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
   c->hint_p0 = out->projidx;             // the state this tick left (ctl_complete writes both)
   c->hint_mu = out->mu_pred;
   c->hint_ok = true;
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_device_us(llampc_ctl* c, double* us) {
+  if (!c || !us) return fail(LLAMPC_E_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lc(c->mu);
+  *us = c->dev_ticks ? (double)c->dev_ticks * 1e-2 : std::nan("");   // s_memrealtime: 100 MHz
   return LLAMPC_OK;
 }
 

@@ -180,6 +180,7 @@ __device__ __forceinline__ int ctl_door(const CtlLaunch& c, double* xl, int* res
     }
     if (host) {                         // the verdict for the other blocks: x_t, drained, then the status
       if (r == (int)kCtlDoorFire) {
+        st_wt(&c.door_dev[kCtlTimeWord], (uint64_t)__builtin_amdgcn_s_memrealtime());
 #pragma unroll
         for (int q = 0; q < kCtlDoorWords - 1; ++q) st_wt(&c.door_dev[q], w[q]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -535,6 +536,9 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
     }
   }
   CTL_STAMP(blockIdx.x, 11);
+  if (tid == 0)                        // x_t on the device -> the record's stores issued (ctl.hpp)
+    __hip_atomic_store(c.host_tag + 1, (uint64_t)__builtin_amdgcn_s_memrealtime() - ld_wt(&c.door_dev[kCtlTimeWord]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __threadfence_system();              // ~0.4 us (a plain vmcnt wait: ~0.3, ctl_record_split.txt)
   __syncthreads();
   CTL_STAMP(blockIdx.x, 9);
@@ -1444,6 +1448,8 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch arg) {
   const Scratch sc(smem);
   int* flag = reinterpret_cast<int*>(smem + kFlagOff);
   const int blk = (int)blockIdx.x;
+  if (blk == 0 && threadIdx.x == 0 && !c.door)   // x_t in the argument: the device time starts here
+    st_wt(&c.door_dev[kCtlTimeWord], (uint64_t)__builtin_amdgcn_s_memrealtime());
   if (blk >= c.nb_lb + c.nb_la) {       // spec blocks (CtlLaunch.n_spec), last in the grid
     ctl_spec<LPM>(c, blk - c.nb_lb - c.nb_la, smem, sc);
     return;

@@ -346,6 +346,10 @@ struct CtlLaunch {
   // which the other blocks poll.  Block 0 gives up after door_bound (2^16 s_memrealtime units):
   // it then posts kCtlDoorExpired, stores host_seq | kCtlTagExpired, and every block exits
   // untouched.  projidx and the mu bracket then come from the state.
+  // door_dev[kCtlTimeWord] (every launch): the s_memrealtime at which x_t reached the device
+  // (armed: block 0 saw the doorbell; launched: block 0 started); the completion stores the
+  // 100 MHz ticks from it to its record stores into host_tag[1], before the tag
+  // (llampc_ctl_device_us)
   const uint64_t* door;
   uint64_t* door_dev;
   uint32_t door_seq, door_bound;
@@ -369,6 +373,7 @@ struct CtlLaunch {
 };
 constexpr int kCtlSpecMax = 64;
 constexpr int kCtlDoorWords = 13;
+constexpr int kCtlTimeWord = 13;            // door_dev's x_t time (kCtlDoorWords <= it < 16)
 constexpr uint32_t kCtlDoorFire = 1, kCtlDoorCancel = 2, kCtlDoorExpired = 3;
 constexpr uint64_t kCtlTagExpired = 1ull << 62;
 

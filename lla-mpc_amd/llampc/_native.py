@@ -148,6 +148,7 @@ _SIGNATURES = {
     "llampc_ctl_destroy": (C.c_int, [C.c_void_p]),
     "llampc_ctl_set_exchange": (C.c_int, [C.c_void_p, C.c_void_p, _dp, C.c_int64]),
     "llampc_ctl_set_prelaunch": (C.c_int, [C.c_void_p, C.c_int32]),
+    "llampc_ctl_device_us": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     "llampc_ctl_merge": (C.c_int, [_dp, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, _dp,
                                    C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "llampc_nlp_create": (C.c_int, [C.c_void_p, C.POINTER(NlpCfg), C.POINTER(C.c_void_p)]),

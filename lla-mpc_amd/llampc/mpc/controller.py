@@ -27,6 +27,7 @@ Host logic restated from the reference driver (llampc/mpc/run_nmpc_orca_llampc_r
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -200,6 +201,14 @@ class DeviceController:
         this controller cancels the armed launch first (the tick after it launches normally)."""
         nat.check(nat.load().llampc_ctl_set_prelaunch(self._h, int(bool(on))))
         self.prelaunch = bool(on)
+
+    def device_us(self) -> float:
+        """The last completed tick's device time (llampc_ctl_device_us): x_t on the device (the
+        doorbell seen, or the launch started) to the record's stores issued, in microseconds by
+        the GPU's 100 MHz clock; NaN before the first tick."""
+        v = ctypes.c_double()
+        nat.check(nat.load().llampc_ctl_device_us(self._h, ctypes.byref(v)))
+        return v.value
 
     def tick(self, x_t, out=None) -> "nat.CtlOut":
         """One blocking step; ``out`` (a CtlOut) is filled and returned (a new one if None)."""
@@ -392,6 +401,10 @@ class LLAMPC:
         """Device mode: arm every next tick (the default; DeviceController.set_prelaunch) or not."""
         if self._ctl is not None and not (self.sharded is not None and self.sharded.exchange):
             self._ctl.set_prelaunch(on)
+
+    def device_us(self) -> float:
+        """Device mode: the last tick's device time (DeviceController.device_us); else NaN."""
+        return self._ctl.device_us() if self._ctl is not None else float("nan")
 
     def tick(self, x_t) -> PlanResult:
         """One control tick.  After the warm-up (t > W) it is ONE fused launch on the bank:

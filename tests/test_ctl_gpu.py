@@ -350,10 +350,14 @@ def test_ctl_prelaunch_two_tracks_and_plan_between(nat):
         plant = O.Vehicle.from_params(O.orca_params())
         recs = []
         try:
+            assert all(np.isnan(c.device_us()) for c in ctls)      # no tick yet
             for t in range(10):
                 for c, x in zip(ctls, xs):
                     c.tick_async(x)
                 outs = [c.wait() for c in ctls]
+                # llampc_ctl_device_us: x_t on the device -> the record issued, by the GPU clock
+                dev = [c.device_us() for c in ctls]
+                assert all(np.isfinite(v) and 1.0 < v < 2000.0 for v in dev), dev
                 other.plan_raw(s[:, t], u[:, t], s[:, t + 1], np.tile(u[:, t], (20, 1))[None], s[:2, :21], u[:, t])
                 for i, o in enumerate(outs):
                     recs.append(_ctl_words(o, 40))
