@@ -1964,9 +1964,10 @@ struct llampc_nlp {
   unsigned char* d_blk = nullptr;
   unsigned char* h_blk = nullptr;        // pinned mirror
   size_t blk_bytes = 0, in_bytes = 0;
-  double* d_cost = nullptr;              // the sample blocks' sorted lists (keys, then indices), then
-                                         // the round's rate-clipped sequences [samples][H][2]
-  unsigned* d_ticket = nullptr;          // [4]: the round ticket, pad, then the round tag (u64)
+  double* d_cost = nullptr;              // the sample blocks' sorted lists as tagged words
+                                         // [3][samples / 64 x len], then the round's rate-clipped
+                                         // sequences [samples][H][2] (NlpLaunch.list_tag, cand)
+  uint64_t* d_ms_tag = nullptr;          // [2][4 HMAX]: a round's mean / std (NlpLaunch.ms_tag)
   bool per_round = false;                // one launch per round (LLAMPC_NLP_ROUND_LAUNCHES=1: A/B)
   NlpResult* h_res = nullptr;            // pinned, coherent, mapped: the last round writes it
   NlpResult* d_res = nullptr;            //   (device alias), then the solve's number into h_tag
@@ -1985,7 +1986,7 @@ int llampc_nlp_destroy(llampc_nlp* p) {
     if (p->b && p->b->stream) (void)hipStreamSynchronize(p->b->stream);
     if (p->d_blk) (void)hipFree(p->d_blk);
     if (p->d_cost) (void)hipFree(p->d_cost);
-    if (p->d_ticket) (void)hipFree(p->d_ticket);
+    if (p->d_ms_tag) (void)hipFree(p->d_ms_tag);
     if (p->h_blk) (void)hipHostFree(p->h_blk);
     if (p->h_res) (void)hipHostFree(p->h_res);
     if (p->h_tag) (void)hipHostFree(p->h_tag);
@@ -2003,8 +2004,8 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
   if (k.H < 1 || k.H > LLAMPC_HMAX) return fail(LLAMPC_E_ARG, "H=%d outside [1, %d]", k.H, LLAMPC_HMAX);
   if (k.samples < 64 || k.samples > 4096 || (k.samples & (k.samples - 1)))
     return fail(LLAMPC_E_ARG, "samples=%d: a power of two in [64, 4096]", k.samples);
-  if (k.elite < 1 || k.elite > 64 || k.elite > k.samples || k.iters < 1)
-    return fail(LLAMPC_E_ARG, "elite=%d (1..64, <= samples) iters=%d", k.elite, k.iters);
+  if (k.elite < 1 || k.elite > 64 || k.elite > k.samples || k.iters < 1 || k.iters > kNlpMaxIters)
+    return fail(LLAMPC_E_ARG, "elite=%d (1..64, <= samples) iters=%d (1..%d)", k.elite, k.iters, kNlpMaxIters);
   if (!(k.Ts > 0) || !std::isfinite(k.Ts)) return fail(LLAMPC_E_ARG, "Ts must be finite > 0");
   if (nlp_lds_bytes(k.H, k.samples, k.elite) > 160 * 1024) return fail(LLAMPC_E_ARG, "H x elite too large for LDS");
   DeviceGuard g(b->device);
@@ -2019,17 +2020,18 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
     return code;
   };
   int rc;
-  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, 2 * (size_t)k.samples * (1 + (size_t)H))) ||
-      (rc = dev_alloc(&p->d_ticket, 4)))
+  // the lists: 3 words per entry, samples / 64 x len <= samples entries
+  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, (size_t)k.samples * (3 + 2 * (size_t)H))) ||
+      (rc = dev_alloc(&p->d_ms_tag, 8 * (size_t)LLAMPC_HMAX)))
     return cleanup(rc);
   {
-    // every round in one launch needs all samples / 64 blocks resident together (each waits
+    // every round in one launch needs all samples / 64 + 1 blocks resident together (each waits
     // for the others' rounds; one block per CU by its LDS request): not on a device, or a
     // partition of one, with fewer CUs than blocks — then one launch per round
     const char* e = std::getenv("LLAMPC_NLP_ROUND_LAUNCHES");
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device) != hipSuccess) cus = 0;
-    const bool resident = k.samples / 64 <= cus;
+    const bool resident = k.samples / 64 + 1 <= cus;
     p->per_round = !nlp_persistent(k.samples) || !resident || (e && e[0] == '1');
   }
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
@@ -2043,8 +2045,10 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
   if (hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_res), p->h_res, 0) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_tag), p->h_tag, 0) != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "hipHostGetDevicePointer(NLP result) failed"));
+  // tagged words start at tag 0, which no solve uses (nlp_seq of a solve number >= 1)
   if (hipMemcpy(p->d_blk, p->h_blk, p->blk_bytes, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(p->d_ticket, 0, 4 * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      hipMemset(p->d_cost, 0, (size_t)k.samples * 3 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(p->d_ms_tag, 0, 8 * LLAMPC_HMAX * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "NLP solver upload failed"));
   *out = p;
   return LLAMPC_OK;
@@ -2089,14 +2093,12 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.st = ds;
   a.x0 = dx;
   a.xref = dx + 6;
-  a.top_key = reinterpret_cast<uint64_t*>(p->d_cost);
-  a.top_idx = reinterpret_cast<uint32_t*>(a.top_key + (size_t)(k.samples / 64) * nlp_list_len(k.elite));
-  a.cand = p->d_cost + 2 * (size_t)k.samples;
+  a.list_tag = reinterpret_cast<uint64_t*>(p->d_cost);
+  a.cand = p->d_cost + 3 * (size_t)k.samples;
   a.res = p->d_res;
   a.host_tag = p->d_tag;
   a.host_seq = p->calls + 1;
-  a.ticket = p->d_ticket;
-  a.round_tag = reinterpret_cast<uint64_t*>(p->d_ticket + 2);
+  a.ms_tag = p->d_ms_tag;
   a.seed = k.seed;
   a.call = p->calls;
   a.up0 = uprev[0];
@@ -2138,11 +2140,9 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
       HIP_TRY(hipStreamSynchronize(s));
       if (__atomic_load_n(p->h_tag, __ATOMIC_ACQUIRE) == want) break;
       // the launch has ended (its blocks give up a round wait after kNlpRoundWait): the next
-      // solve must not meet this one's state — a new call number (so stale round tags never
-      // match) and a zero ticket / round tag (ticket_last would fire early on a stale count)
+      // solve must not meet this one's state — a new call number, so none of this solve's
+      // tagged words (lists, mean / std) matches a later round's tag
       p->calls++;
-      HIP_TRY(hipMemsetAsync(p->d_ticket, 0, 4 * sizeof(unsigned), s));
-      HIP_TRY(hipStreamSynchronize(s));
       return fail(LLAMPC_E_DEVICE, "NLP solve %llu: completion tag never arrived", (unsigned long long)want);
     }
   }

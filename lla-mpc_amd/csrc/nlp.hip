@@ -2,24 +2,26 @@
 // NMPC (nmpc.py:14-203: Euler transcription of Dynamic.casadi, nmpc.py:58-60; the objective
 // nmpc.py:44-111; input bounds and the steering-rate bound nmpc.py:102-105) solved on the
 // device by the cross-entropy method — no IPOPT here (casadi is absent; its optimum is parity
-// unpinned).  One launch per iteration, all enqueued back to back, then the Euler trajectory
-// of the best sequence (integrate_kernel) and ONE copy back:
+// unpinned).  Every round in one launch (or one launch per round, nlp.hpp), then the Euler
+// trajectory of the best sequence and the result into pinned host memory:
 //
-//   sample blocks   each draws 64 sequences from the iteration's (mean, std) — Philox noise
+//   sample blocks   each draws 64 sequences from the round's (mean, std) — Philox noise
 //                   (ctl.hpp), the bounds, the rate chain in order over the horizon; sample 0 is
-//                   the mean itself, sample 1 of the first iteration holds uprev — and rolls
-//                   them out (the plan kernel's rollout, NLP-Euler, four lanes per rollout,
-//                   candidates in LDS), writing each sample's objective (+inf if infeasible);
-//                   Each block then sorts its 64 (objective, index) keys in one wave (a bitonic
-//                   network of DPP / shuffle exchanges: NaN last, ties to the lower index) and
-//                   publishes its best len = next_pow2(E) sorted;
-//   the last block  (ticket) merges the blocks' lists pairwise up a tree — the lower len of two
-//                   sorted lists is min(a_i, b_(len-1-i)), bitonic, then one half-cleaner
-//                   network in registers per level — to the E best overall in order,
-//                   regenerates the E elite sequences and sets the next mean / std to their mean
-//                   / standard deviation (NumPy's axis-0 order), keeping the best sequence seen
-//                   so far.  (A bitonic sort of all samples in LDS took 36 us of the 62 us
-//                   round: 55 barrier-separated passes.)
+//                   the mean itself, sample 1 of the first round holds uprev — and rolls them out
+//                   (the plan kernel's rollout, NLP-Euler, four lanes per rollout, candidates in
+//                   LDS), writing each sample's objective (+inf if infeasible).  Each block then
+//                   sorts its 64 (objective, index) keys in one wave (a bitonic network of
+//                   shuffle exchanges: NaN last, ties to the lower index) and publishes its best
+//                   len = next_pow2(E) sorted, as tagged words; then it draws the NEXT round's
+//                   Philox variates (they do not depend on the mean / std) while the completion
+//                   block works, and waits for the next mean / std (tagged words);
+//   the completion  (the last block of the grid, no samples) polls the lists, merges them
+//   block           pairwise up a tree — the lower len of two sorted lists is
+//                   min(a_i, b_(len-1-i)), bitonic, then one half-cleaner network in registers per
+//                   level — to the E best overall in order, reads the E elite sequences and
+//                   publishes the next mean / std as their mean / standard deviation (NumPy's
+//                   axis-0 order), keeping the best sequence seen so far.  (A bitonic sort of all
+//                   samples in LDS took 36 us of the 62 us round: 55 barrier-separated passes.)
 #include "plan_dev.hpp"
 #include "nlp.hpp"
 
@@ -27,8 +29,9 @@ namespace llampc {
 
 #ifdef LLAMPC_STAMPS
 // Diagnostic build only: s_memrealtime per block and phase of the last launch
-// (tools/diag/nlp_phases.py): 0 entry, 1 drawn, 2 rate-clipped, 3 rolled out; the completing
-// block: 4 keyed, 5 sorted, 6 elite drawn, 7 elite clipped, 8 done; 9 staged (sample blocks).
+// (tools/diag/nlp_phases.py): sample blocks 0 round start, 10 mean / std in, 1 samples formed,
+// 2 rate-clipped, 9 staged, 3 rolled out, 11 next variates drawn; the completion block 7 round
+// start, 4 lists in, 5 merged, 6 elite loaded, 8 next mean / std published.
 static __device__ unsigned long long g_nlp_ph[32][12];
 #define NLP_STAMP(slot)                                                                               \
   do {                                                                                                \
@@ -44,6 +47,10 @@ extern "C" int llampc_debug_nlp_stamps(unsigned long long* out) {
 #endif
 
 namespace {
+
+// s_memrealtime ticks (100 MHz) a block waits for a round's state before it gives up (never
+// expected: the solve then reports that its completion tag did not arrive)
+constexpr uint64_t kNlpRoundWait = 5000000;
 
 // The search's noise: one Philox4x32-10 call per PAIR of values, the counter (i / 2, call lo,
 // call hi, round + 1): value i takes the 16-bit halves (low for even i, high for odd) of the
@@ -81,15 +88,28 @@ __device__ __forceinline__ double nlp_raw_z(const NlpLaunch& a, const double* ms
 }
 
 // u_k <- clip(u_k, u_{k-1} + lo, u_{k-1} + hi) in order over k (nmpc.py:104-105 as the host
-// sampler applies it); lo > hi: no rate bound on this input
+// sampler applies it); lo > hi: no rate bound on this input.  Eight steps at a time in
+// registers: their LDS reads issue together.  (Forming the samples inside this pass too, on
+// its two waves instead of the block's four, measured 3.8 us against 1.8 + 1.7 us split.)
 __device__ __forceinline__ void nlp_rate_chain(double* u, int H, double up, double lo, double hi) {
 #pragma clang fp contract(off)
   if (!(lo <= hi)) return;
   double prev = up;
-  for (int k = 0; k < H; ++k) {
-    const double a = prev + lo, b = prev + hi;
-    prev = np_clip(u[2 * k], a, b);
-    u[2 * k] = prev;
+  for (int k0 = 0; k0 < H; k0 += 8) {
+    const int n = H - k0;
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = i < n ? u[2 * (k0 + i)] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const double a = prev + lo, b = prev + hi;
+      const double c = np_clip(v[i], a, b);
+      prev = i < n ? c : prev;
+      v[i] = c;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < n) u[2 * (k0 + i)] = v[i];
   }
 }
 
@@ -103,15 +123,56 @@ __device__ __forceinline__ double nlp_unkey(uint64_t k) {
   return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
 }
 
-// (key, index) exchange step of a bitonic network across lanes lane ^ j: the lane keeps the
+// lane ^ J's value: DPP quad_perm for J = 1, 2 (a VALU move), ds_swizzle's bit mode for J < 32
+// (no address operand), ds_bpermute for J = 32 — ds_bpermute on every step made the block
+// sort and the merge tree LDS-latency chains
+template <int J>
+__device__ __forceinline__ uint32_t nlp_xor32(uint32_t v) {
+  static_assert(J >= 1 && J <= 32 && (J & (J - 1)) == 0, "a power of two below the wave size");
+  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (J < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (J << 10));
+  else return (uint32_t)__shfl_xor((int)v, J, 64);
+}
+
+// (key, index) exchange step of a bitonic network across lanes lane ^ J: the lane keeps the
 // smaller pair when `low`, else the larger (indices are distinct, so the order is total)
-__device__ __forceinline__ void nlp_cx(uint64_t& k, uint32_t& i, int j, bool low) {
-  const uint64_t pk = __shfl_xor(k, j, 64);
-  const uint32_t pi = __shfl_xor(i, j, 64);
+template <int J>
+__device__ __forceinline__ void nlp_cx(uint64_t& k, uint32_t& i, bool low) {
+  const uint64_t pk = ((uint64_t)nlp_xor32<J>((uint32_t)(k >> 32)) << 32) | nlp_xor32<J>((uint32_t)k);
+  const uint32_t pi = nlp_xor32<J>(i);
   const bool pless = pk < k || (pk == k && pi < i);
   if (low == pless) {
     k = pk;
     i = pi;
+  }
+}
+
+// the half-cleaner steps J, J / 2, .., 1 of a bitonic merge of blocks of W lanes
+// (W = 0: the merge tree's, each lane keeping the lower when its bit J is clear)
+template <int W, int J>
+__device__ __forceinline__ void nlp_clean(uint64_t& k, uint32_t& i, int lane) {
+  nlp_cx<J>(k, i, W ? (((lane & J) == 0) == ((lane & W) == 0)) : ((lane & J) == 0));
+  if constexpr (J > 1) nlp_clean<W, J / 2>(k, i, lane);
+}
+
+// the wave's 64 (key, index) pairs sorted ascending across the lanes (bitonic)
+template <int W = 2>
+__device__ __forceinline__ void nlp_sort64(uint64_t& k, uint32_t& i, int lane) {
+  nlp_clean<W, W / 2>(k, i, lane);
+  if constexpr (W < 64) nlp_sort64<2 * W>(k, i, lane);
+}
+
+// a bitonic sequence of len lanes (a group inside the wave) sorted ascending
+__device__ __forceinline__ void nlp_clean_len(uint64_t& k, uint32_t& i, int lane, int len) {
+  switch (len) {                        // block-uniform
+    case 64: nlp_clean<0, 32>(k, i, lane); break;
+    case 32: nlp_clean<0, 16>(k, i, lane); break;
+    case 16: nlp_clean<0, 8>(k, i, lane); break;
+    case 8: nlp_clean<0, 4>(k, i, lane); break;
+    case 4: nlp_clean<0, 2>(k, i, lane); break;
+    case 2: nlp_clean<0, 1>(k, i, lane); break;
+    default: break;
   }
 }
 
@@ -177,25 +238,68 @@ __device__ __forceinline__ void nlp_traj_quad(const NlpLaunch& a, const double* 
   }
 }
 
-// Round `it`'s completion (the block that added the last ticket): the elite, the next mean /
-// std, the best so far.  The state is handed to the next round's blocks (other CUs, other
-// XCDs) by sc1 stores and loads, as the sample blocks' lists (st_wt / ld_wt).
-__device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem, int it) {
+// The completion block's LDS: the lists' keys kA | kB and indices iA | iB ([nl * len] each,
+// the merge tree's two buffers), then the elite sequences [E][H][2].
+struct NlpCompLds {
+  uint64_t *kA, *kB;
+  uint32_t *iA, *iB;
+  double* eu;
+};
+__device__ __forceinline__ NlpCompLds nlp_comp_lds(unsigned char* smem, int nl, int len) {
+  NlpCompLds L;
+  L.kA = reinterpret_cast<uint64_t*>(smem + kScratchBytes);
+  L.kB = L.kA + (size_t)nl * len;
+  L.iA = reinterpret_cast<uint32_t*>(L.kB + (size_t)nl * len);
+  L.iB = L.iA + (size_t)nl * len;
+  L.eu = reinterpret_cast<double*>(smem + kScratchBytes + 24 * (size_t)nl * len);
+  return L;
+}
+
+// Waits (bounded) for tagged words; returns the block's verdict (every thread the same).
+__device__ __forceinline__ bool nlp_block_ok(int ok, int* rflag) {
+  if (threadIdx.x == 0) *rflag = 1;
+  __syncthreads();
+  if (!ok) *rflag = 0;
+  __syncthreads();
+  return *rflag != 0;
+}
+
+// The completion block: every sample block's sorted list of the round (tag sq) into kA / iA.
+__device__ __forceinline__ bool nlp_poll_lists(const NlpLaunch& a, const NlpCompLds& L, int nl, uint32_t sq,
+                                               int* rflag) {
+  const int nbl = nl * nlp_list_len(a.elite);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  int ok = 1;
+  for (int e = threadIdx.x; e < nbl && ok; e += kBlock) {
+    for (;;) {
+      const uint64_t hi = ld_wt(&a.list_tag[e]), lo = ld_wt(&a.list_tag[nbl + e]), ix = ld_wt(&a.list_tag[2 * nbl + e]);
+      if ((int)tag_ok(hi, sq) & (int)tag_ok(lo, sq) & (int)tag_ok(ix, sq)) {
+        L.kA[e] = join_words(hi, lo);
+        L.iA[e] = (uint32_t)ix;
+        break;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kNlpRoundWait) {
+        ok = 0;
+        break;
+      }
+    }
+  }
+  return nlp_block_ok(ok, rflag);
+}
+
+// Round `it`'s completion (the completion block, the lists in kA / iA): the elite, the next
+// mean / std (tagged words for the sample blocks, which may sit on other XCDs), the best so far.
+__device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem, int it, int nl) {
 #pragma clang fp contract(off)
   const int tid = threadIdx.x, H = a.H, E = a.elite;
-  const int len = nlp_list_len(E), nl = (int)gridDim.x;
+  const int len = nlp_list_len(E);
   NlpState* st = a.st;
-  uint64_t* kA = reinterpret_cast<uint64_t*>(smem + kScratchBytes);       // [nl * len] x 2
-  uint64_t* kB = kA + (size_t)nl * len;
-  uint32_t* iA = reinterpret_cast<uint32_t*>(kB + (size_t)nl * len);
-  uint32_t* iB = iA + (size_t)nl * len;
-  double* eu = reinterpret_cast<double*>(smem + kScratchBytes + 24 * (size_t)nl * len);   // [E][H][2]
-  for (int e = tid; e < nl * len; e += kBlock) {
-    kA[e] = ld_wt(&a.top_key[e]);
-    iA[e] = ld_wt(&a.top_idx[e]);
-  }
-  __syncthreads();
-  NLP_STAMP(4);
+  const NlpCompLds L = nlp_comp_lds(smem, nl, len);
+  uint64_t* kA = L.kA;
+  uint64_t* kB = L.kB;
+  uint32_t* iA = L.iA;
+  uint32_t* iB = L.iB;
+  double* eu = L.eu;                                                  // [E][H][2]
   // merge tree: lists 2g, 2g + 1 -> list g; a group of len lanes (inside one wave) per pair
   for (int n = nl; n > 1; n >>= 1) {
     const int pairs = n >> 1, gpp = kBlock / len, i = tid & (len - 1);
@@ -210,7 +314,7 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
           k = kb;
           x = xb;
         }
-        for (int j = len >> 1; j > 0; j >>= 1) nlp_cx(k, x, j, (i & j) == 0);
+        nlp_clean_len(k, x, i, len);
         kB[(size_t)g * len + i] = k;
         iB[(size_t)g * len + i] = x;
       }
@@ -270,19 +374,24 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
       const double d = at(e) - m;
       s += d * d;
     }
-    st_wt(&st->mean[k][j], m);
-    st_wt(&st->std_[k][j], sqrt(s / E) + a.std_floor);
+    if (it + 1 < a.iters) {             // the next round's mean / std, tagged halves (low, high)
+      const uint32_t sq1 = nlp_seq(a.host_seq, it + 1);
+      const uint64_t mb = (uint64_t)__double_as_longlong(m);
+      const uint64_t sb = (uint64_t)__double_as_longlong(sqrt(s / E) + a.std_floor);
+      const int im = 2 * k + j, is = 2 * H + 2 * k + j;
+      st_wt(&a.ms_tag[2 * im], tag_word(sq1, (uint32_t)mb));
+      st_wt(&a.ms_tag[2 * im + 1], tag_word(sq1, (uint32_t)(mb >> 32)));
+      st_wt(&a.ms_tag[2 * is], tag_word(sq1, (uint32_t)sb));
+      st_wt(&a.ms_tag[2 * is + 1], tag_word(sq1, (uint32_t)(sb >> 32)));
+    }
     if (better) st_wt(&st->best_u[k][j], eu[2 * k + j]);
   }
   // the result (the last round): best objective and round, before this round's update
   const double bj = better ? c0 : bj0;
   const int bit = better ? it : bit0;
-  if (tid == 0) {
-    if (better) {
-      st_wt(&st->best_j, c0);
-      st_wt(&st->best_it, it);
-    }
-    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0 && better) {
+    st_wt(&st->best_j, c0);
+    st_wt(&st->best_it, it);
   }
   NLP_STAMP(8);
   if (it == a.iters - 1) nlp_trajectory(a, smem, eu, better, bj, bit);
@@ -296,16 +405,38 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
 // 64 x H x 64 B fit beside the rest (H <= kNlpStageH).
 constexpr int kNlpStageH = 28;
 
-// s_memrealtime ticks (100 MHz) a block waits for a round's state before it gives up (never
-// expected: the solve then reports that its completion tag did not arrive)
-constexpr uint64_t kNlpRoundWait = 5000000;
+// The round's Philox variates z of this block's samples into Ul (value (s H + k) 2 + j; the
+// pair (s H + k) shares one call): independent of the round's mean / std, so a block draws the
+// next round's while the completion block works.
+__device__ __forceinline__ void nlp_draw(const NlpLaunch& a, int blk, int it, double* Ul) {
+  constexpr int kPerBlock = kBlock / 4;
+  const int H = a.H;
+  for (int e = threadIdx.x; e < kPerBlock * H; e += kBlock) {
+    const int rr = e / H, k = e - rr * H, s = blk * kPerBlock + rr;
+    double z0, z1;
+    nlp_z2((uint32_t)(s * H + k), a.call, a.seed, (uint32_t)(it + 1), z0, z1);
+    Ul[2 * e] = z0;
+    Ul[2 * e + 1] = z1;
+  }
+}
 
 template <bool ST>
 __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const Scratch sc(smem);
-  int* flag = reinterpret_cast<int*>(smem + kFlagOff);
+  int* rflag = reinterpret_cast<int*>(smem + kFlagOff);   // a bounded wait's block verdict
   const int tid = threadIdx.x, H = a.H, blk = (int)blockIdx.x;
+  const int nl = (int)gridDim.x - 1;    // sample blocks; block nl completes every round
+  if (blk == nl) {
+    const NlpCompLds L = nlp_comp_lds(smem, nl, nlp_list_len(a.elite));
+    for (int r = 0; r < a.rounds; ++r) {
+      const int it = a.it + r;
+      NLP_STAMP(7);
+      if (!nlp_poll_lists(a, L, nl, nlp_seq(a.host_seq, it), rflag)) return;
+      NLP_STAMP(4);
+      nlp_complete(a, smem, it, nl);
+    }
+    return;
+  }
   constexpr int LPM = 4, kPerBlock = kBlock / LPM;   // 64 samples per block
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);            // xref [H+1][2]
   double* Ul = sx + 2 * (H + 1);                                            // [64][H][2]
@@ -313,43 +444,48 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   uint64_t* ks = reinterpret_cast<uint64_t*>(x0 + 6);                       // [64] the samples' keys
   double* ms = reinterpret_cast<double*>(ks + 64);                          // the round's mean, std [2][H][2]
   double* su = ms + 4 * (size_t)H;                                          // ST: [H][64][kStageW]
-  int* rflag = flag + 1;                // the round wait's verdict (flag is ticket_last's)
   const NlpState* st = a.st;
+  const int len = nlp_list_len(a.elite), nbl = nl * len;
+  for (int e = tid; e <= H; e += kBlock) {   // the solve's inputs (this block's LDS only)
+    sx[2 * e] = a.xref[e];
+    sx[2 * e + 1] = a.xref[(H + 1) + e];
+  }
+  if (tid < 6) x0[tid] = a.x0[tid];
+  nlp_draw(a, blk, a.it, Ul);               // the first round's variates
   for (int r = 0; r < a.rounds; ++r) {
     const int it = a.it + r;
-    if (r > 0) {                        // the previous round's completion published round it
-      if (tid == 0) {
-        const uint64_t want = tag_word((uint32_t)a.host_seq, (uint32_t)it);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        int ok = 1;
-        while (ld_wt(a.round_tag) != want)
+    const uint32_t sq = nlp_seq(a.host_seq, it);
+    NLP_STAMP(0);
+    // the round's mean / std: the host-staged state (round 0), else the previous round's
+    // completion's tagged halves
+    if (it == 0) {
+      for (int e = tid; e < 4 * H; e += kBlock)
+        ms[e] = ld_wt(e < 2 * H ? &st->mean[0][0] + e : &st->std_[0][0] + (e - 2 * H));
+    } else {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int ok = 1;
+      for (int i = tid; i < 4 * H && ok; i += kBlock) {
+        for (;;) {
+          const uint64_t lo = ld_wt(&a.ms_tag[2 * i]), hi = ld_wt(&a.ms_tag[2 * i + 1]);
+          if ((int)tag_ok(lo, sq) & (int)tag_ok(hi, sq)) {
+            ms[i] = __longlong_as_double((long long)join_words(hi, lo));
+            break;
+          }
           if (__builtin_amdgcn_s_memrealtime() - t0 > kNlpRoundWait) {
             ok = 0;
             break;
           }
-        *rflag = ok;
+        }
       }
-      __syncthreads();
-      if (!*rflag) return;
+      if (!nlp_block_ok(ok, rflag)) return;
     }
-    NLP_STAMP(0);
-    // the round's inputs (the completing block of the previous round used this LDS)
-    for (int e = tid; e <= H; e += kBlock) {
-      sx[2 * e] = a.xref[e];
-      sx[2 * e + 1] = a.xref[(H + 1) + e];
-    }
-    if (tid < 6) x0[tid] = a.x0[tid];
-    for (int e = tid; e < 4 * H; e += kBlock)
-      ms[e] = ld_wt(e < 2 * H ? &st->mean[0][0] + e : &st->std_[0][0] + (e - 2 * H));
     __syncthreads();
-    // value i = (s H + k) 2 + j of the round; pair i / 2 = (s H + k): the (j = 0, 1) values of
-    // one (sample, step) share a Philox call
+    NLP_STAMP(10);
+    // the samples from their variates (drawn ahead): the bounds
     for (int e = tid; e < kPerBlock * H; e += kBlock) {
       const int rr = e / H, k = e - rr * H, s = blk * kPerBlock + rr;
-      double z0, z1;
-      nlp_z2((uint32_t)(s * H + k), a.call, a.seed, (uint32_t)(it + 1), z0, z1);
-      Ul[2 * e] = nlp_raw_z(a, ms, it, s, k, 0, z0);
-      Ul[2 * e + 1] = nlp_raw_z(a, ms, it, s, k, 1, z1);
+      Ul[2 * e] = nlp_raw_z(a, ms, it, s, k, 0, Ul[2 * e]);
+      Ul[2 * e + 1] = nlp_raw_z(a, ms, it, s, k, 1, Ul[2 * e + 1]);
     }
     __syncthreads();
     NLP_STAMP(1);
@@ -359,6 +495,8 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     }
     __syncthreads();
     NLP_STAMP(2);
+    // the rate-clipped sequences for the completion block's elite (each wave drains these
+    // stores before its list is published, below)
     for (int e = tid; e < kPerBlock * H * 2; e += kBlock) st_wt(&a.cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
     const fm::FmK K = fm::FmK::load();
     if constexpr (ST) {
@@ -424,25 +562,23 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     }
     NLP_STAMP(3);
     if (sub == 0) ks[c] = nlp_key(J);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's candidate stores (above)
     __syncthreads();
     if (tid < 64) {                     // wave 0: the block's 64 keys sorted (bitonic, in registers)
       uint64_t k = ks[tid];
       uint32_t x = (uint32_t)(blk * kPerBlock + tid);
-      for (int w = 2; w <= 64; w <<= 1)
-        for (int j = w >> 1; j > 0; j >>= 1) nlp_cx(k, x, j, ((tid & j) == 0) == ((tid & w) == 0));
-      const int len = nlp_list_len(a.elite);
-      if (tid < len) {
-        st_wt(&a.top_key[(size_t)blk * len + tid], k);
-        st_wt(&a.top_idx[(size_t)blk * len + tid], x);
+      nlp_sort64(k, x, tid);
+      if (tid < len) {                  // the list as tagged words (nlp.hpp NlpLaunch.list_tag)
+        const int e = blk * len + tid;
+        st_wt(&a.list_tag[e], tag_word(sq, (uint32_t)(k >> 32)));
+        st_wt(&a.list_tag[nbl + e], tag_word(sq, (uint32_t)k));
+        st_wt(&a.list_tag[2 * nbl + e], tag_word(sq, x));
       }
     }
-    if (!ticket_last(a.ticket, gridDim.x, flag)) continue;
-    nlp_complete(a, smem, it);
-    if (r + 1 < a.rounds) {             // publish the next round: its state stored sc1, drained
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) st_wt(a.round_tag, tag_word((uint32_t)a.host_seq, (uint32_t)(it + 1)));
-    }
+    // the next round's variates while the completion block works (Ul is dead: every wave's
+    // rollout ended before the barrier above)
+    if (r + 1 < a.rounds) nlp_draw(a, blk, it + 1, Ul);
+    NLP_STAMP(11);
   }
 }
 
@@ -456,12 +592,13 @@ size_t nlp_lds_bytes(int H, int samples, int elite) {
 
 hipError_t launch_nlp(const NlpLaunch& a, hipStream_t s) {
   const size_t lds = std::max<size_t>(nlp_lds_bytes(a.H, a.samples, a.elite), 82 * 1024);
+  const dim3 grid(a.samples / 64 + 1);  // the sample blocks, then the completion block
   if (a.H <= kNlpStageH) {
     allow_lds(nlp_kernel<true>);
-    hipLaunchKernelGGL(nlp_kernel<true>, dim3(a.samples / 64), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL(nlp_kernel<true>, grid, dim3(kBlock), lds, s, a);
   } else {
     allow_lds(nlp_kernel<false>);
-    hipLaunchKernelGGL(nlp_kernel<false>, dim3(a.samples / 64), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL(nlp_kernel<false>, grid, dim3(kBlock), lds, s, a);
   }
   return hipGetLastError();
 }

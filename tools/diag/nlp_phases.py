@@ -1,7 +1,8 @@
 """Diagnostic (stamps build): phases of the setupNLP.solve CEM round launches — per block
-(µs from the first block's entry, s_memrealtime): drawn, rate-clipped, rolled out; the
-completing block: 4 lists loaded, 5 merged, 6 elite loaded, 8 mean/std done — for the last
-round of a few solves.  usage: python tools/diag/nlp_phases.py"""
+(µs from the first sample block's round start, s_memrealtime): mean / std in, samples formed,
+rate-clipped, staged, rolled out, next variates drawn; the completion block: 7 round start,
+4 lists in, 5 merged, 6 elite loaded, 8 next mean / std published — for the last round of a
+few solves.  usage: python tools/diag/nlp_phases.py"""
 import ctypes
 import os
 import sys
@@ -36,9 +37,9 @@ for t in range(10, 16):
     nb = nlp.samples // 64
     base = Z[:nb, 0].min()
     us = lambda v: (v - base) / 100.0  # noqa: E731
-    win = int(np.argmax(Z[:nb, 8]))
-    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (1, 2, 9, 3)]
-    comp = [f"{k}: {us(Z[win, k]):.1f}" for k in (4, 5, 6, 8)]
-    print(f"solve {t}: blocks drawn/clipped/rolled (min/max) {' '.join(row)} | completion (block {win}) {' '.join(comp)}",
-          flush=True)
+    win = nb                                   # the completion block: the grid's last
+    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (10, 1, 2, 9, 3, 11)]
+    comp = [f"{k}: {us(Z[win, k]):.1f}" for k in (7, 4, 5, 6, 8)]
+    print(f"solve {t}: sample blocks ms/formed/clipped/staged/rolled/next-drawn (min/max) {' '.join(row)} | "
+          f"completion block {' '.join(comp)}", flush=True)
 nlp.close()
