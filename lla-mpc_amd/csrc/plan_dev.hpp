@@ -53,6 +53,14 @@ static __device__ unsigned long long g_rl_ph[1024][4];         // raceline prolo
       }                                                                                  \
     }                                                                                    \
   } while (0)
+// per rollout step (FAST rollouts, thread 0 of every block < 1024): s_memtime before step k
+// (k < 24) and at the loop's end (slot 24) — the first step's cold code fetch against the rest
+static __device__ unsigned long long g_la_step[1024][25];
+#define STEP_STAMP(k)                                                                    \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && (k) <= 24)                              \
+      g_la_step[blockIdx.x][k] = __builtin_amdgcn_s_memtime();                           \
+  } while (0)
 #define STAMP(slot)                                                                      \
   do {                                                                                   \
     if (threadIdx.x == 0) {                                                              \
@@ -72,6 +80,9 @@ static __device__ unsigned long long g_wq_unit[256][8][16][4][2];
     }                                                                                    \
   } while (0)
 #else
+#define STEP_STAMP(k) \
+  do {                \
+  } while (0)
 #define WQ_STAMP(blk, j, slot) \
   do {                         \
   } while (0)
@@ -735,6 +746,7 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   Dom dm;                               // FAST: the operands' running extremes
   dm.init();
   for (int k = 0; k < H; ++k) {
+    if (FAST) STEP_STAMP(k < 24 ? k : 24);
     double ua, ud;
     Input u;
     FusedIn fi{};

@@ -29,6 +29,9 @@ extern "C" int llampc_debug_la_wave(unsigned long long* out) {
 extern "C" int llampc_debug_la_all(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_all), sizeof(g_la_all)) == hipSuccess ? 0 : -2;
 }
+extern "C" int llampc_debug_la_step(unsigned long long* out) {   // [1024][25]
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_step), sizeof(g_la_step)) == hipSuccess ? 0 : -2;
+}
 extern "C" int llampc_debug_la_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_la_stamps), sizeof(g_la_stamps)) == hipSuccess ? 0 : -2;
 }
