@@ -47,11 +47,11 @@ FLOPS_PER_MODEL_STEP = 264 + 7  # RK4 step + cost accumulation
 # Issue roofline: instructions per rollout step of the fast look-ahead loop, per lane, by lane
 # split (tools/diag/isa_counts.py on the current sources), and the chip's fp64 VALU issue
 # capacity: 1,024 SIMDs x 16 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md max clock).
-ISSUE_INSTR_PER_STEP = {4: 444, 2: 556, 1: 777}   # tools/diag/isa_counts.py (LPM 1: work queue)
+ISSUE_INSTR_PER_STEP = {4: 456, 2: 568, 1: 809}   # tools/diag/isa_counts.py, 8-term cores (LPM 1: work queue)
 ISSUE_PEAK_LANE_INSTR = 1024 * 16 * 2.4e9
 # the controller's and the NLP search's rollout steps (tools/diag/isa_counts.py): the
 # controller's LPM-4 step with its staged input terms, the NLP's LPM-4 Euler step with staged terms
-CTL_INSTR_PER_STEP = 446
+CTL_INSTR_PER_STEP = 453
 NLP_INSTR_PER_STEP = 159
 LOOKBACK_INSTR_PER_MODEL = ISSUE_INSTR_PER_STEP[1]   # one LPM-1 RK4 step + error + ring per model (upper bound)
 

@@ -22,7 +22,7 @@ def listing(tu):
     return open(out).read().split("\n")
 
 
-def loop_of(asm, pattern):
+def loop_of(asm, pattern, fmin=150, rcp=1):
     s = next(i for i, l in enumerate(asm) if re.match(pattern, l))
     e = next(i for i in range(s, len(asm)) if "s_endpgm" in asm[i])
     body = asm[s:e]
@@ -35,7 +35,7 @@ def loop_of(asm, pattern):
             n = sum(1 for x in seg if re.match(r"^\s+(v_|s_)", x))
             f = sum(1 for x in seg if re.match(r"^\s+v_\w+_f64", x))
             # the rollout step: the innermost loop with the division and most fp64 work
-            if any("v_rcp_f64" in x for x in seg) and 200 < n < 2000 and f > 150 and (best is None or n < best[0]):
+            if sum("v_rcp_f64" in x for x in seg) >= rcp and 200 < n < 2000 and f > fmin and (best is None or n < best[0]):
                 best = (n, seg)
     return best
 
@@ -61,4 +61,6 @@ report("plan LPM 1 (staged)", loop_of(asm1, r"^_ZN6llampc11plan_kernelILi0ELb1EL
 report("plan LPM 1 (work queue, 8 waves)", loop_of(asm1, r"^_ZN6llampc11plan_kernelILi0ELb1ELi1ELi0ELb0ELi2E\S+:"))
 asmc = listing("ctl")
 for lpm in (4, 2, 1):
-    report(f"ctl LPM {lpm} (staged inputs)", loop_of(asmc, rf"^_ZN6llampc10ctl_kernelILi{lpm}EEEvNS_9CtlLaunchE:"))
+    # a whole RK4 step: 4 stages x 2 chains' divisions (the look-back's and the walker's loops
+    # divide too)
+    report(f"ctl LPM {lpm} (staged inputs)", loop_of(asmc, rf"^_ZN6llampc10ctl_kernelILi{lpm}ELb0EEEvNS_9CtlLaunchE:", 300, 8))
