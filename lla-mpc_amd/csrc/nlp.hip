@@ -189,7 +189,7 @@ __device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, unsigned char
   __syncthreads();                      // the elite rows are read; best_u is final
   double* sx = ub + 2 * (size_t)H;      // after the sequence: xref [H+1][2], x0 [6]
   double* x0 = sx + 2 * (size_t)(H + 1);
-  for (int e = tid; e < 2 * H; e += kBlock) {
+  for (int e = tid; e < 2 * H; e += (int)blockDim.x) {
     const double v = better ? ub[e] : ld_wt(&st->best_u[0][0] + e);   // an earlier round's completion
     ub[e] = v;
     (&res->best_u[0][0])[e] = v;
@@ -198,7 +198,7 @@ __device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, unsigned char
     res->best_j = bj;
     res->best_it = bit;
   }
-  for (int e = tid; e <= H; e += kBlock) {
+  for (int e = tid; e <= H; e += (int)blockDim.x) {
     sx[2 * e] = a.xref[e];
     sx[2 * e + 1] = a.xref[(H + 1) + e];
   }
@@ -270,7 +270,7 @@ __device__ __forceinline__ bool nlp_poll_lists(const NlpLaunch& a, const NlpComp
   const int nbl = nl * nlp_list_len(a.elite);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   int ok = 1;
-  for (int e = threadIdx.x; e < nbl && ok; e += kBlock) {
+  for (int e = threadIdx.x; e < nbl && ok; e += (int)blockDim.x) {
     for (;;) {
       const uint64_t hi = ld_wt(&a.list_tag[e]), lo = ld_wt(&a.list_tag[nbl + e]), ix = ld_wt(&a.list_tag[2 * nbl + e]);
       if ((int)tag_ok(hi, sq) & (int)tag_ok(lo, sq) & (int)tag_ok(ix, sq)) {
@@ -302,7 +302,7 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   double* eu = L.eu;                                                  // [E][H][2]
   // merge tree: lists 2g, 2g + 1 -> list g; a group of len lanes (inside one wave) per pair
   for (int n = nl; n > 1; n >>= 1) {
-    const int pairs = n >> 1, gpp = kBlock / len, i = tid & (len - 1);
+    const int pairs = n >> 1, gpp = (int)blockDim.x / len, i = tid & (len - 1);
     for (int g0 = 0; g0 < pairs; g0 += gpp) {                      // block-uniform
       const int g = g0 + tid / len;
       if (g < pairs) {
@@ -330,7 +330,7 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   NLP_STAMP(5);
   const uint32_t* idx = iA;                                        // the E best, in order
   // the elite sequences (the sample blocks' rate-clipped candidates)
-  for (int e = tid; e < E * H * 2; e += kBlock) {
+  for (int e = tid; e < E * H * 2; e += (int)blockDim.x) {
     const int r = e / (2 * H), q = e - r * 2 * H;
     eu[e] = ld_wt(&a.cand[2 * (size_t)idx[r] * H + q]);
   }
@@ -409,9 +409,9 @@ constexpr int kNlpStageH = 28;
 // pair (s H + k) shares one call): independent of the round's mean / std, so a block draws the
 // next round's while the completion block works.
 __device__ __forceinline__ void nlp_draw(const NlpLaunch& a, int blk, int it, double* Ul) {
-  constexpr int kPerBlock = kBlock / 4;
+  constexpr int kPerBlock = 64;
   const int H = a.H;
-  for (int e = threadIdx.x; e < kPerBlock * H; e += kBlock) {
+  for (int e = threadIdx.x; e < kPerBlock * H; e += (int)blockDim.x) {
     const int rr = e / H, k = e - rr * H, s = blk * kPerBlock + rr;
     double z0, z1;
     nlp_z2((uint32_t)(s * H + k), a.call, a.seed, (uint32_t)(it + 1), z0, z1);
@@ -420,8 +420,10 @@ __device__ __forceinline__ void nlp_draw(const NlpLaunch& a, int blk, int it, do
   }
 }
 
-template <bool ST>
-__global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
+// NT threads: the rollouts take the first 256 (a quad per sample); the other waves share the
+// sample blocks' per-round loops (bounds, staging, draws), two waves per SIMD
+template <bool ST, int NT>
+__global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int* rflag = reinterpret_cast<int*>(smem + kFlagOff);   // a bounded wait's block verdict
   const int tid = threadIdx.x, H = a.H, blk = (int)blockIdx.x;
@@ -437,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     }
     return;
   }
-  constexpr int LPM = 4, kPerBlock = kBlock / LPM;   // 64 samples per block
+  constexpr int LPM = 4, kPerBlock = 64;             // 64 samples per block, a quad each
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);            // xref [H+1][2]
   double* Ul = sx + 2 * (H + 1);                                            // [64][H][2]
   double* x0 = Ul + 2 * (size_t)kPerBlock * H;                              // [6]
@@ -446,7 +448,7 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
   double* su = ms + 4 * (size_t)H;                                          // ST: [H][64][kStageW]
   const NlpState* st = a.st;
   const int len = nlp_list_len(a.elite), nbl = nl * len;
-  for (int e = tid; e <= H; e += kBlock) {   // the solve's inputs (this block's LDS only)
+  for (int e = tid; e <= H; e += NT) {   // the solve's inputs (this block's LDS only)
     sx[2 * e] = a.xref[e];
     sx[2 * e + 1] = a.xref[(H + 1) + e];
   }
@@ -459,12 +461,12 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     // the round's mean / std: the host-staged state (round 0), else the previous round's
     // completion's tagged halves
     if (it == 0) {
-      for (int e = tid; e < 4 * H; e += kBlock)
+      for (int e = tid; e < 4 * H; e += NT)
         ms[e] = ld_wt(e < 2 * H ? &st->mean[0][0] + e : &st->std_[0][0] + (e - 2 * H));
     } else {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       int ok = 1;
-      for (int i = tid; i < 4 * H && ok; i += kBlock) {
+      for (int i = tid; i < 4 * H && ok; i += NT) {
         for (;;) {
           const uint64_t lo = ld_wt(&a.ms_tag[2 * i]), hi = ld_wt(&a.ms_tag[2 * i + 1]);
           if ((int)tag_ok(lo, sq) & (int)tag_ok(hi, sq)) {
@@ -482,7 +484,7 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     __syncthreads();
     NLP_STAMP(10);
     // the samples from their variates (drawn ahead): the bounds
-    for (int e = tid; e < kPerBlock * H; e += kBlock) {
+    for (int e = tid; e < kPerBlock * H; e += NT) {
       const int rr = e / H, k = e - rr * H, s = blk * kPerBlock + rr;
       Ul[2 * e] = nlp_raw_z(a, ms, it, s, k, 0, Ul[2 * e]);
       Ul[2 * e + 1] = nlp_raw_z(a, ms, it, s, k, 1, Ul[2 * e + 1]);
@@ -497,13 +499,13 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     NLP_STAMP(2);
     // the rate-clipped sequences for the completion block's elite (each wave drains these
     // stores before its list is published, below)
-    for (int e = tid; e < kPerBlock * H * 2; e += kBlock) st_wt(&a.cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
+    for (int e = tid; e < kPerBlock * H * 2; e += NT) st_wt(&a.cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
     const fm::FmK K = fm::FmK::load();
     if constexpr (ST) {
       const CostK& q0 = a.la.cost;
       // consecutive threads take consecutive candidates of one step: their 64-B records are
       // adjacent in LDS (one step per thread-row was a 4 KB stride: every write one bank)
-      for (int f = tid; f < kPerBlock * H; f += kBlock) {
+      for (int f = tid; f < kPerBlock * H; f += NT) {
         const int k = f >> 6, c = f & (kPerBlock - 1), e = c * H + k;
         const double ua = Ul[2 * e], dl = Ul[2 * e + 1];
         double sd, cd;
@@ -523,6 +525,7 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
       NLP_STAMP(9);
     }
     // rollouts: a quad per sample (the plan kernel's NLP-Euler fast stage + the general re-run)
+    if (tid < kPerBlock * LPM) {        // whole waves
     const int sub = tid % LPM, c = tid / LPM;
     const Tire t = load_tire(a.la.params, 1, 0);
     CostK q = a.la.cost;
@@ -562,6 +565,7 @@ __global__ __launch_bounds__(kBlock) void nlp_kernel(NlpLaunch a) {
     }
     NLP_STAMP(3);
     if (sub == 0) ks[c] = nlp_key(J);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's candidate stores (above)
     __syncthreads();
     if (tid < 64) {                     // wave 0: the block's 64 keys sorted (bitonic, in registers)
@@ -594,11 +598,11 @@ hipError_t launch_nlp(const NlpLaunch& a, hipStream_t s) {
   const size_t lds = std::max<size_t>(nlp_lds_bytes(a.H, a.samples, a.elite), 82 * 1024);
   const dim3 grid(a.samples / 64 + 1);  // the sample blocks, then the completion block
   if (a.H <= kNlpStageH) {
-    allow_lds(nlp_kernel<true>);
-    hipLaunchKernelGGL(nlp_kernel<true>, grid, dim3(kBlock), lds, s, a);
+    allow_lds(nlp_kernel<true, 2 * kBlock>);
+    hipLaunchKernelGGL((nlp_kernel<true, 2 * kBlock>), grid, dim3(2 * kBlock), lds, s, a);
   } else {
-    allow_lds(nlp_kernel<false>);
-    hipLaunchKernelGGL(nlp_kernel<false>, grid, dim3(kBlock), lds, s, a);
+    allow_lds(nlp_kernel<false, kBlock>);
+    hipLaunchKernelGGL((nlp_kernel<false, kBlock>), grid, dim3(kBlock), lds, s, a);
   }
   return hipGetLastError();
 }
