@@ -17,10 +17,9 @@ python3 -c "
 import json
 d=json.loads(open('$OUT/bench_default.json').read().strip().splitlines()[-1])
 print('tick', round(d['ms_per_step']*1e3,2), 'us; kernel', round(d['kernel_us']['plan'],2))
-e=d.get('extra',{})
-c=e.get('controller_tick_us',{})
-print('controller p50/p99/max', c.get('p50'), c.get('p99'), c.get('max'), 'kernel', c.get('kernel_us_avg'))
-s=e.get('solve_us',{})
+c=d.get('controller_tick_us') or {}
+print('controller p50/p99/max', c.get('p50'), c.get('p99'), c.get('max'), 'kernel', c.get('kernel_us_avg'), 'device', (c.get('device_us') or {}).get('armed'))
+s=d.get('solve_us') or {}
 print('solve p50', s.get('p50'))
 "
 echo "[$(date +%T)] bench (driver)"
@@ -28,5 +27,5 @@ timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench_k20.jso
 python3 -c "
 import json
 d=json.loads(open('$OUT/bench_k20.json').read().strip().splitlines()[-1])
-print('K20 tick', round(d['ms_per_step']*1e3,2), 'us; kernel', round(d['kernel_us']['plan'],2), 'ctl', d.get('extra',{}).get('controller_tick_us',{}).get('p50'))"
+print('K20 tick', round(d['ms_per_step']*1e3,2), 'us; kernel', round(d['kernel_us']['plan'],2), 'ctl', (d.get('controller_tick_us') or {}).get('p50'))"
 echo "[$(date +%T)] done"
