@@ -289,7 +289,11 @@ __device__ __forceinline__ bool nlp_poll_lists(const NlpLaunch& a, const NlpComp
 
 // Round `it`'s completion (the completion block, the lists in kA / iA): the elite, the next
 // mean / std (tagged words for the sample blocks, which may sit on other XCDs), the best so far.
-__device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem, int it, int nl) {
+// bj / bit: the best objective so far and its round, carried in registers across the launch's
+// rounds (the state's copy, read back sc1 every round, put a memory round trip on each
+// round's critical path); stored to the state too, for the next launch.
+__device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem, int it, int nl, double& bjv,
+                                             int& bitv) {
 #pragma clang fp contract(off)
   const int tid = threadIdx.x, H = a.H, E = a.elite;
   const int len = nlp_list_len(E);
@@ -337,10 +341,9 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   __syncthreads();
   NLP_STAMP(6);
   const double c0 = nlp_unkey(kA[0]);
-  const double bj0 = ld_wt(&st->best_j);
-  const int bit0 = ld_wt(&st->best_it);
+  const double bj0 = bjv;
+  const int bit0 = bitv;
   const bool better = c0 < bj0;                     // the best sequence so far (NaN never)
-  __syncthreads();                                  // every thread has read best_j
   if (tid < 2 * H) {
     // mean / std over the elite in np.mean(axis=0) / np.std(axis=0)'s order: an axis-0
     // reduction adds the rows in sequence (checked against NumPy), std = sqrt(mean((x - m)^2))
@@ -389,6 +392,8 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   // the result (the last round): best objective and round, before this round's update
   const double bj = better ? c0 : bj0;
   const int bit = better ? it : bit0;
+  bjv = bj;
+  bitv = bit;
   if (tid == 0 && better) {
     st_wt(&st->best_j, c0);
     st_wt(&st->best_it, it);
@@ -430,12 +435,16 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a) {
   const int nl = (int)gridDim.x - 1;    // sample blocks; block nl completes every round
   if (blk == nl) {
     const NlpCompLds L = nlp_comp_lds(smem, nl, nlp_list_len(a.elite));
+    // the best so far as the launch starts (host-staged, or an earlier launch's rounds): loaded
+    // while the first round's lists are awaited
+    double bjv = ld_wt(&a.st->best_j);
+    int bitv = ld_wt(&a.st->best_it);
     for (int r = 0; r < a.rounds; ++r) {
       const int it = a.it + r;
       NLP_STAMP(7);
       if (!nlp_poll_lists(a, L, nl, nlp_seq(a.host_seq, it), rflag)) return;
       NLP_STAMP(4);
-      nlp_complete(a, smem, it, nl);
+      nlp_complete(a, smem, it, nl, bjv, bitv);
     }
     return;
   }
