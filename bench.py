@@ -13,7 +13,7 @@ kernel that pushes the record into every peer's IPC-mapped mailbox over xGMI and
 Workload (BASELINE.json configs[1]): ETHZ track, N_models = 10^4 per GPU, H = 20, C = 1
 candidate, W = 10, K = 10, Ts = 0.02, gradual friction change.  Tick inputs are
 synthetic-but-physical: states from the device RK6 plant (Dynamic.sim_continuous)
-driven by the recorded ETHZ controls (tests/golden/dyn_slice.npz) under the gradual
+driven by the recorded ETHZ controls (llampc/tracks/data/dyn_slice.npz) under the gradual
 friction decay D <- D(1 - 1/2600) per tick (rt.py:125-130), xref from ConstantSpeed on the
 packaged ETHZ raceline library.  All tick inputs are resident in HBM before timing.
 
@@ -58,7 +58,7 @@ LOOKBACK_INSTR_PER_MODEL = ISSUE_INSTR_PER_STEP[1]   # one LPM-1 RK4 step + erro
 
 EXCHANGE_DESC = {
     "peer": "peer mailboxes over xGMI (HIP IPC): the plan launch pushes its record, polls and merges (llampc_plan_exchange)",
-    "rccl": "native RCCL all-gather on the tick stream (llampc_exchange_device) + merge_kernel",
+    "rccl": "ncclAllGather on the tick stream over the library's own RCCL communicator (llampc_exchange_rccl) + merge_kernel",
     "c10d": "c10d all_gather_into_tensor (nccl) + merge_kernel",
     "host": "gloo all-gather on the host + merge_kernel",
 }
@@ -379,7 +379,11 @@ def main():
         nat.check(lib.llampc_bank_timing(sb.bank.handle, stride, args.steps // abs(stride) + 8))
     if world > 1:                       # every rank's exchange waits for the others' records
         dist.barrier()
-    for i in range(args.warmup):
+    # every timed tick runs the stated workload, the full-window look-back (window mean, top-K,
+    # lb_final; rt.py:354-360): at least W ticks run before the timed loop, whatever --warmup
+    # says (a tick with a partial window skips the selection)
+    fill = max(args.warmup, W)
+    for i in range(fill):
         step(i)
     if not args.no_timing:              # restart the count: the warmup launches are not timed
         nat.check(lib.llampc_bank_timing_read(sb.bank.handle, avg, cnt))
@@ -388,8 +392,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    count_before = sb.bank.window_count         # host state: the window before the first timed tick
     for i in range(args.steps):
-        step(args.warmup + i, ex_events[i // TIMING_SAMPLE] if ex_events and i % TIMING_SAMPLE == 0 else None)
+        step(fill + i, ex_events[i // TIMING_SAMPLE] if ex_events and i % TIMING_SAMPLE == 0 else None)
     t_issue = time.perf_counter() - t0       # host time to enqueue the K ticks
     torch.cuda.synchronize()
     if world > 1:                            # (at world 1 there is no barrier to re-synchronise after)
@@ -474,6 +479,8 @@ def main():
             "host_issue_us_per_step": t_issue / args.steps * 1e6,
             "lpm": lpm_of(N_local, C),
             "result_check": {"sel_model": merged.best_model, "window_full": merged.window_full,
+                             "window_full_every_timed_tick": bool(count_before >= W),
+                             "untimed_ticks_before": fill,
                              "sel_cand": merged.best_cand, "n_nonfinite": merged.n_nonfinite},
             "cpu_baseline": None,
         }
@@ -593,16 +600,25 @@ def extras(args, sb, stream, world, rank=0):
             except Exception as e:          # noqa: BLE001
                 out[key] = {"error": f"{type(e).__name__}: {e}"}
     else:
-        out["config5"] = concurrent_tracks_sharded(args, world, rank, sb.device)
-        out["controller_tick_us"] = controller_ticks_sharded(args, world, rank, sb.device)
+        # every rank runs each extra (they exchange every tick); a failure on any rank is
+        # reported in the line, decided over the ranks, and never costs the headline
+        for key, fn in (("config5", concurrent_tracks_sharded), ("controller_tick_us", controller_ticks_sharded)):
+            val, err = None, None
+            try:
+                val = fn(args, world, rank, sb.device)
+            except Exception as e:          # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+                print(f"bench.py: rank {rank}: extra {key} failed: {err}", file=sys.stderr, flush=True)
+            failed = max_over_ranks(1.0 if err is not None else 0.0) > 0
+            out[key] = val if not failed else {"error": err or "failed on another rank"}
     return out
 
 
 def controller_ticks_sharded(args, world, rank, dev_index, ticks=1000, warm=60, period=1e-3, H=40, C=64):
     """BASELINE config 5's real loop across the ranks: LLAMPC.tick (device mode) on an ETHZ and an
-    ETHZMobil bank of N_per_gpu x world models each, every bank sharded over the ranks
-    (llampc_ctl_set_exchange: each tick's launch pushes its shard's top-K + argmin to every peer,
-    merges, and rolls out the merged selection's K + 1 models), both tracks ticked concurrently
+    ETHZMobil bank of N_per_gpu x world models each, every bank sharded over the ranks (each
+    tick exchanges the shards' top-K + argmin over the ShardedBank's transport, every rank merges
+    and rolls out the merged selection's K + 1 models), both tracks ticked concurrently
     (tick_begin on both, then tick_end), paced at 1 kHz; p50/p99/max of the step, max over ranks.
     The plant (the host oracle's RK6 would cost ms; the device RK6) advances each car between
     steps, outside the timed region — every rank applies the same control."""
@@ -611,7 +627,7 @@ def controller_ticks_sharded(args, world, rank, dev_index, ticks=1000, warm=60, 
     from llampc.mpc import LLAMPC, generate_bank
     from llampc.mpc.sharded import ShardedBank
     from llampc.params import ORCA
-    from llampc.tracks import ETHZ, ETHZMobil
+    from llampc.tracks import ETHZ, ETHZMobil, dyn_slice
     p = ORCA()
     setups = []
     try:
@@ -621,7 +637,7 @@ def controller_ticks_sharded(args, world, rank, dev_index, ticks=1000, warm=60, 
             ctl = LLAMPC(sb, tr, H=H, C=C, K=args.K, mode="device")
             plant = Dynamic(**p, device=dev_index)
             if tr.name == "ETHZ":
-                x = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))["states"][:, 0].copy()
+                x = dyn_slice()["states"][:, 0].copy()
             else:
                 x = np.array([tr.x_init, tr.y_init, tr.psi_init, 1.0, 0.0, 0.0])
             setups.append([sb, ctl, plant, x])
@@ -642,7 +658,7 @@ def controller_ticks_sharded(args, world, rank, dev_index, ticks=1000, warm=60, 
                 xn, _ = pl.sim_continuous(s[3], r.u_seq[:, 0].reshape(2, 1), [0, 0.02])
                 s[3] = xn[:, -1]
         sel = [int(r.best_model) for r in res]
-        transports = [s[0].transport for s in setups]
+        transports = [s[1]._ctl.transport for s in setups]
     finally:
         for s in setups:
             s[1].close()
@@ -657,9 +673,11 @@ def controller_ticks_sharded(args, world, rank, dev_index, ticks=1000, warm=60, 
             "met": p99 < 1000.0, "tracks": ["ETHZ", "ETHZMobil"], "N_per_track": N * world, "N_per_track_per_gpu": N,
             "H": H, "C": C, "K": K, "W": args.W, "sel_models": sel, "transport": transports,
             "rollout_steps_per_tick": steps_tick, "rollout_steps_per_s_at_p50": 2 * steps_tick / (p50 * 1e-6),
-            "note": "LLAMPC.tick (device mode) on banks sharded over the ranks (llampc_ctl_set_exchange: the "
-                    "selection exchanged inside each tick's launch over the peer mailboxes), two tracks "
-                    "concurrently, paced at 1 ms; max over ranks"}
+            "note": "LLAMPC.tick (device mode) on banks sharded over the ranks: the selection exchanged every "
+                    "tick over `transport` (peer: inside the tick's one launch, llampc_ctl_set_exchange; rccl: "
+                    "ncclAllGather between the tick's two launches; host/c10d: the records carried by the "
+                    "process group between them, llampc_ctl_set_gather), two tracks concurrently, paced at "
+                    "1 ms; max over ranks"}
 
 
 def concurrent_tracks_sharded(args, world, rank, dev_index, ticks=1000, warm=50):
@@ -832,7 +850,7 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
     from llampc.models import Dynamic
     from llampc.mpc import LLAMPC, ModelBank, generate_bank
     from llampc.params import ORCA
-    from llampc.tracks import ETHZ, ETHZMobil
+    from llampc.tracks import ETHZ, ETHZMobil, dyn_slice
     dev = torch_device_index()
     p = ORCA()
     setups = []
@@ -842,7 +860,7 @@ def controller_ticks(args, ticks=1000, warm=60, period=1e-3, H=40, C=64):
         ctl = LLAMPC(b, tr, H=H, C=C, K=args.K, mode="device")
         plant = Dynamic(**p, device=dev)
         if tr.name == "ETHZ":
-            x = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))["states"][:, 0].copy()
+            x = dyn_slice()["states"][:, 0].copy()
         else:
             x = np.array([tr.x_init, tr.y_init, tr.psi_init, 1.0, 0.0, 0.0])
         setups.append([b, ctl, plant, x])
@@ -943,7 +961,8 @@ def solve_latency(args, n=200, warm=10, H=20):
     from llampc.mpc.planner import ConstantSpeed
     from llampc.params import ORCA
     from llampc.tracks import ETHZ
-    d = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))
+    from llampc.tracks import dyn_slice
+    d = dyn_slice()
     s, u = d["states"], d["inputs"]
     tr = ETHZ('optimal', True)
     p = ORCA(control="pwm")

@@ -20,7 +20,7 @@
  *  llampc_plan / llampc_plan_device one LLA-MPC tick: rt.py:300-366 (look-back on the
  *                                  newest transition, selection, look-ahead from x_t)
  *  llampc_merge / _device          (new) cross-shard merge of per-GPU plan results
- *  llampc_exchange_device / _peer  (new) the per-tick gather + merge of the sharded bank
+ *  llampc_exchange_rccl / _peer    (new) the per-tick gather + merge of the sharded bank
  *                                  (SURVEY.md §8e): RCCL all-gather, or xGMI mailboxes
  *  llampc_nlp_*                    setupNLP / .solve (nmpc.py:14-203), solved by sampling
  *  llampc_dynamics_batch           Dynamic.calc_forces_batch (llampc/models/dynamic.py:
@@ -171,7 +171,9 @@ int llampc_bank_window(llampc_bank* bank, double* ring, int32_t* window_count);
 /* stream the bank launches on (hipStream_t as void*); NULL = its own stream */
 int llampc_bank_set_stream(llampc_bank* bank, void* stream);
 /* the stream the bank launches on now (its own or the one set above), for callers that
- * enqueue their own work with it */
+ * enqueue their own work with it.  The bank's OWN stream may be replaced by a dedicated-queue
+ * one (llampc_bank_set_concurrency(banks > 1), llampc_ctl_set_prelaunch(on)): a handle read
+ * earlier is then destroyed — read it again after either call. */
 int llampc_bank_stream(const llampc_bank* bank, void** stream);
 /* the number of banks the caller ticks concurrently on this device (default 1; BASELINE
  * config 5 ticks two tracks together: 2).  The look-ahead sizes its launch for 1/banks of the
@@ -251,28 +253,35 @@ int llampc_merge(const llampc_plan_out* parts, int32_t G, int32_t nan_policy,
                  llampc_plan_out* merged);
 int llampc_merge_device(const void* d_parts, int32_t G, int32_t nan_policy, void* d_merged,
                         int32_t device, void* stream);
+/* ---- RCCL, the library's own communicator (public rccl.h API) ---------------------- */
+/* The library resolves RCCL at first use: the librccl.so.1 the process has already loaded
+ * (torch's, so one RCCL per process), else the system's.  Setup per rank: rank 0 calls
+ * llampc_comm_unique_id (ncclGetUniqueId) and shares the 128-byte id out of band (e.g. a
+ * torch.distributed store or all_gather_object); every rank calls llampc_comm_create
+ * (ncclCommInitRank on `device`; collective: blocks until all `world` ranks joined).
+ * LLAMPC_E_STATE when no RCCL can be loaded. */
+typedef struct llampc_comm llampc_comm;
+int llampc_comm_unique_id(void* id /* 128 bytes out */);
+int llampc_comm_create(const void* id /* 128 bytes */, int32_t world, int32_t rank, int32_t device, llampc_comm** out);
+int llampc_comm_destroy(llampc_comm* comm);
 /* The per-tick exchange of the sharded bank, enqueued on `stream` (hipStream_t) with no
- * host round trip: an RCCL all-gather of this rank's record d_local (one llampc_plan_out)
- * into d_all [world] over `comm`, then merge_kernel into d_merged.  comm is an ncclComm_t
- * (e.g. a torch ProcessGroupNCCL communicator: backend._comm_ptr()); allgather_fn is the
- * address of ncclAllGather in the RCCL library the process already loaded, so this library
- * neither links nor initialises a second RCCL.  Replaces the reference-side gather that
- * SURVEY.md §8e specifies (the reference itself is single-process). */
-int llampc_exchange_device(const void* d_local, void* d_all, int32_t world, void* d_merged,
-                           int32_t nan_policy, void* comm, void* allgather_fn, int32_t device,
-                           void* stream);
+ * host round trip: ncclAllGather of this rank's record d_local (one llampc_plan_out) into
+ * d_all [world] over `comm`, then merge_kernel into d_merged.  Replaces the reference-side
+ * gather that SURVEY.md §8e specifies (the reference itself is single-process). */
+int llampc_exchange_rccl(llampc_comm* comm, const void* d_local, void* d_all, void* d_merged, int32_t nan_policy,
+                         void* stream);
 
 /* Peer exchange: the same per-tick gather + merge with no collective library.  Each rank
  * owns a mailbox (uncached device memory, [2][world] record slots of tagged words) that every
  * peer process maps through HIP IPC; per tick ONE kernel pushes this rank's record into slot
  * [rank] of every mailbox over xGMI (system-scope stores), polls its own mailbox until all
  * `world` records of this tick have arrived and runs merge_kernel's merge — the output equals
- * llampc_exchange_device's.  Setup: create, export the IPC handle (64 bytes), share the
+ * llampc_exchange_rccl's.  Setup: create, export the IPC handle (64 bytes), share the
  * handles out of band (e.g. a torch.distributed all_gather_object), open every peer's.  All
  * ranks must call llampc_exchange_peer the same number of times (the tick number is the tag).
  * A rank that waits more than the poll bound (default 10 s; set_bound) gets status
  * LLAMPC_STATUS_POLL_TIMEOUT in d_merged.  Replaces the same reference-side gather as
- * llampc_exchange_device. */
+ * llampc_exchange_rccl. */
 typedef struct llampc_mailbox llampc_mailbox;
 int llampc_mailbox_create(int32_t world, int32_t rank, int32_t device, llampc_mailbox** out);
 int llampc_mailbox_ipc_handle(llampc_mailbox* mb, void* handle /* 64 bytes out */);
@@ -361,7 +370,14 @@ int llampc_ctl_wait(llampc_ctl* ctl, llampc_ctl_out* out);
  * While armed, the bank's stream holds that launch: every other call on the bank or the
  * controller cancels it first (it exits untouched; the next tick launches normally and re-arms),
  * as does a tick more than 0.5 s after the arming; an armed launch never rung exits after 2 s.
- * Not with llampc_ctl_set_exchange.  on = 0 cancels. */
+ * The armed launch must not hold a hardware queue other work shares (a solve or another bank's
+ * tick enqueued behind it on that queue would wait for the doorbell): on = 1 gives the bank's
+ * own stream a hardware queue of its own (as llampc_bank_set_concurrency(> 1) does) and is
+ * refused (LLAMPC_E_STATE) on a bank launching on a caller's stream (llampc_bank_set_stream).
+ * With llampc_ctl_set_exchange (peer mailboxes) the armed launch runs the exchange after its
+ * doorbell; its mailbox tick number is committed when it fires, so every rank may arm, cancel
+ * or launch independently (call set_exchange first).  Not with llampc_ctl_set_gather (two
+ * launches per tick; LLAMPC_E_STATE).  on = 0 cancels. */
 int llampc_ctl_set_prelaunch(llampc_ctl* ctl, int32_t on);
 /* The last completed tick's device time in microseconds: from x_t reaching the device (an armed
  * launch's block 0 seeing the doorbell; else block 0 starting) to the record's stores issued, by
@@ -387,6 +403,24 @@ int llampc_ctl_inputs(llampc_ctl* ctl, double* xref, double* U);
  * ranks must tick the same number of times (the mailbox's tick number is the tag); the tick's
  * own launch does the exchange (no second kernel).  world <= 16, n_global < 2^32 - 1. */
 int llampc_ctl_set_exchange(llampc_ctl* ctl, llampc_mailbox* mb, const double* gparams, int64_t n_global);
+/* The same sharded controller over a GATHER transport (no peer mailbox; world <= 16): every
+ * full-window tick is two launches on the bank's stream.  The first runs the look-back and
+ * leaves this shard's record — llampc_ctl_record_words(K) words: its top-K and argmin as
+ * (window mean, global index) entries, tagged with the exchange's tick number — in device
+ * memory; the G records are all-gathered; the second launch merges them (the peer exchange's
+ * merge, so the results are the same bitwise) and runs the look-ahead and the completion.
+ * comm != NULL: the library issues ncclAllGather between the launches (stream-ordered, no host
+ * round trip).  comm == NULL: the caller carries the records — after llampc_ctl_tick_async,
+ * llampc_ctl_shard_record(ctl, words, &nw) waits for the first launch and returns this rank's
+ * record (nw = 0: this tick has no exchange, e.g. the window is not full; llampc_ctl_wait
+ * follows directly), the caller all-gathers the records of ranks 0..world-1 in rank order
+ * (any transport) and passes them to llampc_ctl_resume, then llampc_ctl_wait as usual.  A
+ * record whose tag does not match (ranks out of step) fails the tick (record status). */
+int llampc_ctl_set_gather(llampc_ctl* ctl, int32_t world, int32_t rank, llampc_comm* comm, const double* gparams,
+                          int64_t n_global);
+int32_t llampc_ctl_record_words(int32_t K);
+int llampc_ctl_shard_record(llampc_ctl* ctl, uint64_t* words /* [llampc_ctl_record_words(K)] */, int32_t* nw);
+int llampc_ctl_resume(llampc_ctl* ctl, const uint64_t* all_words /* [world][nw] */);
 /* The sharded controller's merge on the host (the device exchange runs the same functions,
  * csrc/ctl.hpp): G records of K + 1 entries each — vals / gids [G][K+1], entries 0..K-1 the
  * shard's sorted top-K (gid -1: none), entry K its argmin — -> the merged top-K (argsort order

@@ -7,7 +7,9 @@
 // reduction partials, the per-model look-ahead result, and pinned host staging so one
 // host-pointer tick = 1 H2D copy + 1 kernel on one stream, the record coming back through
 // pinned host memory with a completion tag (llampc_plan / llampc_plan_wait).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -762,23 +764,29 @@ int llampc_bank_stream(const llampc_bank* b, void** stream) {
   return LLAMPC_OK;
 }
 
+// The bank's own stream on a hardware queue of its own (bank_stream), replacing a plain one
+// (the caller holds b->mu; nothing may be armed on it).
+static int bank_dedicate(llampc_bank* b) {
+  if (b->dedicated) return LLAMPC_OK;
+  b->dedicated = true;
+  if (b->own_stream) {
+    DeviceGuard g(b->device);
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    hipStream_t s = nullptr;
+    HIP_TRY(bank_stream(b->device, true, &s));
+    (void)hipStreamDestroy(b->stream);
+    b->stream = s;
+  }
+  return LLAMPC_OK;
+}
+
 int llampc_bank_set_concurrency(llampc_bank* b, int32_t banks) {
   if (!b) return fail(LLAMPC_E_ARG, "bank is NULL");
   if (banks < 1 || banks > 64) return fail(LLAMPC_E_ARG, "banks=%d outside [1, 64]", banks);
   std::lock_guard<std::mutex> lk(b->mu);
   bank_disarm(b);
   b->share = banks;
-  if (banks > 1 && !b->dedicated) {      // concurrent banks: a hardware queue of its own (bank_stream)
-    b->dedicated = true;
-    if (b->own_stream) {
-      DeviceGuard g(b->device);
-      HIP_TRY(hipStreamSynchronize(b->stream));
-      hipStream_t s = nullptr;
-      HIP_TRY(bank_stream(b->device, true, &s));
-      (void)hipStreamDestroy(b->stream);
-      b->stream = s;
-    }
-  }
+  if (banks > 1) return bank_dedicate(b);   // concurrent banks: a hardware queue of its own
   return LLAMPC_OK;
 }
 
@@ -1054,21 +1062,108 @@ int llampc_merge_device(const void* d_parts, int32_t G, int32_t nan_policy, void
   return LLAMPC_OK;
 }
 
-// ncclAllGather(sendbuff, recvbuff, sendcount, datatype, comm, stream) (rccl.h); datatype
-// ncclUint8 = 1, ncclSuccess = 0.  Called through the process's own RCCL (see llampc.h).
-typedef int (*AllGatherFn)(const void*, void*, size_t, int, void*, hipStream_t);
+}  // extern "C"
 
-int llampc_exchange_device(const void* d_local, void* d_all, int32_t world, void* d_merged,
-                           int32_t nan_policy, void* comm, void* allgather_fn, int32_t device,
-                           void* stream) {
-  if (!d_local || !d_all || !d_merged || !comm || !allgather_fn || world < 1 || world > 32)
-    return fail(LLAMPC_E_ARG, "bad exchange arguments (world=%d, 1..32)", world);
+// ---- RCCL: the library's own communicator (rccl.h) ----------------------------------
+// RCCL is resolved at first use, not linked: the librccl.so.1 the process already holds
+// (torch's bundled RCCL carries that soname: one RCCL per process, whatever the import order
+// of torch and this library), else the system's.  A process that never exchanges over RCCL
+// never loads it.
+namespace {
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGetErrorString) err_str = nullptr;
+  bool ok = false;
+  std::string why;
+};
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      x.why = e ? e : "librccl.so.1 not found";
+      return x;
+    }
+    x.get_id = reinterpret_cast<decltype(x.get_id)>(dlsym(h, "ncclGetUniqueId"));
+    x.init_rank = reinterpret_cast<decltype(x.init_rank)>(dlsym(h, "ncclCommInitRank"));
+    x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.all_gather = reinterpret_cast<decltype(x.all_gather)>(dlsym(h, "ncclAllGather"));
+    x.err_str = reinterpret_cast<decltype(x.err_str)>(dlsym(h, "ncclGetErrorString"));
+    x.ok = x.get_id && x.init_rank && x.destroy && x.all_gather && x.err_str;
+    if (!x.ok) x.why = "librccl.so.1 lacks an ncclGetUniqueId/ncclCommInitRank/ncclAllGather symbol";
+    return x;
+  }();
+  return r;
+}
+static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes (llampc_comm_unique_id)");
+}  // namespace
+
+struct llampc_comm {
+  ncclComm_t comm = nullptr;
+  int32_t world = 0, rank = 0, device = 0;
+};
+
+#define RCCL_TRY(expr)                                                                         \
+  do {                                                                                         \
+    const ncclResult_t r_ = (expr);                                                            \
+    if (r_ != ncclSuccess) return fail(LLAMPC_E_HIP, "%s failed: %s", #expr, rccl().err_str(r_)); \
+  } while (0)
+
+extern "C" {
+
+int llampc_comm_unique_id(void* id) {
+  if (!id) return fail(LLAMPC_E_ARG, "id is NULL");
+  if (!rccl().ok) return fail(LLAMPC_E_STATE, "RCCL unavailable: %s", rccl().why.c_str());
+  ncclUniqueId u;
+  RCCL_TRY(rccl().get_id(&u));
+  std::memcpy(id, &u, sizeof u);
+  return LLAMPC_OK;
+}
+
+int llampc_comm_create(const void* id, int32_t world, int32_t rank, int32_t device, llampc_comm** out) {
+  if (!out) return fail(LLAMPC_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (!id || world < 1 || rank < 0 || rank >= world) return fail(LLAMPC_E_ARG, "bad comm arguments (world=%d rank=%d)", world, rank);
+  if (!rccl().ok) return fail(LLAMPC_E_STATE, "RCCL unavailable: %s", rccl().why.c_str());
   DeviceGuard g(device);
   if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", device);
-  const int r = reinterpret_cast<AllGatherFn>(allgather_fn)(d_local, d_all, sizeof(llampc_plan_out), 1,
-                                                            comm, (hipStream_t)stream);
-  if (r != 0) return fail(LLAMPC_E_HIP, "ncclAllGather failed: ncclResult %d", r);
-  HIP_TRY(launch_merge((const llampc_plan_out*)d_all, world, nan_policy == LLAMPC_NAN_FIRST,
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  ncclComm_t comm = nullptr;
+  RCCL_TRY(rccl().init_rank(&comm, world, u, rank));
+  auto* c = new llampc_comm();
+  c->comm = comm;
+  c->world = world;
+  c->rank = rank;
+  c->device = device;
+  *out = c;
+  return LLAMPC_OK;
+}
+
+int llampc_comm_destroy(llampc_comm* c) {
+  if (!c) return LLAMPC_OK;
+  if (c->comm && rccl().ok) {
+    DeviceGuard g(c->device);
+    (void)rccl().destroy(c->comm);
+  }
+  delete c;
+  return LLAMPC_OK;
+}
+
+int llampc_exchange_rccl(llampc_comm* comm, const void* d_local, void* d_all, void* d_merged, int32_t nan_policy,
+                         void* stream) {
+  if (!comm || !d_local || !d_all || !d_merged || comm->world > 32)
+    return fail(LLAMPC_E_ARG, "bad exchange arguments (world 1..32)");
+  DeviceGuard g(comm->device);
+  if (!g.ok) return fail(LLAMPC_E_HIP, "hipSetDevice(%d) failed", comm->device);
+  RCCL_TRY(rccl().all_gather(d_local, d_all, sizeof(llampc_plan_out), ncclUint8, comm->comm, (hipStream_t)stream));
+  HIP_TRY(launch_merge((const llampc_plan_out*)d_all, comm->world, nan_policy == LLAMPC_NAN_FIRST,
                        (llampc_plan_out*)d_merged, (hipStream_t)stream));
   return LLAMPC_OK;
 }
@@ -1253,6 +1348,17 @@ struct llampc_ctl {
   llampc_mailbox* mb = nullptr;
   double* d_gparams = nullptr;           // [6][n_global]
   int64_t n_global = 0;
+  // sharded over a gather transport (llampc_ctl_set_gather; CtlLaunch.px_phase): RCCL, or the
+  // caller carries the records (xg_comm null) between the two launches of a full-window tick
+  int32_t xg_world = 0, xg_rank = 0;
+  llampc_comm* xg_comm = nullptr;
+  uint64_t* d_xsend = nullptr;           // [nw] this shard's record (the first launch writes it)
+  uint64_t* d_xgath = nullptr;           // [G][nw] the gathered records
+  uint64_t* h_xstage = nullptr;          // pinned [G][nw] (the host transport's staging)
+  uint32_t xg_seq = 0;
+  bool xg_wait = false;                  // the host transport's second launch awaits llampc_ctl_resume
+  bool xg_read = false;                  //   and this rank's record has been read
+  int32_t xg_nw = 0;
   // armed launches (llampc_ctl_set_prelaunch): the next tick's launch is enqueued behind this
   // one and waits for x_t on the doorbell (CtlLaunch.door)
   bool prelaunch = false;
@@ -1285,7 +1391,7 @@ struct llampc_ctl {
     int64_t t = 0;
     bool do_lb = false;
     int32_t count = 0;
-  } arm;
+  } arm, xg_second;                      // xg_second: the host transport's pending second launch
   std::mutex mu;
 };
 
@@ -1300,8 +1406,11 @@ static void ctl_cancel(llampc_ctl* c) {
   __atomic_store_n(&c->h_door[kCtlDoorWords - 1], ((uint64_t)c->arm.L.door_seq << 32) | kCtlDoorCancel,
                    __ATOMIC_RELEASE);
   // its completion number is spent: a launch that expired before the cancel has stored it
-  // (with kCtlTagExpired) into the tag the next tick's wait reads
+  // (with kCtlTagExpired) into the tag the next tick's wait reads.  So is its selection tag: the
+  // cancelled launch may have published spec_tag words tagged arm.seq before its doorbell, which
+  // a relaunch with the same tag would read as its own
   c->hseq = c->arm.hs;
+  c->seq = c->arm.seq;
   c->armed = false;
   if (c->b && c->b->armed == c) c->b->armed = nullptr;
 }
@@ -1313,7 +1422,10 @@ static void bank_disarm(llampc_bank* b) {
 // Controllers whose tick was rung and whose next launch is still to be armed (arm_next).  The
 // first llampc_ctl_wait of a step arms them ALL before it spins: with two tracks (tick_async on
 // both, then wait on both) the second controller's launch call would otherwise sit between the
-// first's result and its own (~5 us on the two-track step).
+// first's result and its own (~5 us on the two-track step).  The arming pass holds g_arm_mu
+// throughout and only try-locks the controllers it visits; llampc_ctl_destroy removes its
+// controller under g_arm_mu before anything is freed, so the pass never holds a controller that
+// is being destroyed.
 static std::mutex g_arm_mu;
 static std::vector<llampc_ctl*> g_arm_list;
 static void arm_list_add(llampc_ctl* c) {
@@ -1351,9 +1463,12 @@ int llampc_ctl_destroy(llampc_ctl* c) {
                  c->d_xref_tag};
     for (void* p : d)
       if (p) (void)hipFree(p);
+    if (c->d_xsend) (void)hipFree(c->d_xsend);
+    if (c->d_xgath) (void)hipFree(c->d_xgath);
     if (c->h_out) (void)hipHostFree(c->h_out);
     if (c->h_tag) (void)hipHostFree(c->h_tag);
     if (c->h_door) (void)hipHostFree(c->h_door);
+    if (c->h_xstage) (void)hipHostFree(c->h_xstage);
   }
   delete c;
   return LLAMPC_OK;
@@ -1587,16 +1702,18 @@ static int ctl_prepare(llampc_ctl* c, const double* x_t, llampc_ctl::Prep& P) {
   // rank); the selection is global, the look-ahead reads the replicated global table
   L.sel_goff = b->goff;
   uint32_t px_seq = 0;
-  if (c->mb) {                           // (the caller holds mb->mu)
+  if (c->mb || c->xg_world) {            // (the caller holds mb->mu)
+    L.la.params = c->d_gparams;
+    L.la.n = c->n_global;
+    L.la.goff = 0;
+    L.sel_goff = 0;
+  }
+  if (c->mb) {
     llampc_mailbox* mb = c->mb;
     if (!mb->box_synced) {
       HIP_TRY(hipMemcpy(mb->d_box, mb->box, kPeerMax * sizeof(uint64_t*), hipMemcpyHostToDevice));
       mb->box_synced = true;
     }
-    L.la.params = c->d_gparams;
-    L.la.n = c->n_global;
-    L.la.goff = 0;
-    L.sel_goff = 0;
     if (full) {
       px_seq = next_seq(mb->seq);
       L.px_box = mb->d_box;
@@ -1606,6 +1723,15 @@ static int ctl_prepare(llampc_ctl* c, const double* x_t, llampc_ctl::Prep& P) {
       L.px_bound = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((mb->bound + 0xFFFF) >> 16, 1), UINT32_MAX);
       L.poll = std::max(L.poll, L.px_bound);   // the look-ahead blocks wait for the merged selection
     }
+  } else if (c->xg_world && full) {      // gather transport: two launches (CtlLaunch.px_phase)
+    px_seq = next_seq(c->xg_seq);
+    L.px_G = c->xg_world;
+    L.px_rank = c->xg_rank;
+    L.px_seq = px_seq;
+    L.px_phase = 1;
+    L.px_send = c->d_xsend;
+    L.px_gath = c->d_xgath;
+    L.px_bound = 16;                     // ~10 ms: the records are there when the launch starts
   }
   // the look-ahead blocks stage every (candidate, step)'s input terms when they fit in LDS
   // (CtlLaunch.s4; LLAMPC_CTL_NO_STAGE=1 at create: never, for A/B runs)
@@ -1655,7 +1781,10 @@ static void ctl_commit(llampc_ctl* c, const llampc_ctl::Prep& P) {
   llampc_bank* b = c->b;
   c->hseq = P.hs;
   c->seq = P.seq;
-  if (P.L.px_G) c->mb->seq = P.px_seq;   // committed after the launch was enqueued (next_seq)
+  if (P.L.px_G) {                        // committed after the launch was enqueued (next_seq)
+    if (c->mb) c->mb->seq = P.px_seq;
+    else c->xg_seq = P.px_seq;
+  }
   c->t = P.t + 1;
   c->pending = true;
   c->pend_seq = P.hs;
@@ -1667,9 +1796,16 @@ static void ctl_commit(llampc_ctl* c, const llampc_ctl::Prep& P) {
 }
 
 // Enqueues tick c->t's launch armed (llampc_ctl_set_prelaunch): it runs behind the tick in
-// flight and waits for the doorbell.  Not with a sharded exchange.
+// flight and waits for the doorbell.  The caller holds c->mu, c->b->mu and, with a peer
+// exchange, c->mb->mu.  With the peer exchange the armed launch takes the mailbox's next tick
+// number (the exchange runs after its doorbell, inside it); the number is committed only when
+// the doorbell fires (ctl_commit), so a cancelled armed launch — which exits before the doorbell,
+// never pushing — leaves the sequence to its relaunch, and the ranks' sequences stay in step
+// whichever of them armed, fired or relaunched.  Not with a gather transport (two launches).
 static int ctl_arm(llampc_ctl* c) {
-  if (c->armed || c->mb) return LLAMPC_OK;
+  if (c->armed || c->xg_world) return LLAMPC_OK;
+  if (!c->b->own_stream || !c->b->dedicated)   // the stream changed since set_prelaunch
+    return fail(LLAMPC_E_STATE, "an armed launch needs the bank's own dedicated-queue stream");
   llampc_ctl::Prep P;
   int rc = ctl_prepare(c, nullptr, P);
   if (rc) return rc;
@@ -1691,9 +1827,13 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
   std::lock_guard<std::mutex> lk(b->mu);
   if (b->async_pending) return fail(LLAMPC_E_STATE, "an async plan tick is outstanding on the bank");
   DeviceGuard g(b->device);
+  std::unique_lock<std::mutex> lm;
+  if (c->mb) lm = std::unique_lock<std::mutex>(c->mb->mu);
   if (c->armed) {
     const double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - c->arm_t).count();
-    if (age < kArmFreshS && c->arm.t == c->t) {
+    // (with a peer exchange the armed launch's tick number must still be the mailbox's next)
+    const bool px_ok = !c->arm.L.px_G || !c->mb || c->arm.px_seq == next_seq(c->mb->seq);
+    if (age < kArmFreshS && c->arm.t == c->t && px_ok) {
       // fire: every word tagged (block 0 polls until all carry the tag: no order needed)
       const uint64_t tg = (uint64_t)c->arm.L.door_seq << 32;
       for (int j = 0; j < 6; ++j) {
@@ -1712,11 +1852,35 @@ int llampc_ctl_tick_async(llampc_ctl* c, const double* x_t) {
     }
     ctl_cancel(c);                       // stale: this tick launches normally
   }
-  std::unique_lock<std::mutex> lm;
-  if (c->mb) lm = std::unique_lock<std::mutex>(c->mb->mu);
   llampc_ctl::Prep P;
   int rc = ctl_prepare(c, x_t, P);
   if (rc) return rc;
+  if (P.L.px_phase == 1) {               // gather transport: the look-back launch, the gather, the rest
+    llampc_ctl::Prep P2 = P;
+    P2.L.px_phase = 2;
+    P2.L.nb_lb = 1;                      // block 0 merges and completes
+    llampc_ctl::Prep P1 = P;
+    P1.L.nb_la = 0;                      // the look-back blocks alone
+    P1.L.n_spec = 0;
+    {
+      TimedLaunch tl(b, 0, b->stream);
+      HIP_TRY(launch_ctl(P1.L, P1.lpm, P1.lds, b->stream));
+      if (c->xg_comm) {
+        RCCL_TRY(rccl().all_gather(c->d_xsend, c->d_xgath, (size_t)c->xg_nw, ncclUint64, c->xg_comm->comm, b->stream));
+        HIP_TRY(launch_ctl(P2.L, P2.lpm, P2.lds, b->stream));
+      }
+    }
+    ctl_commit(c, P);
+    if (!c->xg_comm) {                   // the caller carries the records (llampc_ctl_resume)
+      c->xg_second = P2;
+      c->xg_wait = true;
+      c->xg_read = false;
+      return LLAMPC_OK;
+    }
+    c->arm_next = c->prelaunch;
+    if (c->arm_next) arm_list_add(c);
+    return LLAMPC_OK;
+  }
   {
     TimedLaunch tl(b, 0, b->stream);
     HIP_TRY(launch_ctl(P.L, P.lpm, P.lds, b->stream));
@@ -1731,6 +1895,7 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
   if (!c || !out) return fail(LLAMPC_E_ARG, "controller/out is NULL");
   std::lock_guard<std::mutex> lc(c->mu);
   if (!c->pending) return fail(LLAMPC_E_STATE, "no controller tick outstanding");
+  if (c->xg_wait) return fail(LLAMPC_E_STATE, "the tick's records are not gathered yet: call llampc_ctl_resume");
   c->pending = false;
   c->hint_ok = false;                    // until this tick's record is read
   DeviceGuard g(c->b->device);
@@ -1740,13 +1905,9 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
     // launch call, and for every rung controller at once (g_arm_list); the launch calls overlap
     // the device time.  Another controller is armed only if its locks are free (else its own
     // wait arms it).  A failed arm only turns prelaunch off.
-    std::vector<llampc_ctl*> todo;
-    {
-      std::lock_guard<std::mutex> g(g_arm_mu);
-      todo.swap(g_arm_list);
-    }
+    std::lock_guard<std::mutex> ga(g_arm_mu);
     std::vector<llampc_ctl*> keep;
-    for (llampc_ctl* x : todo) {
+    for (llampc_ctl* x : g_arm_list) {
       const bool self = x == c;
       if (!self && !x->mu.try_lock()) {
         keep.push_back(x);
@@ -1754,9 +1915,14 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
       }
       if (x->arm_next) {
         if (x->b->mu.try_lock()) {
-          x->arm_next = false;
-          DeviceGuard gx(x->b->device);
-          if (!x->b->async_pending && ctl_arm(x) != LLAMPC_OK) x->prelaunch = false;
+          if (!x->mb || x->mb->mu.try_lock()) {
+            x->arm_next = false;
+            DeviceGuard gx(x->b->device);
+            if (!x->b->async_pending && ctl_arm(x) != LLAMPC_OK) x->prelaunch = false;
+            if (x->mb) x->mb->mu.unlock();
+          } else {
+            keep.push_back(x);
+          }
           x->b->mu.unlock();
         } else {
           keep.push_back(x);
@@ -1764,10 +1930,7 @@ int llampc_ctl_wait(llampc_ctl* c, llampc_ctl_out* out) {
       }
       if (!self) x->mu.unlock();
     }
-    if (!keep.empty()) {
-      std::lock_guard<std::mutex> g(g_arm_mu);
-      g_arm_list.insert(g_arm_list.end(), keep.begin(), keep.end());
-    }
+    g_arm_list.swap(keep);
   }
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t spins = 0;
@@ -1809,10 +1972,18 @@ int llampc_ctl_device_us(llampc_ctl* c, double* us) {
 int llampc_ctl_set_prelaunch(llampc_ctl* c, int32_t on) {
   if (!c) return fail(LLAMPC_E_ARG, "controller is NULL");
   std::lock_guard<std::mutex> lc(c->mu);
-  if (on && c->mb) return fail(LLAMPC_E_STATE, "prelaunch is not available with a sharded exchange");
+  if (on && c->xg_world) return fail(LLAMPC_E_STATE, "prelaunch is not available with a gather transport");
   llampc_bank* b = c->b;
   std::lock_guard<std::mutex> lk(b->mu);
   DeviceGuard g(b->device);
+  if (on) {
+    if (!b->own_stream)
+      return fail(LLAMPC_E_STATE, "prelaunch needs the bank's own stream (the bank launches on a caller's stream)");
+    if (!b->dedicated) {                  // an armed launch must not sit on a shared hardware queue
+      bank_disarm(b);
+      if (int rc = bank_dedicate(b)) return rc;
+    }
+  }
   c->prelaunch = on != 0;
   c->arm_next = c->prelaunch && c->pending;   // a tick in flight: armed by its wait
   if (c->arm_next) arm_list_add(c);
@@ -1822,6 +1993,8 @@ int llampc_ctl_set_prelaunch(llampc_ctl* c, int32_t on) {
   }
   if (c->pending || b->async_pending) return LLAMPC_OK;
   bank_disarm(b);                         // another controller's launch on this bank
+  std::unique_lock<std::mutex> lm;
+  if (c->mb) lm = std::unique_lock<std::mutex>(c->mb->mu);
   return ctl_arm(c);
 }
 
@@ -1891,6 +2064,7 @@ int llampc_ctl_set_exchange(llampc_ctl* c, llampc_mailbox* mb, const double* gpa
   std::lock_guard<std::mutex> lc(c->mu);
   if (c->pending) return fail(LLAMPC_E_STATE, "a controller tick is outstanding");
   if (c->t != 0) return fail(LLAMPC_E_STATE, "set the exchange before the first tick");
+  if (c->xg_world) return fail(LLAMPC_E_STATE, "the controller already exchanges over a gather transport");
   ctl_cancel(c);                         // no armed launches with an exchange
   c->prelaunch = false;
   DeviceGuard g(b->device);
@@ -1904,6 +2078,86 @@ int llampc_ctl_set_exchange(llampc_ctl* c, llampc_mailbox* mb, const double* gpa
   c->d_gparams = d;
   c->n_global = n_global;
   c->mb = mb;
+  return LLAMPC_OK;
+}
+
+int32_t llampc_ctl_record_words(int32_t K) { return (K < 1 || K > LLAMPC_KMAX) ? 0 : ctl_rec_words(K); }
+
+int llampc_ctl_set_gather(llampc_ctl* c, int32_t world, int32_t rank, llampc_comm* comm, const double* gparams,
+                          int64_t n_global) {
+  if (!c || !gparams) return fail(LLAMPC_E_ARG, "NULL argument");
+  llampc_bank* b = c->b;
+  if (world < 1 || world > kCtlPxMax || rank < 0 || rank >= world)
+    return fail(LLAMPC_E_ARG, "world=%d rank=%d (world 1..%d)", world, rank, kCtlPxMax);
+  if (comm && (comm->world != world || comm->rank != rank || comm->device != b->device))
+    return fail(LLAMPC_E_ARG, "the communicator is rank %d of %d on device %d, the controller rank %d of %d on %d",
+                comm->rank, comm->world, comm->device, rank, world, b->device);
+  if (n_global < b->goff + b->n || n_global >= (int64_t)0xFFFFFFFFll)
+    return fail(LLAMPC_E_ARG, "n_global=%lld: must hold this shard [%lld, %lld) and be < 2^32 - 1", (long long)n_global,
+                (long long)b->goff, (long long)(b->goff + b->n));
+  std::lock_guard<std::mutex> lc(c->mu);
+  if (c->pending) return fail(LLAMPC_E_STATE, "a controller tick is outstanding");
+  if (c->t != 0) return fail(LLAMPC_E_STATE, "set the exchange before the first tick");
+  if (c->mb) return fail(LLAMPC_E_STATE, "the controller already exchanges over peer mailboxes");
+  ctl_cancel(c);                         // no armed launches with an exchange
+  c->prelaunch = false;
+  DeviceGuard g(b->device);
+  const int nw = ctl_rec_words(c->cfg.K);
+  double* d = nullptr;
+  if (int rc = dev_alloc(&d, 6 * (size_t)n_global)) return rc;
+  if (hipMemcpy(d, gparams, 6 * (size_t)n_global * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return fail(LLAMPC_E_HIP, "global parameter table upload failed");
+  }
+  if (c->d_gparams) (void)hipFree(c->d_gparams);
+  c->d_gparams = d;
+  c->n_global = n_global;
+  if (!c->d_xsend) {
+    int rc;
+    if ((rc = dev_alloc(&c->d_xsend, (size_t)nw)) || (rc = dev_alloc(&c->d_xgath, (size_t)kCtlPxMax * nw))) return rc;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_xstage), (size_t)kCtlPxMax * nw * sizeof(uint64_t),
+                      hipHostMallocDefault) != hipSuccess)
+      return fail(LLAMPC_E_OOM, "hipHostMalloc(gather staging) failed");
+    HIP_TRY(hipMemset(c->d_xsend, 0, (size_t)nw * sizeof(uint64_t)));
+    HIP_TRY(hipMemset(c->d_xgath, 0, (size_t)kCtlPxMax * nw * sizeof(uint64_t)));
+  }
+  c->xg_nw = nw;
+  c->xg_world = world;
+  c->xg_rank = rank;
+  c->xg_comm = comm;
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_shard_record(llampc_ctl* c, uint64_t* words, int32_t* nw) {
+  if (!c || !words || !nw) return fail(LLAMPC_E_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lc(c->mu);
+  *nw = 0;
+  if (!c->xg_wait) return LLAMPC_OK;     // no exchange on this tick (or RCCL carries it)
+  DeviceGuard g(c->b->device);
+  const size_t bytes = (size_t)c->xg_nw * sizeof(uint64_t);
+  HIP_TRY(hipMemcpyAsync(c->h_xstage, c->d_xsend, bytes, hipMemcpyDeviceToHost, c->b->stream));
+  HIP_TRY(hipStreamSynchronize(c->b->stream));
+  std::memcpy(words, c->h_xstage, bytes);
+  c->xg_read = true;
+  *nw = c->xg_nw;
+  return LLAMPC_OK;
+}
+
+int llampc_ctl_resume(llampc_ctl* c, const uint64_t* all_words) {
+  if (!c || !all_words) return fail(LLAMPC_E_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lc(c->mu);
+  if (!c->xg_wait || !c->xg_read)
+    return fail(LLAMPC_E_STATE, "no tick awaits its gathered records (llampc_ctl_shard_record first)");
+  llampc_bank* b = c->b;
+  std::lock_guard<std::mutex> lk(b->mu);
+  DeviceGuard g(b->device);
+  const size_t bytes = (size_t)c->xg_world * c->xg_nw * sizeof(uint64_t);
+  std::memcpy(c->h_xstage, all_words, bytes);
+  HIP_TRY(hipMemcpyAsync(c->d_xgath, c->h_xstage, bytes, hipMemcpyHostToDevice, b->stream));
+  const llampc_ctl::Prep& P2 = c->xg_second;
+  HIP_TRY(launch_ctl(P2.L, P2.lpm, P2.lds, b->stream));
+  c->xg_wait = false;
+  c->xg_read = false;
   return LLAMPC_OK;
 }
 

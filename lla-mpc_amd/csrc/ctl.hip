@@ -559,6 +559,26 @@ __device__ __forceinline__ void ctl_complete(const CtlLaunch& c, unsigned char* 
 // top-K Dr / Df for mu-hat are written.  A peer that never arrives (past px_bound): this
 // shard's own selection is used and the record's status says so.
 // ------------------------------------------------------------------------------------
+// Word w of this shard's record: entry w / 4 of lb_final<2>'s lists (cs.ids local index / cs.xv
+// window mean) as value hi, lo, global index hi, lo (index -1: none).
+__device__ __forceinline__ uint32_t ctl_rec_word(const CtlSel& cs, int64_t goff, int w) {
+  const int e = w >> 2;
+  const uint32_t l = cs.ids[e];
+  const uint64_t q = (w & 2) ? (uint64_t)(l == kNoLocal ? (int64_t)-1 : goff + (int64_t)l)
+                             : (uint64_t)__double_as_longlong(cs.xv[e]);
+  return (w & 1) ? (uint32_t)q : (uint32_t)(q >> 32);
+}
+
+// A gather transport's first launch (px_phase 1): the look-back's ticket winner stores this
+// shard's record, tagged px_seq, at px_send for the all-gather between the launches, and
+// re-arms the look-back ticket (the completion does it on one-launch ticks).
+__device__ __forceinline__ void ctl_px_send(const CtlLaunch& c, const CtlSel& cs) {
+  __syncthreads();                                       // lb_final's wave 0 wrote cs.ids / xv
+  const int nw = ctl_rec_words(c.K);
+  for (int w = threadIdx.x; w < nw; w += kBlock) st_wt(&c.px_send[w], tag_word(c.px_seq, ctl_rec_word(cs, c.fin.goff, w)));
+  if (threadIdx.x == 0) __hip_atomic_store(&c.tickets[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void ctl_exchange(const CtlLaunch& c, unsigned char* smem, const CtlSel& cs) {
   const int tid = threadIdx.x;
   const int G = c.px_G, rank = c.px_rank, K = c.K, nw = ctl_rec_words(K), M = G * K;
@@ -569,22 +589,26 @@ __device__ __forceinline__ void ctl_exchange(const CtlLaunch& c, unsigned char* 
   uint64_t* eid = ekey + M;
   int* top = reinterpret_cast<int*>(eid + M);            // [KMAX] entry of each merged rank
   int* wlate = top + LLAMPC_KMAX;                        // [kWaves]
-  __syncthreads();                                       // lb_final's wave 0 wrote cs.ids / xv
-  // (a) this shard's record: to LDS and, tagged, to every peer (one (peer, word) per thread)
-  const size_t slot0 = (size_t)(c.px_seq & 1) * G * kRecWords;
+  const bool gath = c.px_phase == 2;                     // launch-uniform
+  if (!gath) __syncthreads();                            // lb_final's wave 0 wrote cs.ids / xv
+  // (a) this shard's record: to LDS and, tagged, to every peer (one (peer, word) per thread);
+  // gathered: the own record from px_send (the first launch's), the peers' come from px_gath
+  const size_t slot0 = gath ? 0 : (size_t)(c.px_seq & 1) * G * kRecWords;
   const size_t mine = slot0 + (size_t)rank * kRecWords;
-  for (int p = tid; p < G * nw; p += kBlock) {
-    const int g = p / nw, w = p - g * nw, e = w >> 2;
-    const uint32_t l = cs.ids[e];
-    const uint64_t q = (w & 2) ? (uint64_t)(l == kNoLocal ? (int64_t)-1 : goff + (int64_t)l)
-                               : (uint64_t)__double_as_longlong(cs.xv[e]);
-    const uint32_t word = (w & 1) ? (uint32_t)q : (uint32_t)(q >> 32);
-    if (g == rank) rec32[(size_t)rank * nw + w] = word;
-    else __hip_atomic_store(c.px_box[g] + mine + w, tag_word(c.px_seq, word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (gath) {
+    for (int w = tid; w < nw; w += kBlock) rec32[(size_t)rank * nw + w] = (uint32_t)ld_wt(&c.px_send[w]);
+  } else {
+    for (int p = tid; p < G * nw; p += kBlock) {
+      const int g = p / nw, w = p - g * nw;
+      const uint32_t word = ctl_rec_word(cs, goff, w);
+      if (g == rank) rec32[(size_t)rank * nw + w] = word;
+      else __hip_atomic_store(c.px_box[g] + mine + w, tag_word(c.px_seq, word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
-  // (b) the peers' records from this rank's mailbox
+  // (b) the peers' records from this rank's mailbox (gathered: from px_gath, stride nw)
   constexpr int kPer = (kCtlPxMax * ctl_rec_words(LLAMPC_KMAX) + kBlock - 1) / kBlock;
-  const uint64_t* own = c.px_box[rank] + slot0;
+  const uint64_t* own = gath ? c.px_gath : c.px_box[rank] + slot0;
+  const size_t stride = gath ? (size_t)nw : (size_t)kRecWords;
   const int total = G * nw;
   uint64_t need = 0;
 #pragma unroll
@@ -601,7 +625,7 @@ __device__ __forceinline__ void ctl_exchange(const CtlLaunch& c, unsigned char* 
     for (int j = 0; j < kPer; ++j) {
       const int e = ((need >> j) & 1) ? tid + j * kBlock : rank * nw;   // idle: own slot (never read back)
       const int g = e / nw, w = e - g * nw;
-      v[j] = __hip_atomic_load(own + (size_t)g * kRecWords + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      v[j] = __hip_atomic_load(own + (size_t)g * stride + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -1448,7 +1472,8 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch arg) {
   const Scratch sc(smem);
   int* flag = reinterpret_cast<int*>(smem + kFlagOff);
   const int blk = (int)blockIdx.x;
-  if (blk == 0 && threadIdx.x == 0 && !c.door)   // x_t in the argument: the device time starts here
+  // x_t in the argument: the device time starts here (a gathered tick's: at its first launch)
+  if (blk == 0 && threadIdx.x == 0 && !c.door && !(PX && c.px_phase == 2))
     st_wt(&c.door_dev[kCtlTimeWord], (uint64_t)__builtin_amdgcn_s_memrealtime());
   if (blk >= c.nb_lb + c.nb_la) {       // spec blocks (CtlLaunch.n_spec), last in the grid
     ctl_spec<LPM>(c, blk - c.nb_lb - c.nb_la, smem, sc);
@@ -1483,7 +1508,12 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch arg) {
     }
     return xl;
   };
-  if (c.do_lb) {
+  if (PX && c.px_phase == 2) {         // a gathered tick's second launch: block 0 merges, completes
+    if (!door(0.0, false, 0)) return;
+    ctl_exchange(c, smem, cs);
+    __threadfence_system();             // the record's look-back half (pinned host memory)
+    __syncthreads();
+  } else if (c.do_lb) {
     LookbackLaunch lb = c.lb;           // x_prev / u_prev: the state
     CTL_STAMP(blk, 0);
     if (!lookback_block<true>(lb, blk, sc, door)) return;
@@ -1492,6 +1522,10 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch arg) {
     if (c.full) {
       if constexpr (PX) {
         lb_final<2>(c.fin, smem, &cs);  // this shard's lists, then the exchange and the merge
+        if (c.px_phase == 1) {          // gathered: the record out, the rest in the second launch
+          ctl_px_send(c, cs);
+          return;
+        }
         ctl_exchange(c, smem, cs);
       } else {
         lb_final<1>(c.fin, smem, &cs);

@@ -338,6 +338,16 @@ struct CtlLaunch {
   int32_t px_G, px_rank;
   uint32_t px_seq;            // the mailbox's tick number of this exchange
   uint32_t px_bound;          // the peers' wait bound, units of 2^16 s_memrealtime ticks
+  // gather transports (llampc_ctl_set_gather: RCCL or the host carries the records, no peer
+  // mailbox): a full-window tick is two launches.  px_phase 1 — the look-back blocks alone; the
+  // ticket winner stores this shard's record, ctl_rec_words(K) words tagged px_seq, at px_send
+  // and exits.  Between the launches the G records are all-gathered into px_gath [G][nw].
+  // px_phase 2 — block 0 (nb_lb = 1) reads them (ctl_exchange: the same merge, the own record
+  // from px_send, the peers' from px_gath, every word's tag checked) and completes the tick;
+  // the look-ahead blocks as in one launch.  px_phase 0: the peer mailbox (one launch).
+  int32_t px_phase;
+  uint64_t* px_send;          // [nw] (phase 1 writes, phase 2 reads)
+  const uint64_t* px_gath;    // [G][nw]
   // armed launch (door != null, llampc_ctl_set_prelaunch): enqueued behind the previous tick,
   // it runs its x_t-independent prologue and then waits for the host's doorbell: kCtlDoorWords
   // tagged words (tag door_seq) in pinned memory — x_t as 12 32-bit halves, then the status

@@ -15,19 +15,11 @@
 
 #include "fastmath.hpp"
 
-// Transcendentals of the model: the short-chain versions (fastmath.hpp) by default;
-// -DLLAMPC_OCML_MATH selects ocml's for A/B measurements.
-#ifdef LLAMPC_OCML_MATH
-#define LL_ATAN2P(y, x) atan2((y), (x))
-#define LL_ATAN(z) atan(z)
-#define LL_SIN(a) sin(a)
-#define LL_SINCOS(a, s, c) sincos((a), (s), (c))
-#else
+// Transcendentals of the model: the short-chain versions (fastmath.hpp).
 #define LL_ATAN2P(y, x) ::llampc::fm::atan2_xpos((y), (x))
 #define LL_ATAN(z) ::llampc::fm::atan_(z)
 #define LL_SIN(a) ::llampc::fm::sin_(a)
 #define LL_SINCOS(a, s, c) ::llampc::fm::sincos_((a), (s), (c))
-#endif
 namespace llampc {
 
 // Per-bank constants in kernel-argument space (wave-uniform → SGPRs).
@@ -227,22 +219,11 @@ __device__ __forceinline__ double dpp_bcast(double v) {
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
-// The same quad_perm through the LDS crossbar (ds_swizzle_b32, QDMode: offset bit 15 set,
-// bits 7:0 = the quad_perm selector, the DPP encoding): issued to the LDS pipe instead of
-// the VALU (a v_mov_b32_dpp costs ~8 VALU cycles), longer latency.  LLAMPC_SWZ_MASK selects
-// which of the quad's four broadcasts (bit 0 Ffy, 1 Fry, 2 sp, 3 cp) take this route (A/B).
-#ifndef LLAMPC_SWZ_MASK
-#define LLAMPC_SWZ_MASK 0
-#endif
+// (The same quad_perm through the LDS crossbar, ds_swizzle_b32 QDMode, measured slower in
+// round 2: the broadcasts stay DPP.)
 template <int CTRL, int BIT>
 __device__ __forceinline__ double quad_bcast(double v) {
-  if constexpr (((LLAMPC_SWZ_MASK >> BIT) & 1) != 0) {
-    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x8000 | CTRL);
-    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x8000 | CTRL);
-    return __hiloint2double(hi, lo);
-  } else {
-    return dpp_bcast<CTRL>(v);
-  }
+  return dpp_bcast<CTRL>(v);
 }
 // quad_perm broadcasts within lane pairs: [0,0,2,2] = 0xA0, [1,1,3,3] = 0xF5; within a
 // quad: lane q to all four = 0x00, 0x55, 0xAA, 0xFF; xor-1 / xor-2 swaps = 0xB1, 0x4E.
@@ -300,15 +281,9 @@ struct Dom {
   }
 };
 
-// -DLLAMPC_PAIR_LA: the LPM-1 look-ahead lane evaluates its front and rear chains with one
-// reciprocal per division pair (chain_pair; lean cores only).  A/B only: 16 -> 8 v_rcp_f64 but
-// 843 -> 858 instructions per step, and C = 64 ran 375-380 -> 383-385 us per tick
-// (profiles/r03/v31/ab_pair_c64.log), so the default keeps two chain_fast.
-#ifdef LLAMPC_PAIR_LA
-constexpr bool kPairLA = true;
-#else
-constexpr bool kPairLA = false;
-#endif
+// (Round 3 measured the LPM-1 lane's front and rear chains with one reciprocal per division
+// pair, chain_pair: 16 -> 8 v_rcp_f64 but 843 -> 858 instructions per step, C = 64 375-380 ->
+// 383-385 us per tick, profiles/r03/v31/ab_pair_c64.log; the rollouts keep two chain_fast.)
 
 // F = D sin(C atan(B slip)) with slip = dsel - atan2(yy, den) for the front tire
 // (dsel = delta) and atan2(yy, den) for the rear (dsel = 0); yy = lf om + vy | lr om - vy
@@ -379,13 +354,8 @@ __device__ __forceinline__ double chain_fold(const Chain& c, double den, double 
   const double pa = fma(pm, rr, po);
   const int fs = __double2loint(t2) << 31;               // (-1)^k on the argument
   const double arg_psi = __hiloint2double(__double2hiint(pa) ^ fs, __double2loint(pa));
-#ifdef LLAMPC_FOLD_MASK   // A/B: lanes 2/3 masked off (exec) during the chain's atans
-  double at = 0.0;
-  if (pm == 0.0) {
-#else
   double at;
   {
-#endif
     const double yy = fma(c.lw, om, c.sg * vy);
     double h2;
     const double a2 = fm::atan2_fast<LEAN>(yy, den, K, h2);
@@ -472,8 +442,6 @@ __device__ __forceinline__ StageF forces_fast(const StageK& sk, double den, doub
     const double r = chain_fast<LEAN>(sk.ch[0], den, vy, om, d * sk.fw, dm, K);
     f.Ffy = dpp_bcast<kPair0>(r);
     f.Fry = dpp_bcast<kPair1>(r);
-  } else if constexpr (LEAN && kPairLA) {
-    chain_pair(sk.ch[0], sk.ch[1], den, vy, om, d, dm, K, f.Ffy, f.Fry);
   } else {
     f.Ffy = chain_fast<LEAN, false>(sk.ch[0], den, vy, om, d, dm, K);
     f.Fry = chain_fast<LEAN, false>(sk.ch[1], den, vy, om, 0.0, dm, K);
@@ -548,13 +516,8 @@ __device__ __forceinline__ Input make_input_fast(double a, double d, const fm::F
 // FmK::load<kLeanLA>()): ~1e-13 relative on the tire forces (8 terms, round 4; ~1e-14 with 9);
 // 456 instructions per step at LPM 4 (467 with 9 terms, 494 with the precise 10-term cores,
 // 507 in round 2), A/B 28.8 -> 27.2 us per tick with 9 terms (profiles/r03/ab_lean), 26.6
-// with 8 (profiles/r04/ab_lean8.log).  -DLLAMPC_PRECISE_LA
-// builds the precise (<= 4 ulp) cores into the look-ahead too, for A/B runs.
-#ifdef LLAMPC_PRECISE_LA
-constexpr bool kLeanLA = false;
-#else
+// with 8 (profiles/r04/ab_lean8.log).
 constexpr bool kLeanLA = true;
-#endif
 
 struct FusedK {
   double h, hm, hIlf, hIlr, m1, m0, m2, m3;   // hm = h/m; m1 = hm k1, m0 = hm k0,
@@ -562,14 +525,10 @@ struct FusedK {
 
 // The fused rollouts that carry the scaled yaw state (W = h omega, Psi = (2/pi) psi, see
 // make_fused): the LPM-4 quad (round 2) and, from round 3, the LPM-1 lane (its sin/cos psi by
-// the fold of forces_fast; -DLLAMPC_NO_SCALED1 keeps LPM 1 on sincos_fast for A/B runs).
+// the fold of forces_fast).
 // LPM 2 keeps omega and psi.
 constexpr bool scaled_yaw(int lpm) {
-#ifdef LLAMPC_NO_SCALED1
-  return lpm == 4;
-#else
   return lpm == 4 || lpm == 1;
-#endif
 }
 // SCALED (the LPM = 4 quad): the rollout state carries W = h omega and Psi = (2/pi) psi
 // instead of omega and psi.  Then the yaw increment IS W (no h omega product), vy W and vx W

@@ -173,7 +173,7 @@ constexpr double kSinWQ[10] = {
 // atan(t) = t + t*s*QR(s) for |t| <= tan(pi/8) (10 terms: fit error 1.5e-16 relative, <= 1 ulp): the fast cores reduce their
 // ratio r in [0, 1] by atan(r) = pi/4 + atan((r - 1)/(r + 1)) when r > tan(pi/8), so the
 // polynomial is half as long as QA's on [0, 1] for 6 more instructions
-// (tools/fit_fastmath.py; -DLLAMPC_ATAN_FULL keeps the 22-term core for A/B runs).
+// (tools/fit_fastmath.py).
 constexpr double kAtanR[10] = {
     -0.3333333333333325,  0.19999999999898407,  -0.1428571426609662,
     0.11111109636534361,  -0.09090852557176049,  0.0769105515839315,
@@ -226,12 +226,8 @@ constexpr double kSinWideMax = 3.0;   // sin(a) = a + a*s*QW(s) (10 terms, fit e
 // VGPR constant for free, while a rematerialised 64-bit constant costs two v_mov/s_mov
 // issue slots per use — 2.5x on a Horner chain in the one-wave-per-SIMD regime.
 struct FmK {
-#ifdef LLAMPC_ATAN_FULL
-  double at[22];
-#else
   double ar[10];
   double tp8, pio4;
-#endif
   double sw[10], sq[7], cq[7];
   double pio2, two_pi, cw0, cw1, cw2, sixth, six, rmagic, rmagic2, one;
   double inv_pi, inv_3pi;                 // (2/pi)/2, (2/pi)/6: the scaled yaw's RK4 weights
@@ -242,17 +238,12 @@ struct FmK {
   __device__ __forceinline__ static FmK load() {
     FmK k;
     constexpr int nA = LEAN ? kLeanTerms : 10;
-#ifdef LLAMPC_ATAN_FULL
-#pragma unroll
-    for (int i = 0; i < 22; ++i) { k.at[i] = kAtanQ[i]; pin(k.at[i]); }
-#else
 #pragma unroll
     for (int i = 0; i < nA; ++i) { k.ar[i] = LEAN ? kAtanRL[i] : kAtanR[i]; pin(k.ar[i]); }
     k.tp8 = kTanPi8;
     k.pio4 = kPio4;
     pin(k.tp8);
     pin(k.pio4);
-#endif
 #pragma unroll
     for (int i = 0; i < nA; ++i) { k.sw[i] = LEAN ? kSinWQL[i] : kSinWQ[i]; pin(k.sw[i]); }
 #pragma unroll
@@ -283,9 +274,6 @@ struct FmK {
 
 template <int N>
 __device__ __forceinline__ double horner(const double* c, double s) {
-#ifdef LLAMPC_ABL_NOPOLY  // diagnostic ablation builds only
-  return fma(c[1], s, c[0]);
-#endif
   double p = c[N - 1];
 #pragma unroll
   for (int i = N - 2; i >= 0; --i) p = fma(p, s, c[i]);
@@ -298,9 +286,6 @@ __device__ __forceinline__ double horner(const double* c, double s) {
 // tests, whose every call divides, bound the result).
 template <bool LEAN = false>
 __device__ __forceinline__ double div_fast(double num, double den) {
-#ifdef LLAMPC_ABL_NODIV   // diagnostic ablation builds only (tools/micro/ablate.sh)
-  return num * den;
-#endif
   double r = __builtin_amdgcn_rcp(den);
   const double e = fma(-den, r, 1.0);
   r = fma(r, e, r);
@@ -366,17 +351,11 @@ __device__ __forceinline__ double vmin_abs2(double a, double b) {  // min(|a|, |
 // fix-ups (tests: test_fast_cores_ulp_on_domain).
 template <bool LEAN = false>
 __device__ __forceinline__ double atan_ratio_k(double n, double d, const FmK& K) {
-#ifdef LLAMPC_ATAN_FULL
-  const double t = div_fast(n, d);
-  const double s = t * t;
-  return fma(t * s, horner<22>(K.at, s), t);
-#else
   const bool red = n > K.tp8 * d;
   const double sf = __hiloint2double(red ? 0x3FF00000 : 0, 0);
   const double t = div_fast<LEAN>(fma(-sf, d, n), fma(sf, n, d));
   const double s = t * t;
   return fma(sf, K.pio4, fma(t * s, horner<LEAN ? kLeanTerms : 10>(K.ar, s), t));
-#endif
 }
 
 // atan2(y, x) for x >= 0 on the domain atan2_fast_ok(y, x): the sum |y| + x in

@@ -14,12 +14,8 @@ constexpr int kBlock = 256;            // 4 waves of 64 lanes
 // The work-queue layout's look-ahead blocks (throughput regime): 8 waves, one block per CU,
 // so each SIMD interleaves two rollout waves (a lone fp64 wave issues ~4.7 cycles per
 // instruction against the VALU's 4).  The other roles of that launch use 256 threads (the
-// rest of their waves exit at once).  -DLLAMPC_WQ_BLOCK=256 keeps one wave per SIMD (A/B).
-#ifdef LLAMPC_WQ_BLOCK
-constexpr int kBlockWQ = LLAMPC_WQ_BLOCK;
-#else
+// rest of their waves exit at once).
 constexpr int kBlockWQ = 512;
-#endif
 // Work-queue layouts (plan kernel template argument WQ): 0 = none (block per models), 1 = one
 // 4-wave block per CU, 2 = one 8-wave block per CU (two rollout waves per SIMD; staged launches
 // only — the unstaged rollout would spill at 256 VGPRs).  launch_plan picks by the size of the

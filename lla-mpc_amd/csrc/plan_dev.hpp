@@ -574,20 +574,6 @@ __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk,
       Dom dm;
       dm.init();
       step_fast<0, 1>(a.veh, t, sk, x, uf, a.Ts, K, dm);
-#ifdef LLAMPC_LB_TWICE
-      // diagnostic (stamps build only): the same step again, warm — its cycles against the first's
-      // split the first step's time into the code's cold fetch + the operands' loads vs the issue
-      if (r == 0) {
-        LB_STAMP(blk, 4);
-        double x2[6];
-        for (int j = 0; j < 6; ++j) x2[j] = a.x_prev[j];
-        Dom d2;
-        d2.init();
-        step_fast<0, 1>(a.veh, t, sk, x2, uf, a.Ts, K, d2);
-        asm volatile("" ::"v"(x2[0]), "v"(x2[1]), "v"(x2[2]), "v"(x2[3]));
-        LB_STAMP(blk, 5);
-      }
-#endif
       bad = (int)ubad | (int)!sk.sok | (int)!dm.ok();
     }
     double s = sq_err4(x, x_now);                         // rt.py:349 mean over 4 states
@@ -842,8 +828,7 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
   // the later stages' positions, the last stage's feeds vx, vy, omega only through a NaN
   // state that the position update already carries), so a non-finite J is re-run too
   if (FAST) {
-    constexpr bool kPaired = INTEG == 0 && LPM == 1 && kLeanLA && kPairLA;   // dyn.hpp chain_pair
-    const bool dok = kPaired ? dm.ok_paired() : dm.ok();
+    const bool dok = dm.ok();
     bad = (int)bad | (int)!sk.sok | (int)!dok | (int)!(fabs(J) <= __DBL_MAX__);
     if (S4) bad = (int)bad | (int)(feas_s != feas_s);   // a steering outside sincos_fast's domain
   }
@@ -2051,15 +2036,10 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
   // WQ launches run kBlockWQ threads per block: every role but the work-queue look-ahead is
   // written for kBlock and its surplus waves leave at once (s_barrier waits for the waves
   // that have not ended)
-  // block roles: look-back blocks first in the grid (dispatch order); -DLLAMPC_LA_FIRST puts
-  // the look-ahead blocks first (A/B)
-#ifdef LLAMPC_LA_FIRST
-  const bool is_lb = (int)blockIdx.x >= fin.nb_la;
-  const int lb_blk = (int)blockIdx.x - fin.nb_la, la_blk = (int)blockIdx.x;
-#else
+  // block roles: look-back blocks first in the grid (dispatch order; the look-ahead blocks
+  // first measured 26.82-26.92 -> 27.67-27.75 us per tick)
   const bool is_lb = (int)blockIdx.x < fin.nb_lb;
   const int lb_blk = (int)blockIdx.x, la_blk = (int)blockIdx.x - fin.nb_lb;
-#endif
   if constexpr (wq_threads(WQ) > kBlock) {
     if (is_lb && threadIdx.x >= kBlock) return;
   }
@@ -2067,10 +2047,6 @@ __device__ __forceinline__ void plan_body(const LookbackLaunch& lb, const Lookah
     lookback_block(lb, lb_blk, sc);
     if (!ticket_last(&fin.tickets[0], (unsigned)fin.nb_lb, flag)) return;
     if (fin.full) {
-#ifdef LLAMPC_LBF_TWICE                       // diagnostic: the stamps then time a warm lb_final
-      lb_final(fin, smem);
-      __syncthreads();
-#endif
       lb_final(fin, smem);
       // host completion: lb_final's record stores are performed before any later hand-off
       // (the final block, possibly another one, publishes the host tag after them)

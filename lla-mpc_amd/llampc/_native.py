@@ -24,7 +24,12 @@ E_ARG, E_HIP, E_NODEV, E_STATE, E_OOM, E_DEVICE = -1, -2, -3, -4, -5, -6
 
 
 class NativeError(RuntimeError):
-    """A libllampc_hip call failed (message = llampc_last_error())."""
+    """A libllampc_hip call failed (message = llampc_last_error(); ``code`` = its LLAMPC_E_* return
+    code, None when raised by the Python layer)."""
+
+    def __init__(self, msg="", code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 class NoDeviceError(NativeError):
@@ -127,8 +132,10 @@ _SIGNATURES = {
     "llampc_merge": (C.c_int, [C.POINTER(PlanOut), C.c_int32, C.c_int32, C.POINTER(PlanOut)]),
     "llampc_merge_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
                                       C.c_void_p]),
-    "llampc_exchange_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
-                                         C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "llampc_comm_unique_id": (C.c_int, [C.c_void_p]),
+    "llampc_comm_create": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "llampc_comm_destroy": (C.c_int, [C.c_void_p]),
+    "llampc_exchange_rccl": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "llampc_mailbox_create": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     "llampc_mailbox_ipc_handle": (C.c_int, [C.c_void_p, C.c_void_p]),
     "llampc_mailbox_open_peer": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
@@ -147,6 +154,10 @@ _SIGNATURES = {
                                        _dp, C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
     "llampc_ctl_destroy": (C.c_int, [C.c_void_p]),
     "llampc_ctl_set_exchange": (C.c_int, [C.c_void_p, C.c_void_p, _dp, C.c_int64]),
+    "llampc_ctl_set_gather": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, _dp, C.c_int64]),
+    "llampc_ctl_record_words": (C.c_int32, [C.c_int32]),
+    "llampc_ctl_shard_record": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)]),
+    "llampc_ctl_resume": (C.c_int, [C.c_void_p, C.c_void_p]),
     "llampc_ctl_set_prelaunch": (C.c_int, [C.c_void_p, C.c_int32]),
     "llampc_ctl_device_us": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     "llampc_ctl_merge": (C.c_int, [_dp, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, _dp,
@@ -207,7 +218,7 @@ def load():
 def check(rc: int):
     if rc != 0:
         msg = load().llampc_last_error().decode(errors="replace")
-        raise (NoDeviceError if rc == E_NODEV else NativeError)(f"llampc error {rc}: {msg}")
+        raise (NoDeviceError if rc == E_NODEV else NativeError)(f"llampc error {rc}: {msg}", rc)
 
 
 def device_count() -> int:

@@ -128,7 +128,10 @@ class ModelBank:
         nat.check(nat.load().llampc_bank_set_stream(self.handle, stream_ptr))
 
     def stream_handle(self) -> int:
-        """The hipStream_t the bank launches on (its own stream: a hardware queue of its own)."""
+        """The hipStream_t the bank launches on now.  Its own stream is a plain one until
+        set_concurrency(> 1) or an armed controller (LLAMPC prelaunch) gives it a hardware queue
+        of its own — which REPLACES the stream: a handle read before either call is destroyed
+        (read it again; llampc_bank_stream)."""
         h = nat.C.c_void_p()
         nat.check(nat.load().llampc_bank_stream(self.handle, nat.C.byref(h)))
         return int(h.value or 0)

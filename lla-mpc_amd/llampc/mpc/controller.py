@@ -190,6 +190,8 @@ class DeviceController:
         lib = nat.load()
         self._xp = self._x.ctypes.data
         self._f_async, self._f_wait = lib.llampc_ctl_tick_async, lib.llampc_ctl_wait
+        self._carrier = None                 # a ShardedBank whose process group carries the exchange
+        self.transport = None                # the sharded exchange's transport (set_exchange)
         self.prelaunch = False
         if prelaunch:
             self.set_prelaunch(True)
@@ -215,6 +217,9 @@ class DeviceController:
         out = nat.CtlOut() if out is None else out
         x = self._x
         x[:] = x_t
+        if self._carrier is not None:        # the host carries the exchange between the launches
+            self.tick_async(x_t)
+            return self.wait(out)
         nat.check(nat.load().llampc_ctl_tick(self._h, x.ctypes.data, nat.C.addressof(out)))
         return out
 
@@ -226,23 +231,48 @@ class DeviceController:
 
     def wait(self, out=None) -> "nat.CtlOut":
         out = nat.CtlOut() if out is None else out
+        if self._carrier is not None:
+            self._carry()
         rc = self._f_wait(self._h, nat.C.addressof(out))
         if rc:
             nat.check(rc)
         return out
 
+    def _carry(self):
+        """The host-carried exchange of a gathered tick (llampc_ctl_shard_record / _resume): this
+        rank's record after the first launch, the group's all-gather, the second launch."""
+        lib = nat.load()
+        nw = nat.C.c_int32()
+        nat.check(lib.llampc_ctl_shard_record(self._h, self._words.ctypes.data, nat.C.byref(nw)))
+        if nw.value == 0:                    # no exchange on this tick (the window is not full)
+            return
+        allw = np.ascontiguousarray(self._carrier.gather_words(self._words[:nw.value]))
+        nat.check(lib.llampc_ctl_resume(self._h, allw.ctypes.data))
+
     def set_exchange(self, sharded):
-        """Tick this controller as one rank of a SHARDED bank (llampc_ctl_set_exchange): ``sharded``
-        is this rank's ShardedBank (its shard is the bank this controller drives; its peer
-        mailbox carries the per-tick exchange).  Every rank then holds the unsharded controller's
-        selection, record and state.  Call on every rank before the first tick."""
+        """Tick this controller as one rank of a SHARDED bank: ``sharded`` is this rank's
+        ShardedBank (its shard is the bank this controller drives).  Every rank then holds the
+        unsharded controller's selection, record and state.  Call on every rank before the first
+        tick.  The transport is the ShardedBank's: its peer mailboxes (llampc_ctl_set_exchange: the
+        exchange inside the tick's one launch), its RCCL communicator (llampc_ctl_set_gather: two
+        launches with ncclAllGather between them on the bank's stream), or the process group on
+        the host (c10d / host: llampc_ctl_set_gather without a communicator, the records carried
+        by ``wait``)."""
         if sharded.bank is not self.bank:
             raise ValueError("the controller must drive the ShardedBank's own shard")
-        if sharded.mailbox is None:
-            raise nat.NativeError("the sharded controller needs the peer mailbox transport "
-                                  f"(transport {sharded.transport!r}: {sharded.fallback_reason})")
         pg = sharded.params_global
-        nat.check(nat.load().llampc_ctl_set_exchange(self._h, sharded.mailbox, nat.dptr(pg), int(pg.shape[1])))
+        lib = nat.load()
+        if sharded.mailbox is not None:
+            nat.check(lib.llampc_ctl_set_exchange(self._h, sharded.mailbox, nat.dptr(pg), int(pg.shape[1])))
+            self.transport = "peer"
+        else:
+            comm = sharded.comm
+            nat.check(lib.llampc_ctl_set_gather(self._h, int(sharded.world), int(sharded.rank), comm, nat.dptr(pg),
+                                                int(pg.shape[1])))
+            if comm is None:
+                self._carrier = sharded
+                self._words = np.zeros(int(lib.llampc_ctl_record_words(int(self.cfg.K))), dtype=np.uint64)
+            self.transport = "rccl" if comm is not None else sharded.transport
         self._gparams = pg
 
     def inputs(self):
@@ -373,6 +403,11 @@ class LLAMPC:
                                          nan_policy=nan_policy, debug_inputs=debug_inputs)
             if sharded is not None and sharded.exchange:
                 self._ctl.set_exchange(sharded)
+                if prelaunch and self._ctl.transport == "peer":
+                    # an armed launch needs the bank's own (dedicated-queue) stream, not the
+                    # ShardedBank's torch stream of plan() ticks (the shard is the controller's alone)
+                    bank.set_stream(None)
+                    self._ctl.set_prelaunch(True)
             elif prelaunch:
                 self._ctl.set_prelaunch(True)
         else:
@@ -398,9 +433,17 @@ class LLAMPC:
         self.last_topk = None
 
     def set_prelaunch(self, on=True):
-        """Device mode: arm every next tick (the default; DeviceController.set_prelaunch) or not."""
-        if self._ctl is not None and not (self.sharded is not None and self.sharded.exchange):
-            self._ctl.set_prelaunch(on)
+        """Device mode: arm every next tick (the default; DeviceController.set_prelaunch) or not.
+        A sharded controller arms over the peer transport only (the gather transports run two
+        launches per tick)."""
+        if self._ctl is None:
+            return
+        if self.sharded is not None and self.sharded.exchange:
+            if self._ctl.transport != "peer":
+                return
+            if on and not self._ctl.prelaunch:
+                self.bank.set_stream(None)
+        self._ctl.set_prelaunch(on)
 
     def device_us(self) -> float:
         """Device mode: the last tick's device time (DeviceController.device_us); else NaN."""
@@ -503,11 +546,19 @@ class LLAMPC:
                                   "bank and the controller")
 
     def _guarded(self, fn):
-        """A device tick that raises (a wait that timed out, a record with status != 0) has still
-        advanced the device controller's tick and window: the host mirror records the step
-        (t advances) and the controller refuses further ticks."""
+        """A device tick that failed on the device (a wait that timed out or expired: LLAMPC_E_DEVICE;
+        a HIP error; a record with status != 0) has still advanced the device controller's tick and
+        window: the host mirror records the step (t advances) and the controller refuses further
+        ticks.  A call the library refused before launching anything (an argument or
+        state error: LLAMPC_E_ARG / E_STATE) consumed no step and is re-raised as it is."""
         try:
             return fn()
+        except nat.NativeError as e:
+            if e.code in (nat.E_ARG, nat.E_STATE, nat.E_OOM, nat.E_NODEV):
+                raise
+            self.failed = self.t
+            self.t += 1
+            raise
         except Exception:
             self.failed = self.t
             self.t += 1

@@ -15,12 +15,7 @@ One tick's pack is [x_prev 6 | u_prev 2 | x_now 6 | uprev 2 | xref 2(H+1) | U 2C
 the layout of ShardedBank.make_plan_in.  The plant runs on the device (the library's RK6)."""
 from __future__ import annotations
 
-import os
-
 import numpy as np
-
-_DYN = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))),
-                    "tests", "golden", "dyn_slice.npz")
 
 
 def default_scenario(track_name: str) -> str:
@@ -47,7 +42,7 @@ def scenario_ticks(track_name: str, H: int, C: int, T: int, scenario: str | None
     from llampc.mpc.controller import CandidateGenerator
     from llampc.mpc.planner import ConstantSpeed
     from llampc.params import ORCA
-    from llampc.tracks import ETHZ, ETHZMobil
+    from llampc.tracks import ETHZ, ETHZMobil, dyn_slice
     p = ORCA()
     plant = Dynamic(**p, device=device)
     track = ETHZ('optimal', True) if track_name == "ETHZ" else ETHZMobil('optimal', True)
@@ -58,7 +53,7 @@ def scenario_ticks(track_name: str, H: int, C: int, T: int, scenario: str | None
         v0, u_rec = mobil_controls(T + 1)
         x = np.array([track.x_init, track.y_init, track.psi_init, *v0])
     else:
-        d = np.load(dyn_path or _DYN)
+        d = np.load(dyn_path) if dyn_path else dyn_slice()
         u_rec = d["inputs"]
         x = d["states"][:, 0].copy()
     if scenario == "gradual":

@@ -18,7 +18,9 @@ Transports of the exchange (LLAMPC_EXCHANGE; the merged record is the same for a
         per rank per tick; LLAMPC_PEER_SPLIT=1 runs the exchange as a second kernel).  Set up with one
         all_gather_object of the IPC handles on any backend (gloo included), then checked by a
         probe exchange against the host merge; on any failure every rank falls back together.
-  rccl  — ncclAllGather of the process's RCCL on the tick stream + merge_kernel.
+  rccl  — ncclAllGather on the tick stream over the library's own communicator (llampc_comm_*:
+        ncclGetUniqueId on rank 0, shared through the process group, ncclCommInitRank on every
+        rank; the RCCL the process already holds) + merge_kernel.
   c10d  — torch.distributed.all_gather_into_tensor + merge_kernel.
   host  — (gloo) records gathered on the host, merged by merge_kernel.
 """
@@ -40,20 +42,6 @@ def _bytes_of(o: nat.PlanOut) -> np.ndarray:
 
 def _out_of(b: np.ndarray) -> nat.PlanOut:
     return nat.PlanOut.from_buffer_copy(np.ascontiguousarray(b, dtype=np.uint8).tobytes())
-
-
-def _rccl_allgather_addr() -> int:
-    """Address of ncclAllGather in the RCCL this process already loaded (torch's), found in
-    /proc/self/maps: llampc_exchange_device calls it, so no second RCCL is loaded."""
-    path = None
-    with open("/proc/self/maps") as f:
-        for line in f:
-            if "librccl" in line:
-                path = line.split()[-1]
-                break
-    if path is None:
-        raise nat.NativeError("no RCCL library loaded in this process")
-    return C.cast(C.CDLL(path).ncclAllGather, C.c_void_p).value
 
 
 def _all_gather_obj(obj, group=None) -> list:
@@ -165,9 +153,9 @@ class ShardedBank:
         # (the self-spawned 2-rank bench crashed at the end with the bank's stream destroyed)
         self.stream = torch.cuda.Stream(device=dev)
         self.bank.set_stream(self.stream.cuda_stream)
-        # native exchange (nccl): the all-gather is issued by llampc_exchange_device straight
-        # on the tick's stream, over the communicator of a group of its own — no c10d stream
-        # hand-off, ~1 us of host time per tick.  LLAMPC_C10D_EXCHANGE=1 keeps the c10d call.
+        # native exchange: the all-gather is issued by llampc_exchange_rccl straight on the
+        # tick's stream over the library's own RCCL communicator — no c10d stream hand-off,
+        # ~1 us of host time per tick.  LLAMPC_C10D_EXCHANGE=1 keeps the c10d call.
         self._comm = None
         self._mailbox = None
         self.transport = None
@@ -176,7 +164,7 @@ class ShardedBank:
             mode = exchange_mode()
             if mode in ("auto", "peer"):
                 self._setup_peer_exchange(dev, required=mode == "peer")
-            if self._mailbox is None and self.backend == "nccl" and mode in ("auto", "rccl"):
+            if self._mailbox is None and ((self.backend == "nccl" and mode == "auto") or mode == "rccl"):
                 self._setup_native_exchange(dev)
             self.transport = self._decide_transport()
 
@@ -239,23 +227,57 @@ class ShardedBank:
         self._mailbox = mb
 
     def _setup_native_exchange(self, dev):
+        """The library's RCCL communicator (llampc_comm_*, rccl.h): every rank checks that RCCL
+        loads and makes an id, rank 0's id is shared through the process group (any backend),
+        then every rank joins (ncclCommInitRank).  Each step is decided collectively, so no rank
+        waits in an init the others never enter; on failure all keep the c10d / host gather."""
         import sys
+        lib = nat.load()
+        err, uid = None, b""
+        try:
+            buf = (C.c_ubyte * 128)()
+            nat.check(lib.llampc_comm_unique_id(buf))
+            uid = bytes(buf)
+        except Exception as e:                     # noqa: BLE001 — decided collectively below
+            err = e
+        ok = all(_all_gather_obj(err is None, self.group))
+        comm = C.c_void_p()
+        if ok:
+            uids = _all_gather_obj(uid if self.rank == 0 else b"", self.group)
+            try:
+                nat.check(lib.llampc_comm_create((C.c_ubyte * 128).from_buffer_copy(uids[0]), self.world, self.rank,
+                                                 self.device, C.byref(comm)))
+            except Exception as e:                 # noqa: BLE001
+                err = e
+            ok = all(_all_gather_obj(err is None, self.group))
+        if not ok:
+            if comm.value:
+                lib.llampc_comm_destroy(comm)
+            msg = f"{err or 'failed on another rank'}"
+            print(f"llampc: native RCCL exchange unavailable ({msg}); using the c10d / host gather", file=sys.stderr)
+            self.fallback_reason = ((self.fallback_reason + "; ") if self.fallback_reason else "") + f"rccl: {msg}"
+            return
+        self._comm = comm
+
+    @property
+    def comm(self):
+        """This rank's RCCL communicator (llampc_comm*) when the exchange uses it, else None."""
+        return self._comm
+
+    def gather_words(self, words: np.ndarray) -> np.ndarray:
+        """All-gather a fixed-size uint64 record of every rank, in rank order, over the process
+        group: the host-carried transport of the sharded controller (llampc_ctl_resume)."""
         import torch
         import torch.distributed as dist
-        xg = dist.new_group(backend="nccl")        # collective: every rank builds its shard
-        # one c10d collective creates the group's communicator before its raw use
-        dist.all_gather_into_tensor(self.d_all, self.d_local, group=xg)
-        torch.cuda.synchronize(dev)
-        try:
-            comm = xg._get_backend(dev)._comm_ptr()
-            fn = _rccl_allgather_addr()
-        except Exception as e:                     # transport only: results are the same
-            print(f"llampc: native exchange unavailable ({e}); using the c10d all-gather",
-                  file=sys.stderr)
-            self.fallback_reason = ((self.fallback_reason + "; ") if self.fallback_reason else "") + f"rccl: {e}"
-            return
-        if comm:
-            self._xgroup, self._comm, self._allgather = xg, comm, fn
+        t = torch.from_numpy(np.ascontiguousarray(words, dtype=np.uint64).view(np.int64))
+        if self.backend == "nccl":
+            d = t.to(self.d_local.device)
+            out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=d.device)
+            dist.all_gather_into_tensor(out, d, group=self.group)
+            return out.cpu().numpy().view(np.uint64)
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t, group=self.group)
+        return torch.cat(parts).numpy().view(np.uint64)
 
     def stage(self, x_prev, u_prev, x_now, U, xref, uprev) -> dict:
         """Upload one tick's inputs into a device pack (kept resident by the caller)."""
@@ -325,9 +347,8 @@ class ShardedBank:
             exchange_events[1].record(s)
             return s
         if self._comm is not None:           # native: all-gather + merge on stream s
-            nat.check(lib.llampc_exchange_device(self.d_local.data_ptr(), self.d_all.data_ptr(), self.world,
-                                                 self.d_merged.data_ptr(), pin.nan_policy, self._comm,
-                                                 self._allgather, self.device, s.cuda_stream))
+            nat.check(lib.llampc_exchange_rccl(self._comm, self.d_local.data_ptr(), self.d_all.data_ptr(),
+                                               self.d_merged.data_ptr(), pin.nan_policy, s.cuda_stream))
         elif self.exchange:
             import torch.distributed as dist
             if self.backend == "nccl":
@@ -359,6 +380,10 @@ class ShardedBank:
         if self._mailbox is not None:        # after this rank's last exchange (it synchronises)
             nat.load().llampc_mailbox_destroy(self._mailbox)
             self._mailbox = None
+        if self._comm is not None:
+            self.stream.synchronize()
+            nat.load().llampc_comm_destroy(self._comm)
+            self._comm = None
         self.bank.close()
 
     def fetch(self, stream=None, U=None) -> PlanResult:

@@ -6,7 +6,7 @@ Reference: llampc/tracks/track.py:12-160 (``Track``) and llampc/tracks/ethz.py:1
 ethz.py:20-42) and the optimal racelines with their per-friction speed profiles
 (``ethz_raceline_long_.npz``, ``ethz_raceline_.npz``, ``ethzMobil_raceline_long_.npz``,
 ethz.py:73-95) — is repacked, as data only, into ``tracks/data/tracks.npz`` by
-tests/golden/gen_golden.py; ``ETHZTrack.load_txt`` reads the reference's txt format directly.
+the test tree's golden generator (gen_golden.py); ``ETHZTrack.load_txt`` reads the reference's txt format directly.
 
 Constructor semantics follow ethz.py:106-138: ``reference='center'`` (the reference's
 default) fits the raceline spline to the centre line and carries no speed profiles
@@ -21,6 +21,16 @@ import numpy as np
 from llampc.utils import Spline, Spline2D, project_segments
 
 _DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "tracks.npz")
+_DYN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "dyn_slice.npz")
+
+
+def dyn_slice() -> dict:
+    """The recorded ETHZ closed-loop slice (the reference's
+    llampc/data/DYN-GPMPC-NOCONS-with_var_speedsETHZ.npz, states[:6, 470:621] and
+    inputs[:, 470:620], repacked as data by the test tree's gen_golden.py): ``states`` [6, 151],
+    ``inputs`` [2, 150], ``first_index``.  The config-2 scenario's controls and start state."""
+    with np.load(_DYN) as d:
+        return {k: d[k] for k in d.files}
 
 
 class Track:

@@ -151,6 +151,9 @@ def main():
     inputs = np.asarray(dyn["inputs"], dtype=np.float64)
     lo, hi = 470, 620
     save("dyn_slice.npz", states=states[:, lo:hi + 1], inputs=inputs[:, lo:hi], first_index=np.array(lo))
+    # the same bytes as package data: the scenario generator and the bench read it from there
+    import shutil
+    shutil.copyfile(os.path.join(HERE, "dyn_slice.npz"), os.path.join(dpath, "dyn_slice.npz"))
     config1(states, inputs, 0)
 
     # ---------------- bank generation: rt.py loop vs randn(N,6) ----------------

@@ -329,9 +329,16 @@ def test_ctl_prelaunch_equals_launched(nat, monkeypatch, spec):
 
 def test_ctl_prelaunch_two_tracks_and_plan_between(nat):
     """Two armed controllers ticked concurrently (config 5's shape) equal two launched ones, and
-    a plan() call on a third bank between ticks leaves them alone; after the loop a plan() on an
-    armed controller's own bank (which cancels its armed launch) returns normally."""
+    a plan() call on a third bank and a setupNLP.solve (its own bank) between ticks leave them
+    alone — and are not held behind the armed launches: each returns in milliseconds, not at the
+    armed launches' 2 s expiry (an armed launch gets a hardware queue of its own).
+    After the loop a plan() on an armed controller's own bank (which cancels its armed launch)
+    returns normally."""
+    import time
+    from llampc.models import Dynamic
     from llampc.mpc import DeviceController, ModelBank, generate_bank
+    from llampc.mpc.nmpc import setupNLP
+    from llampc.mpc.planner import ConstantSpeed
     from llampc.params import ORCA
     nominal = [ORCA()[k] for k in ("Bf", "Cf", "Df", "Br", "Cr", "Dr")]
     setups = []
@@ -341,14 +348,19 @@ def test_ctl_prelaunch_two_tracks_and_plan_between(nat):
     d = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))
     s, u = d["states"], d["inputs"]
 
+    p = ORCA(control="pwm")
+    tr0 = setups[0][1]
+    xref0, _, _ = ConstantSpeed(s[:2, 10], s[3, 10], tr0, 20, TS, 0)
+
     def run(armed):
         banks = [ModelBank(q, W=5, device=0) for q, _, _ in setups]
         other = ModelBank(generate_bank(500, seed=9), W=5, device=0)
+        nlp = setupNLP(20, TS, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, Dynamic(**p, device=0), tr0, device=0)
         ctls = [DeviceController(bk, tr, H=40, C=64, K=10, nominal6=nominal, prelaunch=armed)
                 for bk, (_, tr, _) in zip(banks, setups)]
         xs = [x.copy() for _, _, x in setups]
         plant = O.Vehicle.from_params(O.orca_params())
-        recs = []
+        recs, between = [], []
         try:
             assert all(np.isnan(c.device_us()) for c in ctls)      # no tick yet
             for t in range(10):
@@ -358,7 +370,11 @@ def test_ctl_prelaunch_two_tracks_and_plan_between(nat):
                 # llampc_ctl_device_us: x_t on the device -> the record issued, by the GPU clock
                 dev = [c.device_us() for c in ctls]
                 assert all(np.isfinite(v) and 1.0 < v < 2000.0 for v in dev), dev
+                t0 = time.perf_counter()
                 other.plan_raw(s[:, t], u[:, t], s[:, t + 1], np.tile(u[:, t], (20, 1))[None], s[:2, :21], u[:, t])
+                t1 = time.perf_counter()
+                nlp.solve(s[:, 10], xref0, u[:, 9])
+                between.append((t1 - t0, time.perf_counter() - t1))
                 for i, o in enumerate(outs):
                     recs.append(_ctl_words(o, 40))
                     xn, _ = O.sim_continuous(plant, xs[i], np.array(o.u_seq[0][:]).reshape(2, 1), [0, TS])
@@ -367,8 +383,12 @@ def test_ctl_prelaunch_two_tracks_and_plan_between(nat):
         finally:
             for c in ctls:
                 c.close()
+            nlp.close()
             for bk in banks + [other]:
                 bk.close()
+        # after the first (code loading): a plan and a solve take well under 50 ms
+        worst = np.max(np.array(between[1:]), axis=0)
+        assert worst[0] < 0.05 and worst[1] < 0.05, (armed, worst)
         return recs
 
     for a, c in zip(run(False), run(True)):

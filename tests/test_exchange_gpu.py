@@ -3,7 +3,7 @@ forced on (LLAMPC_FORCE_EXCHANGE=1), so each tick runs plan -> all-gather -> mer
 exactly as a rank of the 8-GPU job does.  Every tick's merged record must equal the plain
 single-bank tick on the same inputs, for each transport: the peer mailbox (llampc_exchange_peer:
 push over IPC-mapped memory, poll, merge — one kernel), RCCL issued natively
-(llampc_exchange_device on the tick's stream) and c10d.
+(llampc_exchange_rccl over the library's RCCL communicator, on the tick's stream) and c10d.
 No per-tick synchronisation: the stream order alone must make the records right."""
 import os
 import tempfile

@@ -442,52 +442,40 @@ def test_bench_spawn_ranks_environment_and_failure():
 
 
 def test_native_exchange_fallback_reported(monkeypatch):
-    """The RCCL path's private pieces fail (ProcessGroupNCCL._comm_ptr() missing, or no RCCL in
-    /proc/self/maps): ShardedBank keeps the c10d all-gather, reports transport 'c10d' and says
-    why in transport_fallback (the bench line carries both)."""
-    import torch
-    import torch.distributed as dist
-    from llampc import _native as nat
+    """The library's RCCL communicator (llampc_comm_*) cannot be made — here: no HIP device, so
+    ncclGetUniqueId fails — ShardedBank keeps the c10d / host gather, reports the transport and
+    says why in transport_fallback (the bench line carries both); with a communicator it takes
+    'rccl'.  Every step is decided over the ranks (here a one-rank stand-in group)."""
     from llampc.mpc import sharded
 
-    class Backend:                                 # a backend without _comm_ptr
-        pass
-
-    class Group:
-        def _get_backend(self, dev):
-            return Backend()
-
-    monkeypatch.setattr(dist, "new_group", lambda **kw: Group())
-    monkeypatch.setattr(dist, "all_gather_into_tensor", lambda *a, **kw: None)
-    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **kw: None)
+    monkeypatch.setattr(sharded, "_all_gather_obj", lambda obj, group=None: [obj])
 
     def fresh(fallback=None):
         sb = sharded.ShardedBank.__new__(sharded.ShardedBank)
         sb._mailbox, sb._comm, sb.backend = None, None, "nccl"
+        sb.rank, sb.world, sb.device, sb.group = 0, 1, 0, None
         sb.fallback_reason = fallback
-        sb.d_all = sb.d_local = None
         return sb
 
     sb = fresh("peer: IPC unavailable")
-    sb._setup_native_exchange("cpu")
+    sb._setup_native_exchange("cpu")           # the real library: RCCL loads, no device for its id
     assert sb._comm is None and sb._decide_transport() == "c10d"
-    assert sb.fallback_reason.startswith("peer: IPC unavailable; rccl: ") and "_comm_ptr" in sb.fallback_reason
+    assert sb.fallback_reason.startswith("peer: IPC unavailable; rccl: llampc error")
 
-    class Backend2:
-        def _comm_ptr(self):
-            return 1234
+    class Lib:                                 # a library whose RCCL works
+        def llampc_comm_unique_id(self, buf):
+            buf[0] = 7
+            return 0
 
-    Group._get_backend = lambda self, dev: Backend2()
-    monkeypatch.setattr(sharded, "_rccl_allgather_addr",
-                        lambda: (_ for _ in ()).throw(nat.NativeError("no RCCL library loaded in this process")))
+        def llampc_comm_create(self, uid, world, rank, dev, out):
+            assert bytes(uid)[0] == 7 and (world, rank, dev) == (1, 0, 0)
+            out._obj.value = 1234
+            return 0
+
+    monkeypatch.setattr(sharded.nat, "load", lambda: Lib())
     sb = fresh()
     sb._setup_native_exchange("cpu")
-    assert sb._decide_transport() == "c10d" and sb.fallback_reason == "rccl: no RCCL library loaded in this process"
-    # both present: the native path, nothing to report
-    monkeypatch.setattr(sharded, "_rccl_allgather_addr", lambda: 99)
-    sb = fresh()
-    sb._setup_native_exchange("cpu")
-    assert sb._decide_transport() == "rccl" and sb.fallback_reason is None and sb._allgather == 99
+    assert sb._decide_transport() == "rccl" and sb.fallback_reason is None and sb.comm.value == 1234
     sb.backend = "gloo"
     sb._comm = None
     assert sb._decide_transport() == "host"
@@ -530,3 +518,30 @@ def test_controller_oracle_restatement():
         u = o["u_seq"][:, 0].copy()
         xn, _ = O.sim_continuous(plant, x, u.reshape(2, 1), [0, 0.02])
         x = xn[:, -1]
+
+
+def test_controller_guard_marks_only_device_failures():
+    """LLAMPC._guarded: a tick the library refused before launching anything (an
+    argument or state error) leaves the host mirror and the controller usable; a tick that failed
+    on the device (LLAMPC_E_DEVICE: a wait that expired or timed out; a record with a status)
+    consumed its step — t advances and the controller refuses further ticks."""
+    from llampc import _native as nat
+    from llampc.mpc.controller import LLAMPC
+    ctl = LLAMPC.__new__(LLAMPC)
+    ctl.failed, ctl.t = None, 5
+
+    def boom(code):
+        def f():
+            raise nat.NativeError("x", code)
+        return f
+
+    for code in (nat.E_ARG, nat.E_STATE):
+        with pytest.raises(nat.NativeError):
+            ctl._guarded(boom(code))
+        assert (ctl.failed, ctl.t) == (None, 5)
+    ctl._usable()
+    with pytest.raises(nat.NativeError):
+        ctl._guarded(boom(nat.E_DEVICE))
+    assert (ctl.failed, ctl.t) == (5, 6)
+    with pytest.raises(nat.NativeError, match="unusable"):
+        ctl._usable()

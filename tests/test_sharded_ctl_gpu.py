@@ -1,8 +1,15 @@
-"""The sharded controller (llampc_ctl_set_exchange; BASELINE config 5's real loop across GPUs):
-world 2, 3 and 8 ranks — self-spawned processes sharing cuda:0, each ticking LLAMPC (device mode)
-on its contiguous shard with the per-tick exchange inside the tick's launch (push of the shard's
-top-K and argmin into every peer's IPC-mapped mailbox, poll, merge, the merged selection's
-K + 1 models rolled out by every rank from the replicated global table).  In closed loop with
+"""The sharded controller (BASELINE config 5's real loop across GPUs): world 2, 3 and 8 ranks —
+self-spawned processes sharing cuda:0, each ticking LLAMPC (device mode) on its contiguous shard
+with the per-tick exchange, over each transport the ShardedBank can take:
+  peer  llampc_ctl_set_exchange: inside the tick's launch (push of the shard's top-K and argmin
+        into every peer's IPC-mapped mailbox, poll, merge);
+  host  llampc_ctl_set_gather without a communicator: two launches, the records carried by the
+        process group (gloo) between them (llampc_ctl_shard_record / llampc_ctl_resume);
+  rccl  llampc_ctl_set_gather with the library's RCCL communicator: ncclAllGather between the two
+        launches on the bank's stream — at world 1 (RCCL refuses two ranks on one device, and
+        this box has one; the merge of several records is the host transport's, same kernel).
+Every rank rolls out the merged selection's K + 1 models from the replicated global table.  In
+closed loop with
 the RK6 plant (the oracle's, on the host: every rank applies the same control), every rank's
 llampc_ctl_out record must equal the UNSHARDED controller's, bitwise, tick after tick —
 through the warm-up (no exchange), the first full window and the ticks after it.  One case has
@@ -55,9 +62,11 @@ def C_OUT_BYTES(nat):
     return ctypes.sizeof(nat.CtlOut)
 
 
-def _worker(rank, world, store, q, n, case):
+def _worker(rank, world, store, q, n, case, transport):
     try:
-        os.environ["LLAMPC_EXCHANGE"] = "peer"
+        os.environ["LLAMPC_EXCHANGE"] = transport
+        if world == 1:
+            os.environ["LLAMPC_FORCE_EXCHANGE"] = "1"     # the exchange path on a one-rank group
         for pth in (REPO, PKG_ROOT):
             if pth not in sys.path:
                 sys.path.insert(0, pth)
@@ -70,8 +79,9 @@ def _worker(rank, world, store, q, n, case):
         dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=60))
         sb = ShardedBank(_bank(n, case), rank, world, 0, W=W)
-        assert sb.transport == "peer", (sb.transport, sb.fallback_reason)
+        assert sb.exchange and sb.transport == transport, (sb.transport, sb.fallback_reason)
         ctl = LLAMPC(sb, ETHZ('optimal', True), H=H, C=C, K=K, mode="device")
+        assert ctl._ctl.transport == transport
         recs = _loop(ctl, golden("dyn_slice.npz")["states"][:, 0], T)
         ctl.close()
         dist.barrier()
@@ -83,12 +93,13 @@ def _worker(rank, world, store, q, n, case):
         q.put((rank, None, traceback.format_exc()))
 
 
-def _run_ranks(world, n, case):
+def _run_ranks(world, n, case, transport="peer"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     tmp = tempfile.mkdtemp(prefix="llampc_rdzv_")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, os.path.join(tmp, "store"), q, n, case)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, os.path.join(tmp, "store"), q, n, case, transport))
+             for r in range(world)]
     for p in procs:
         p.start()
     got, errs = {}, []
@@ -111,16 +122,19 @@ def _run_ranks(world, n, case):
     return got
 
 
-@pytest.mark.parametrize("world,n,case", [(2, 4000, "plain"), (3, 4001, "plain"), (8, 8000, "plain"),
-                                          (3, 3001, "nan")])
-def test_sharded_controller_equals_unsharded(world, n, case):
+@pytest.mark.parametrize("world,n,case,transport", [(2, 4000, "plain", "peer"), (3, 4001, "plain", "peer"),
+                                                    (8, 8000, "plain", "peer"), (3, 3001, "nan", "peer"),
+                                                    (2, 4000, "plain", "host"), (3, 4001, "plain", "host"),
+                                                    (3, 3001, "nan", "host"),
+                                                    (1, 4000, "plain", "rccl"), (1, 3001, "nan", "rccl")])
+def test_sharded_controller_equals_unsharded(world, n, case, transport):
     from llampc import _native as nat
     from llampc.mpc import LLAMPC, ModelBank
     from llampc.tracks import ETHZ
     nat.load()
     if nat.device_count() < 1:
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X")
-    got = _run_ranks(world, n, case)
+    got = _run_ranks(world, n, case, transport)
     with ModelBank(_bank(n, case), W=W, device=0) as b, LLAMPC(b, ETHZ('optimal', True), H=H, C=C, K=K) as ctl:
         ref = _loop(ctl, golden("dyn_slice.npz")["states"][:, 0], T)
     dt = np.dtype(nat.CtlOut)

@@ -150,17 +150,20 @@ def test_sharded_tick_equals_unsharded_on_gpu(world, transport, C):
                     assert A[k] == B[k] or (A[k] != A[k] and B[k] != B[k]), (rank, t, k, A[k], B[k])
 
 
-def test_bench_spawns_its_own_ranks():
+@pytest.mark.parametrize("exchange", ["peer", "host"])
+def test_bench_spawns_its_own_ranks(exchange):
     """`python bench.py --gpus 2` with no launcher (no RANK in the environment) starts its two
     rank processes itself (the parent never touches the GPU) and rank 0 prints ONE JSON line
     for the whole job — rehearsed on one GPU (LLAMPC_SAME_DEVICE=1, gloo for the host-side
-    collectives; the records travel through the peer mailboxes) — extras included: C = 64
-    ticks and BASELINE config 5 (two tracks) sharded over both ranks."""
+    collectives; the records travel through the peer mailboxes, or with LLAMPC_EXCHANGE=host
+    through the process group: the transport a node without peer access falls back to) —
+    extras included: C = 64 ticks, BASELINE config 5 (two tracks) sharded over both ranks and
+    the sharded controller."""
     import json
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
                                                               "MASTER_ADDR", "MASTER_PORT")}
-    env.update(LLAMPC_DIST_BACKEND="gloo", LLAMPC_SAME_DEVICE="1")
+    env.update(LLAMPC_DIST_BACKEND="gloo", LLAMPC_SAME_DEVICE="1", LLAMPC_EXCHANGE=exchange)
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "40",
                         "--warmup", "5", "--ticks", "4", "--n-per-gpu", "2000",
                         "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=300)
@@ -169,12 +172,12 @@ def test_bench_spawns_its_own_ranks():
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["N_models_total"] == 4000
-    assert rec["config"]["transport"] == "peer" and rec["config"]["transport_fallback"] is None
+    assert rec["config"]["transport"] == exchange and rec["config"]["transport_fallback"] is None
     assert rec["value"] > 0 and rec["plan_call_us"]["p50"] > 0
     # the extras run on every rank: C = 64 ticks and BASELINE config 5 sharded over the ranks
     assert rec["C64"]["ms_per_step"] > 0
     c5 = rec["config5"]
-    assert c5["N_per_track"] == 4000 and c5["transport"] == ["peer", "peer"] and c5["p99_us"] > 0
+    assert c5["N_per_track"] == 4000 and c5["transport"] == [exchange] * 2 and c5["p99_us"] > 0
     # the sharded controller (config 5's real loop): both tracks' controllers over both ranks
     ct = rec["controller_tick_us"]
-    assert ct["N_per_track"] == 4000 and ct["transport"] == ["peer", "peer"] and 0 < ct["p50"] <= ct["p99"]
+    assert ct["N_per_track"] == 4000 and ct["transport"] == [exchange] * 2 and 0 < ct["p50"] <= ct["p99"]

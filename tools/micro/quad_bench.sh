@@ -1,5 +1,5 @@
 #!/bin/bash
-# Builds tools/micro/quad_bench in variants (diagnostic only): ROLL=1/2 and ablations.
+# Builds tools/micro/quad_bench in variants (diagnostic only): ROLL=1/2.
 set -e
 D=$(cd "$(dirname "$0")" && pwd)
 build() {  # name, flags
@@ -8,5 +8,3 @@ build() {  # name, flags
 }
 build full ""
 build roll2 "-DROLL=2"
-build nopoly "-DLLAMPC_ABL_NOPOLY"
-build nodiv "-DLLAMPC_ABL_NODIV"
