@@ -642,15 +642,19 @@ def controller_ticks_sharded(args, world, rank, dev_index, ticks=1000, warm=60, 
                 x = np.array([tr.x_init, tr.y_init, tr.psi_init, 1.0, 0.0, 0.0])
             setups.append([sb, ctl, plant, x])
         dist.barrier()
-        lat = []
-        nxt = time.perf_counter() + period
+        lat, devt = [], []
+        # every rank's step starts at the same instant (one x_t for the whole node, as from one
+        # sensor): the ranks pace to a common CLOCK_MONOTONIC epoch (one clock per host), so a
+        # step's latency holds no skew between the ranks' own timers
+        nxt = max_over_ranks(time.monotonic() + 0.005)
         for i in range(ticks + warm):
-            nxt = pace(nxt, period)
+            nxt = pace(nxt, period, time.monotonic)
             t0 = time.perf_counter()
             for s in setups:
                 s[1].tick_begin(s[3])
             res = [s[1].tick_end() for s in setups]
             lat.append(time.perf_counter() - t0)
+            devt.append([s[1].device_us() for s in setups])
             for s, r in zip(setups, res):
                 pl = s[2]
                 pl.Df -= pl.Df / 2600.
@@ -667,9 +671,16 @@ def controller_ticks_sharded(args, world, rank, dev_index, ticks=1000, warm=60, 
             s[0].close()
     q = pctl(np.array(lat[warm:]) * 1e6)
     p50, p99, mx = max_over_ranks(q["p50"]), max_over_ranks(q["p99"]), max_over_ranks(q["max"])
+    dv = np.array(devt[warm:], dtype=np.float64).ravel()
+    dv = dv[np.isfinite(dv)]
+    device_us = {"p50": max_over_ranks(float(np.percentile(dv, 50))), "p99": max_over_ranks(float(np.percentile(dv, 99))),
+                 "note": "llampc_ctl_device_us per tick and track (x_t on the device -> the record's stores issued, "
+                         "the exchange included), max over ranks"} if dv.size else None
     N, K = args.n_per_gpu, args.K
     steps_tick = N * world + (K + 1) * C * H
     return {"p50": p50, "p99": p99, "max": mx, "ticks": q["ticks"], "period_us": period * 1e6, "budget_us": 1000.0,
+            "device_us": device_us, "armed": [bool(s[1]._ctl.prelaunch) for s in setups],
+            "paced": "every rank to a common CLOCK_MONOTONIC epoch (the same step start on all ranks)",
             "met": p99 < 1000.0, "tracks": ["ETHZ", "ETHZMobil"], "N_per_track": N * world, "N_per_track_per_gpu": N,
             "H": H, "C": C, "K": K, "W": args.W, "sel_models": sel, "transport": transports,
             "rollout_steps_per_tick": steps_tick, "rollout_steps_per_s_at_p50": 2 * steps_tick / (p50 * 1e-6),
@@ -732,9 +743,9 @@ def concurrent_tracks_sharded(args, world, rank, dev_index, ticks=1000, warm=50)
                     "its own exchange on its own stream, device-resident inputs, both merged records read back"}
 
 
-def pace(nxt, period):
+def pace(nxt, period, clock=time.perf_counter):
     """Busy-wait to the next period boundary (the 1 kHz control loop); returns the next one."""
-    while time.perf_counter() < nxt:
+    while clock() < nxt:
         pass
     return nxt + period
 

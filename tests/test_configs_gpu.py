@@ -10,14 +10,15 @@
   config 3  ETHZMobil, N = 10^4, H = 40, the sudden-drop scenario's synthetic Mobil states
             (track start, seed 3), same checks
 Tolerances: one integration step 1e-9 (the look-back); rollout costs RTOL_ROLL = 1e-7, or for
-an ill-conditioned rollout KAPPA_ULP times its own one-ulp sensitivity in the oracle
-(conftest.assert_costs_close; DESIGN §4 has the measured errors per shape); indices exact."""
+an ill-conditioned rollout its core-error bound: the lean cores' measured errors propagated
+through the oracle's rollout (conftest.core_error_bound / assert_costs_close; DESIGN §4 has the
+measured errors per shape); indices exact."""
 import os
 
 import numpy as np
 import pytest
 
-from conftest import REPO, assert_costs_close, cost_sensitivity, golden
+from conftest import REPO, assert_costs_close, core_error_bound, golden
 from oracle import llampc_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -127,7 +128,7 @@ def test_config_scenario_ticks_vs_oracle(nat, track, H, seed):
             np.testing.assert_array_equal(res.topk, win.best_k)
             cref = O.mpc_cost(O.rollout_rk4(shared(), tuple(p), f["x_now"], f["U"], TS), f["U"], f["xref"],
                               f["uprev"], Q, R, P)
-            sens = lambda idx: cost_sensitivity(shared(), tuple(p[:, idx]), f["x_now"], f["U"], f["xref"],  # noqa: E731
+            sens = lambda idx: core_error_bound(shared(), tuple(p[:, idx]), f["x_now"], f["U"], f["xref"],  # noqa: E731
                                                 f["uprev"], Q, R, P)
             conditioned += assert_costs_close(res.costs.ravel(), cref, RTOL_ROLL, sens)
             assert_costs_close([res.cost], [cref[win.current]], RTOL_ROLL, lambda idx: sens(np.array([win.current])))

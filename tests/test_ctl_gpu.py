@@ -5,14 +5,15 @@ look-ahead of the selected and top-K models, mu-hat) tick by tick in closed loop
 plant, and the device ConstantSpeed against the reference's own planner vectors.
 Tolerances: candidates and indices exact; the reference trajectory 1e-10 (the device walks the
 banded-solve spline coefficients, the oracle the reference's dense solve); costs 1e-7, or for an
-ill-conditioned rollout KAPPA_ULP times its one-ulp sensitivity (conftest.assert_costs_close);
+ill-conditioned rollout its core-error bound — the lean cores' measured errors propagated
+through the oracle's rollout (conftest.core_error_bound / assert_costs_close);
 mu-hat 1e-12."""
 import os
 
 import numpy as np
 import pytest
 
-from conftest import REPO, assert_costs_close, cost_sensitivity, golden
+from conftest import REPO, assert_costs_close, core_error_bound, golden
 from oracle import llampc_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -137,9 +138,9 @@ def test_ctl_closed_loop_vs_oracle(nat, N, C, H, W, K, name, ticks, lap, seed):
             up = np.zeros(2) if orc.u_prev is None else orc.u_prev.copy()
             o = orc.tick(x)
 
-            def sens(models, cands, o=o, up=up, x=x):            # the pairs' one-ulp sensitivity
+            def sens(models, cands, o=o, up=up, x=x):            # the pairs' core-error bounds
                 cols = [orc.nominal.reshape(6, 1) if m is None else bank_p[:, [m]] for m in models]
-                return [cost_sensitivity(shared(), tuple(cl), x, o["U"][c:c + 1], o["xref"], up, Q, R, P)[0]
+                return [core_error_bound(shared(), tuple(cl), x, o["U"][c:c + 1], o["xref"], up, Q, R, P)[0]
                         for cl, c in zip(cols, cands)]
             xref, U = ctl.inputs()
             np.testing.assert_array_equal(U, o["U"], err_msg=f"tick {t}")

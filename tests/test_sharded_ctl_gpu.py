@@ -2,7 +2,9 @@
 self-spawned processes sharing cuda:0, each ticking LLAMPC (device mode) on its contiguous shard
 with the per-tick exchange, over each transport the ShardedBank can take:
   peer  llampc_ctl_set_exchange: inside the tick's launch (push of the shard's top-K and argmin
-        into every peer's IPC-mapped mailbox, poll, merge);
+        into every peer's IPC-mapped mailbox, poll, merge); launched, and armed ("peer-armed":
+        every rank's launch enqueued during the previous tick, rung with x_t, the exchange after
+        its doorbell — with rank 0 cancelling its arming for one tick mid-run);
   host  llampc_ctl_set_gather without a communicator: two launches, the records carried by the
         process group (gloo) between them (llampc_ctl_shard_record / llampc_ctl_resume);
   rccl  llampc_ctl_set_gather with the library's RCCL communicator: ncclAllGather between the two
@@ -38,14 +40,17 @@ def _bank(n, case):
     return p
 
 
-def _loop(ctl, x0, ticks):
-    """Closed loop: tick, apply u_seq[0] to the RK6 plant (friction dropping 1/260 per tick)."""
+def _loop(ctl, x0, ticks, before=None):
+    """Closed loop: tick, apply u_seq[0] to the RK6 plant (friction dropping 1/260 per tick);
+    before(t) runs ahead of tick t."""
     from oracle import llampc_oracle as O
     from llampc import _native as nat
     plant = O.Vehicle.from_params(O.orca_params())
     x = x0.copy()
     recs = []
-    for _ in range(ticks):
+    for t in range(ticks):
+        if before is not None:
+            before(t)
         r = ctl.tick(x)
         recs.append(np.frombuffer(bytes(r.raw), dtype=np.uint8).copy())
         u = np.array(r.raw.u_seq[0][:])
@@ -64,6 +69,8 @@ def C_OUT_BYTES(nat):
 
 def _worker(rank, world, store, q, n, case, transport):
     try:
+        armed = transport == "peer-armed"
+        transport = "peer" if armed else transport
         os.environ["LLAMPC_EXCHANGE"] = transport
         if world == 1:
             os.environ["LLAMPC_FORCE_EXCHANGE"] = "1"     # the exchange path on a one-rank group
@@ -80,9 +87,16 @@ def _worker(rank, world, store, q, n, case, transport):
                                 timeout=datetime.timedelta(seconds=60))
         sb = ShardedBank(_bank(n, case), rank, world, 0, W=W)
         assert sb.exchange and sb.transport == transport, (sb.transport, sb.fallback_reason)
-        ctl = LLAMPC(sb, ETHZ('optimal', True), H=H, C=C, K=K, mode="device")
-        assert ctl._ctl.transport == transport
-        recs = _loop(ctl, golden("dyn_slice.npz")["states"][:, 0], T)
+        ctl = LLAMPC(sb, ETHZ('optimal', True), H=H, C=C, K=K, mode="device", prelaunch=armed)
+        assert ctl._ctl.transport == transport and ctl._ctl.prelaunch == armed
+        before = None
+        if armed and rank == 0:            # a cancel mid-run on one rank only: its tick 8 launches
+            def before(t):                 # while the other ranks' armed launches are rung
+                if t == 8:
+                    ctl.set_prelaunch(False)
+                elif t == 9:
+                    ctl.set_prelaunch(True)
+        recs = _loop(ctl, golden("dyn_slice.npz")["states"][:, 0], T, before)
         ctl.close()
         dist.barrier()
         sb.close()
@@ -124,6 +138,10 @@ def _run_ranks(world, n, case, transport="peer"):
 
 @pytest.mark.parametrize("world,n,case,transport", [(2, 4000, "plain", "peer"), (3, 4001, "plain", "peer"),
                                                     (8, 8000, "plain", "peer"), (3, 3001, "nan", "peer"),
+                                                    (2, 4000, "plain", "peer-armed"),
+                                                    (3, 4001, "plain", "peer-armed"),
+                                                    (8, 8000, "plain", "peer-armed"),
+                                                    (3, 3001, "nan", "peer-armed"),
                                                     (2, 4000, "plain", "host"), (3, 4001, "plain", "host"),
                                                     (3, 3001, "nan", "host"),
                                                     (1, 4000, "plain", "rccl"), (1, 3001, "nan", "rccl")])
@@ -135,7 +153,9 @@ def test_sharded_controller_equals_unsharded(world, n, case, transport):
     if nat.device_count() < 1:
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X")
     got = _run_ranks(world, n, case, transport)
-    with ModelBank(_bank(n, case), W=W, device=0) as b, LLAMPC(b, ETHZ('optimal', True), H=H, C=C, K=K) as ctl:
+    # the unsharded controller, launched (prelaunch=False): armed ticks equal launched ones
+    with ModelBank(_bank(n, case), W=W, device=0) as b, \
+            LLAMPC(b, ETHZ('optimal', True), H=H, C=C, K=K, prelaunch=False) as ctl:
         ref = _loop(ctl, golden("dyn_slice.npz")["states"][:, 0], T)
     dt = np.dtype(nat.CtlOut)
     for rank in range(world):

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round 6 quick check: the given GPU tests, then (optional) the 2-rank one-device rehearsal bench
+# and the default bench line.
+# usage (gpurun): bash tools/gpu_r06_quick.sh gpurun_out/<tag> "<pytest args>" [g2] [bench]
+set -o pipefail
+OUT=${1:?out dir}
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export HIP_FORCE_DEV_KERNARG=1 TMPDIR=/tmp
+mkdir -p "$OUT"
+step() { echo "[$(date +%T)] $*"; }
+if [ -n "$2" ]; then
+  step "gpu tests: $2"
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $2 > "$OUT/tests.log" 2>&1
+  rc=$?
+  tail -4 "$OUT/tests.log"
+  [ $rc -eq 0 ] || { step "tests rc=$rc: stopping"; exit $rc; }
+fi
+shift 2
+for what in "$@"; do
+  case $what in
+    g2) step "bench 2 ranks, self-spawned, one device"
+        LLAMPC_DIST_BACKEND=gloo LLAMPC_SAME_DEVICE=1 timeout -k 10 300 python -u bench.py --gpus 2 --no-cpu-baseline \
+          > "$OUT/bench_g2.json" 2> "$OUT/bench_g2.err" || exit $? ;;
+    g2host) step "bench 2 ranks, host exchange"
+        LLAMPC_EXCHANGE=host LLAMPC_DIST_BACKEND=gloo LLAMPC_SAME_DEVICE=1 timeout -k 10 300 python -u bench.py --gpus 2 \
+          --no-cpu-baseline > "$OUT/bench_g2host.json" 2> "$OUT/bench_g2host.err" || exit $? ;;
+    bench) step "bench"
+        timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $? ;;
+    k20) step "driver's command"
+        timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench_k20.json" 2> "$OUT/bench_k20.err" || exit $? ;;
+  esac
+done
+step "done"
