@@ -633,7 +633,10 @@ def controller_ticks_sharded(args, world, rank, dev_index, ticks=1000, warm=60, 
     try:
         for seed, tr in ((0, ETHZ('optimal', True)), (1, ETHZMobil('optimal', True))):
             sb = ShardedBank(generate_bank(args.n_per_gpu * world, seed=seed), rank, world, dev_index, W=args.W)
-            sb.bank.set_concurrency(2)
+            # the controllers ticked together on this device: two tracks, times the ranks when a
+            # one-GPU rehearsal puts every rank on it (LLAMPC_SAME_DEVICE) — an armed launch's
+            # blocks must all be resident (llampc_bank_set_concurrency sizes its spec blocks)
+            sb.bank.set_concurrency(2 * (world if os.environ.get("LLAMPC_SAME_DEVICE") else 1))
             ctl = LLAMPC(sb, tr, H=H, C=C, K=args.K, mode="device")
             plant = Dynamic(**p, device=dev_index)
             if tr.name == "ETHZ":

@@ -644,7 +644,8 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
   if (bank_stream(device, b->dedicated, &b->stream) != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
   b->own_stream = true;
-  const int64_t lbl = (int64_t)lookback_blocks(n) * (kBlock / 64);   // look-back lists (waves)
+  // look-back lists (waves); 8 blocks more for the XCD-aligned layout (launch_plan)
+  const int64_t lbl = ((int64_t)lookback_blocks(n) + 8) * (kBlock / 64);
   const int64_t lab = n;                 // worst case: one model per block (wave-role, G=64)
   if ((rc = dev_alloc(&b->d_params, 6 * (size_t)n)) || (rc = dev_alloc(&b->d_ring, (size_t)W * n)) ||
       (rc = dev_alloc(&b->d_am_val, lbl)) || (rc = dev_alloc(&b->d_am_idx, lbl)) ||
@@ -1746,12 +1747,26 @@ static int ctl_prepare(llampc_ctl* c, const double* x_t, llampc_ctl::Prep& P) {
   {
     const llampc_cost& cq = k.cost;
     const bool diag = cq.Q[1] == 0.0 && cq.Q[2] == 0.0 && cq.P[1] == 0.0 && cq.P[2] == 0.0;
+    // sharded over the peer mailboxes: the ranks' lists are exchanged too (ctl.hip
+    // ctl_spec_exchange), in the slot after the selection record's words
+    // the armed footprint: every block of an armed launch holds a CU from the end of the tick
+    // before to its doorbell, and all launches of the banks ticked together
+    // (llampc_bank_set_concurrency) must be resident at once — the exchange's peers and the
+    // tick's own look-back wait on each other — so the spec blocks take what is left of the
+    // banks' share of the CUs (INTEGRATION.md "What armed launches cost")
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device) != hipSuccess || cus < 1) cus = 256;
+    const int room = cus / std::max(1, b->share) - (L.nb_lb + L.nb_la);
+    const int ns = (int)std::min<int64_t>(std::min<int64_t>(c->spec_cap, room), c->mb ? c->n_global : b->n);
+    const int spec_off = ctl_rec_words(k.K);
+    const bool px_fits = !c->mb || (L.px_G && spec_off + 4 * ns <= kRecWords);
     if (!x_t && !c->no_spec && !warm && full && R == 1 && L.s4 && lpm == 4 && L.cpl == 1 && L.G == k.C && diag &&
-        !c->mb && L.nb_lb <= c->spec_nb) {
+        !c->xg_world && px_fits && ns >= 4 && L.nb_lb <= c->spec_nb) {
       size_t poll_sp = 0;
-      const int ns = (int)std::min<int64_t>(c->spec_cap, b->n);
-      const size_t lds_sp = ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &poll_sp, true, 0, ns);
+      const size_t lds_sp = ctl_lds_bytes(k.H, k.C, b->rl_n, L.nb_lb, k.K, &poll_sp, true, L.px_G, ns);
       if (lds_sp <= 160 * 1024) {
+        L.px_spec_off = spec_off;
+        L.px_spec_wait = 20000;           // 200 us: the ranks arm within microseconds of each other
         L.n_spec = ns;
         L.spec_val = c->d_spec_val;
         L.spec_idx = c->d_spec_idx;
@@ -2219,8 +2234,9 @@ struct llampc_nlp {
   unsigned char* h_blk = nullptr;        // pinned mirror
   size_t blk_bytes = 0, in_bytes = 0;
   double* d_cost = nullptr;              // the sample blocks' sorted lists as tagged words
-                                         // [3][samples / 64 x len], then the round's rate-clipped
-                                         // sequences [samples][H][2] (NlpLaunch.list_tag, cand)
+                                         // [2][3][samples], then the rounds' rate-clipped
+                                         // sequences [2][samples][H][2] (NlpLaunch.list_tag, cand;
+                                         // by round parity)
   uint64_t* d_ms_tag = nullptr;          // [2][4 HMAX]: a round's mean / std (NlpLaunch.ms_tag)
   bool per_round = false;                // one launch per round (LLAMPC_NLP_ROUND_LAUNCHES=1: A/B)
   NlpResult* h_res = nullptr;            // pinned, coherent, mapped: the last round writes it
@@ -2274,18 +2290,18 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
     return code;
   };
   int rc;
-  // the lists: 3 words per entry, samples / 64 x len <= samples entries
-  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, (size_t)k.samples * (3 + 2 * (size_t)H))) ||
+  // the lists: 3 words per entry, samples / 64 x len <= samples entries; both by round parity
+  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, (size_t)k.samples * (6 + 4 * (size_t)H))) ||
       (rc = dev_alloc(&p->d_ms_tag, 8 * (size_t)LLAMPC_HMAX)))
     return cleanup(rc);
   {
-    // every round in one launch needs all samples / 64 + 1 blocks resident together (each waits
-    // for the others' rounds; one block per CU by its LDS request): not on a device, or a
-    // partition of one, with fewer CUs than blocks — then one launch per round
+    // every round in one launch needs all samples / 64 blocks resident together (each waits for
+    // the others' rounds; one block per CU by its LDS request): not on a device, or a partition
+    // of one, with fewer CUs than blocks — then one launch per round
     const char* e = std::getenv("LLAMPC_NLP_ROUND_LAUNCHES");
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device) != hipSuccess) cus = 0;
-    const bool resident = k.samples / 64 + 1 <= cus;
+    const bool resident = k.samples / 64 <= cus;
     p->per_round = !nlp_persistent(k.samples) || !resident || (e && e[0] == '1');
   }
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
@@ -2301,7 +2317,7 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
     return cleanup(fail(LLAMPC_E_HIP, "hipHostGetDevicePointer(NLP result) failed"));
   // tagged words start at tag 0, which no solve uses (nlp_seq of a solve number >= 1)
   if (hipMemcpy(p->d_blk, p->h_blk, p->blk_bytes, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(p->d_cost, 0, (size_t)k.samples * 3 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(p->d_cost, 0, (size_t)k.samples * 6 * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(p->d_ms_tag, 0, 8 * LLAMPC_HMAX * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "NLP solver upload failed"));
   *out = p;
@@ -2348,7 +2364,7 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.x0 = dx;
   a.xref = dx + 6;
   a.list_tag = reinterpret_cast<uint64_t*>(p->d_cost);
-  a.cand = p->d_cost + 3 * (size_t)k.samples;
+  a.cand = p->d_cost + 6 * (size_t)k.samples;
   a.res = p->d_res;
   a.host_tag = p->d_tag;
   a.host_seq = p->calls + 1;

@@ -202,6 +202,87 @@ __device__ __forceinline__ int ctl_door(const CtlLaunch& c, double* xl, int* res
 // ---- the speculative look-ahead (CtlLaunch.n_spec; ctl.hpp) --------------------------------
 // The n_spec best of the look-back blocks' sorted lists: a tree merge in LDS (the cross-shard
 // merge's), published as tagged words (local model index; kNoLocal: none).
+// Polls this rank's mailbox words own[g stride + w] (w < nw, every g != rank) until each carries
+// the tag seq — every thread issues all of its loads of a round before checking any (one memory
+// round trip per round; a load under a per-word condition waits its own) — into rec32[g nw + w].
+// Gives up after `bound` s_memrealtime ticks; returns this thread's late flag.
+template <int kPer>
+__device__ __forceinline__ int ctl_poll_words(const uint64_t* own, size_t stride, int G, int nw, int rank,
+                                              uint32_t seq, uint64_t bound, uint32_t* rec32) {
+  const int tid = threadIdx.x, total = G * nw;
+  uint64_t need = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int e = tid + j * kBlock;
+    if (e < total && e / nw != rank) need |= 1ull << j;
+  }
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (need) {
+    uint64_t v[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int e = ((need >> j) & 1) ? tid + j * kBlock : rank * nw;   // idle: own slot (never read back)
+      const int g = e / nw, w = e - g * nw;
+      v[j] = __hip_atomic_load(own + (size_t)g * stride + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (((need >> j) & 1) && tag_ok(v[j], seq)) {
+        rec32[tid + j * kBlock] = (uint32_t)v[j];
+        need &= ~(1ull << j);
+      }
+    }
+    if (!need) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > bound) return 1;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return 0;
+}
+
+// The sharded controller's speculative list (peer transport, armed ticks): this shard's n_spec
+// best by the window mean without x_t (value, GLOBAL index) as 4 n_spec tagged words pushed into
+// every peer's mailbox slot at px_spec_off (after the selection record's words; the same tick
+// number: the exchange of this tick, only earlier), the peers' lists polled, and the n_spec best
+// over the ranks published — global indices, which the spec blocks roll out from the replicated
+// global table.  All before the doorbell.  A peer whose list does not arrive within
+// px_spec_wait (a rank that launched this tick instead of arming it has none) leaves this rank
+// with its own list: the speculation only decides which models are rolled out early, never a
+// result, so the ranks' records stay equal whatever their lists.
+__device__ __forceinline__ void ctl_spec_exchange(const CtlLaunch& c, unsigned char* base, const Ent* top) {
+  const int tid = threadIdx.x, G = c.px_G, rank = c.px_rank, M = c.n_spec, nw = 4 * M;
+  uint32_t* rec32 = reinterpret_cast<uint32_t*>(base);                          // [G][nw]
+  Ent* g0 = reinterpret_cast<Ent*>(base + align16(4 * (size_t)G * nw));
+  Ent* g1 = g0 + (size_t)G * M;
+  const int64_t goff = c.fin.goff;
+  const size_t slot0 = (size_t)(c.px_seq & 1) * G * kRecWords;
+  const size_t mine = slot0 + (size_t)rank * kRecWords + c.px_spec_off;
+  for (int p = tid; p < G * nw; p += kBlock) {
+    const int g = p / nw, w = p - g * nw;
+    const Ent& x = top[w >> 2];
+    const uint64_t q = (w & 2) ? (uint64_t)(x.i == kNoIndex ? (int64_t)-1 : goff + x.i) : (uint64_t)__double_as_longlong(x.v);
+    const uint32_t word = (w & 1) ? (uint32_t)q : (uint32_t)(q >> 32);
+    if (g == rank) rec32[(size_t)rank * nw + w] = word;
+    else __hip_atomic_store(c.px_box[g] + mine + w, tag_word(c.px_seq, word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  constexpr int kPer = (kCtlPxMax * 4 * kCtlSpecMax + kBlock - 1) / kBlock;
+  const int late = __syncthreads_or(
+      ctl_poll_words<kPer>(c.px_box[rank] + slot0 + c.px_spec_off, kRecWords, G, nw, rank, c.px_seq, c.px_spec_wait, rec32));
+  const int Gm = late ? 1 : G;
+  for (int e = tid; e < Gm * M; e += kBlock) {
+    const int g = late ? rank : e / M, j = e - (late ? 0 : g) * M;
+    const uint32_t* r = rec32 + (size_t)g * nw + 4 * j;
+    const int64_t id = (int64_t)join_words(r[2], r[3]);
+    g0[e] = Ent{__longlong_as_double((long long)join_words(r[0], r[1])), id < 0 ? kNoIndex : id};
+  }
+  __syncthreads();
+  const Ent* gtop = tree_merge(g0, g1, Gm, M);
+  if (tid < M) {
+    const int64_t i = gtop[tid].i;
+    st_wt(&c.spec_tag[tid], tag_word(c.seq, i == kNoIndex ? kNoLocal : (uint32_t)i));
+  }
+}
+
+template <bool PX>
 __device__ __forceinline__ void ctl_spec_merge(const CtlLaunch& c, unsigned char* smem) {
   const int L = c.nb_lb, M = c.n_spec, tid = threadIdx.x;
   Ent* b0 = reinterpret_cast<Ent*>(smem + kScratchBytes);
@@ -209,6 +290,12 @@ __device__ __forceinline__ void ctl_spec_merge(const CtlLaunch& c, unsigned char
   for (int e = tid; e < L * M; e += kBlock) b0[e] = Ent{ld_wt(&c.spec_val[e]), ld_wt(&c.spec_idx[e])};
   __syncthreads();
   const Ent* top = tree_merge(b0, b1, L, M);
+  if constexpr (PX) {
+    if (c.px_G) {                       // launch-uniform: the lists of every rank
+      ctl_spec_exchange(c, smem + kScratchBytes + align16(2 * sizeof(Ent) * (size_t)L * M), top);
+      return;
+    }
+  }
   if (tid < M) {
     const int64_t i = top[tid].i;
     st_wt(&c.spec_tag[tid], tag_word(c.seq, i == kNoIndex ? kNoLocal : (uint32_t)i));
@@ -218,6 +305,7 @@ __device__ __forceinline__ void ctl_spec_merge(const CtlLaunch& c, unsigned char
 // A look-back block's part, before the doorbell: its models ranked by the window mean without
 // x_t (pred; NaN last, ties to the lower index — lb_final's order), the n_spec best stored
 // sorted; the last block (ticket 1, reset at once: every block has drawn) merges the lists.
+template <bool PX>
 __device__ __forceinline__ void ctl_spec_lists(const CtlLaunch& c, int blk, double pred, bool valid, int64_t n,
                                                unsigned char* smem, int* flag) {
   const int tid = threadIdx.x, M = c.n_spec;
@@ -237,7 +325,7 @@ __device__ __forceinline__ void ctl_spec_lists(const CtlLaunch& c, int blk, doub
   }
   if (!ticket_last(&c.tickets[1], (unsigned)c.nb_lb, flag)) return;
   if (tid == 0) __hip_atomic_store(&c.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ctl_spec_merge(c, smem);
+  ctl_spec_merge<PX>(c, smem);
 }
 
 // The deferred tracking cost (rollout<DEFER>): the split rollout's epilogue with the reference
@@ -609,38 +697,7 @@ __device__ __forceinline__ void ctl_exchange(const CtlLaunch& c, unsigned char* 
   constexpr int kPer = (kCtlPxMax * ctl_rec_words(LLAMPC_KMAX) + kBlock - 1) / kBlock;
   const uint64_t* own = gath ? c.px_gath : c.px_box[rank] + slot0;
   const size_t stride = gath ? (size_t)nw : (size_t)kRecWords;
-  const int total = G * nw;
-  uint64_t need = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int e = tid + j * kBlock;
-    if (e < total && e / nw != rank) need |= 1ull << j;
-  }
-  const uint64_t bound = (uint64_t)c.px_bound << 16;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  int late = 0;
-  while (need) {
-    uint64_t v[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int e = ((need >> j) & 1) ? tid + j * kBlock : rank * nw;   // idle: own slot (never read back)
-      const int g = e / nw, w = e - g * nw;
-      v[j] = __hip_atomic_load(own + (size_t)g * stride + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      if (((need >> j) & 1) && tag_ok(v[j], c.px_seq)) {
-        rec32[tid + j * kBlock] = (uint32_t)v[j];
-        need &= ~(1ull << j);
-      }
-    }
-    if (!need) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {
-      late = 1;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
+  int late = ctl_poll_words<kPer>(own, stride, G, nw, rank, c.px_seq, (uint64_t)c.px_bound << 16, rec32);
   const int wl = __any(late);
   if ((tid & 63) == 0) wlate[tid >> 6] = wl;
   __syncthreads();
@@ -1494,7 +1551,7 @@ __global__ __launch_bounds__(kBlock) void ctl_kernel(CtlLaunch arg) {
   double* xl = reinterpret_cast<double*>(pl + 3072);
   auto door = [&](double pred, bool pvalid, int64_t pn) -> const double* {
     // the speculative look-ahead's ranking first: it needs only the window (before x_t)
-    if (c.n_spec) ctl_spec_lists(c, blk, pred, pvalid, pn, smem, flag);
+    if (c.n_spec) ctl_spec_lists<PX>(c, blk, pred, pvalid, pn, smem, flag);
     if (c.door) {
       const int r = ctl_door(c, xl, reinterpret_cast<int*>(pl + 3584));
       if (r != (int)kCtlDoorFire) {     // cancelled or expired: nothing touched
@@ -1584,8 +1641,13 @@ size_t ctl_lds_bytes(int H, int C, int n, int nb_lb, int K, size_t* poll_off, bo
   const size_t px = px_G ? kScratchBytes + ctl_px_bytes(px_G, K) : 0;   // ctl_exchange's region
   // the speculative look-ahead: a spec block's layout, the look-back blocks' ranking and the
   // spec merge's two list buffers
+  // (sharded: then the ranks' lists, ctl_spec_exchange)
+  const size_t spec_px = px_G ? align16(2 * sizeof(Ent) * Lb * n_spec) + align16(16 * (size_t)px_G * n_spec) +
+                                    2 * sizeof(Ent) * (size_t)px_G * n_spec
+                              : 0;
   const size_t spec = n_spec ? std::max(spec_lds(H, C).end,
-                                        kScratchBytes + std::max<size_t>(12 * kBlock, 2 * sizeof(Ent) * Lb * n_spec))
+                                        kScratchBytes + std::max<size_t>(std::max<size_t>(12 * kBlock, 2 * sizeof(Ent) * Lb * n_spec),
+                                                                         spec_px))
                              : 0;
   size_t off = std::max(std::max(std::max(L.end, px), std::max(lbf, rank)), spec);
   off = align16(off);

@@ -348,6 +348,12 @@ struct CtlLaunch {
   int32_t px_phase;
   uint64_t* px_send;          // [nw] (phase 1 writes, phase 2 reads)
   const uint64_t* px_gath;    // [G][nw]
+  // armed ticks with the peer exchange and n_spec > 0: every rank's speculative list goes
+  // through the mailbox slot too, at word px_spec_off (after the selection record), before the
+  // doorbell; a peer's list that is not there after px_spec_wait s_memrealtime ticks is not
+  // waited for (ctl.hip ctl_spec_exchange)
+  int32_t px_spec_off;
+  uint32_t px_spec_wait;
   // armed launch (door != null, llampc_ctl_set_prelaunch): enqueued behind the previous tick,
   // it runs its x_t-independent prologue and then waits for the host's doorbell: kCtlDoorWords
   // tagged words (tag door_seq) in pinned memory — x_t as 12 32-bit halves, then the status

@@ -12,16 +12,21 @@
 //                   LDS), writing each sample's objective (+inf if infeasible).  Each block then
 //                   sorts its 64 (objective, index) keys in one wave (a bitonic network of
 //                   shuffle exchanges: NaN last, ties to the lower index) and publishes its best
-//                   len = next_pow2(E) sorted, as tagged words; then it draws the NEXT round's
-//                   Philox variates (they do not depend on the mean / std) while the completion
-//                   block works, and waits for the next mean / std (tagged words);
-//   the completion  (the last block of the grid, no samples) polls the lists, merges them
-//   block           pairwise up a tree — the lower len of two sorted lists is
-//                   min(a_i, b_(len-1-i)), bitonic, then one half-cleaner network in registers per
-//                   level — to the E best overall in order, reads the E elite sequences and
-//                   publishes the next mean / std as their mean / standard deviation (NumPy's
-//                   axis-0 order), keeping the best sequence seen so far.  (A bitonic sort of all
-//                   samples in LDS took 36 us of the 62 us round: 55 barrier-separated passes.)
+//                   len = next_pow2(E) sorted, as tagged words;
+//   every block     then completes the round itself (round 6; until then one completion block
+//                   did and handed the next mean / std back through tagged words, ~1.5 us a
+//                   round): it polls every block's list, merges them pairwise up a tree — the
+//                   lower len of two sorted lists is min(a_i, b_(len-1-i)), bitonic, then one
+//                   half-cleaner network in registers per level — to the E best overall in order,
+//                   reads the E elite sequences and sets the next mean / std as their mean /
+//                   standard deviation (NumPy's axis-0 order): every block computes the same
+//                   values in the same order, so all hold the same next distribution.  Block 0
+//                   keeps the state (the best sequence so far) and writes the result.  The
+//                   lists and the sequences are double-buffered by round parity: a block can be
+//                   a round ahead of another, never two.  The next round's Philox variates (they
+//                   do not depend on the mean / std) are drawn by the helper waves during the
+//                   rollouts.  (A bitonic sort of all samples in LDS took 36 us of the 62 us
+//                   round: 55 barrier-separated passes.)
 #include "plan_dev.hpp"
 #include "nlp.hpp"
 
@@ -181,8 +186,7 @@ __device__ __forceinline__ void nlp_traj_quad(const NlpLaunch& a, const double* 
 // xmpc (nmpc.py:58-60): the NLP's Euler trajectory of the best sequence over all rounds, by
 // one quad of the completing block (the sample blocks' fast rollout, the general re-run when
 // its domain check fails) — it was a separate one-lane launch of the general evaluation, 32 us.
-__device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, unsigned char* smem, double* ub, bool better,
-                                               double bj, int bit) {
+__device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, double* ub, bool better, double bj, int bit) {
   const int tid = threadIdx.x, H = a.H;
   const NlpState* st = a.st;
   NlpResult* res = a.res;
@@ -238,21 +242,36 @@ __device__ __forceinline__ void nlp_traj_quad(const NlpLaunch& a, const double* 
   }
 }
 
-// The completion block's LDS: the lists' keys kA | kB and indices iA | iB ([nl * len] each,
+// A round's lists and sequences, double-buffered by round parity (every block completes every
+// round, so a block may run one round ahead of another — never two: round r + 2's stores follow
+// the writer's completion of round r + 1, which needs every block's list of round r + 1, which
+// each block publishes only after it has read round r's buffers).
+__device__ __forceinline__ uint64_t* nlp_lists(const NlpLaunch& a, int it) {
+  return a.list_tag + (size_t)(it & 1) * 3 * (size_t)a.samples;
+}
+__device__ __forceinline__ double* nlp_cand(const NlpLaunch& a, int it) {
+  return a.cand + (size_t)(it & 1) * 2 * (size_t)a.samples * a.H;
+}
+
+// The completion's LDS (every block): the lists' keys kA | kB and indices iA | iB ([nl * len] each,
 // the merge tree's two buffers), then the elite sequences [E][H][2].
 struct NlpCompLds {
   uint64_t *kA, *kB;
   uint32_t *iA, *iB;
   double* eu;
 };
-__device__ __forceinline__ NlpCompLds nlp_comp_lds(unsigned char* smem, int nl, int len) {
+__device__ __forceinline__ NlpCompLds nlp_comp_lds(unsigned char* base, int nl, int len) {
   NlpCompLds L;
-  L.kA = reinterpret_cast<uint64_t*>(smem + kScratchBytes);
+  L.kA = reinterpret_cast<uint64_t*>(base);
   L.kB = L.kA + (size_t)nl * len;
   L.iA = reinterpret_cast<uint32_t*>(L.kB + (size_t)nl * len);
   L.iB = L.iA + (size_t)nl * len;
-  L.eu = reinterpret_cast<double*>(smem + kScratchBytes + 24 * (size_t)nl * len);
+  L.eu = reinterpret_cast<double*>(base + 24 * (size_t)nl * len);
   return L;
+}
+// its bytes: the lists, the elite rows, and the trajectory's reference and x0 after them
+__host__ __device__ __forceinline__ size_t nlp_comp_bytes(int H, int nl, int elite) {
+  return 24 * (size_t)nl * nlp_list_len(elite) + 16 * (size_t)elite * H + 16 * (size_t)(H + 1) + 48;
 }
 
 // Waits (bounded) for tagged words; returns the block's verdict (every thread the same).
@@ -265,14 +284,15 @@ __device__ __forceinline__ bool nlp_block_ok(int ok, int* rflag) {
 }
 
 // The completion block: every sample block's sorted list of the round (tag sq) into kA / iA.
-__device__ __forceinline__ bool nlp_poll_lists(const NlpLaunch& a, const NlpCompLds& L, int nl, uint32_t sq,
+__device__ __forceinline__ bool nlp_poll_lists(const NlpLaunch& a, const NlpCompLds& L, int nl, int it, uint32_t sq,
                                                int* rflag) {
   const int nbl = nl * nlp_list_len(a.elite);
+  const uint64_t* lt = nlp_lists(a, it);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   int ok = 1;
   for (int e = threadIdx.x; e < nbl && ok; e += (int)blockDim.x) {
     for (;;) {
-      const uint64_t hi = ld_wt(&a.list_tag[e]), lo = ld_wt(&a.list_tag[nbl + e]), ix = ld_wt(&a.list_tag[2 * nbl + e]);
+      const uint64_t hi = ld_wt(&lt[e]), lo = ld_wt(&lt[nbl + e]), ix = ld_wt(&lt[2 * nbl + e]);
       if ((int)tag_ok(hi, sq) & (int)tag_ok(lo, sq) & (int)tag_ok(ix, sq)) {
         L.kA[e] = join_words(hi, lo);
         L.iA[e] = (uint32_t)ix;
@@ -287,18 +307,20 @@ __device__ __forceinline__ bool nlp_poll_lists(const NlpLaunch& a, const NlpComp
   return nlp_block_ok(ok, rflag);
 }
 
-// Round `it`'s completion (the completion block, the lists in kA / iA): the elite, the next
-// mean / std (tagged words for the sample blocks, which may sit on other XCDs), the best so far.
+// Round `it`'s completion, run by every block (the lists in kA / iA): the elite, the next mean /
+// std into ms (this block's LDS: every block computes the same), the best so far.  Block 0 alone
+// writes the state and, on the solve's last round, the result; on a launch's last round it also
+// publishes the next mean / std as tagged words for the next launch (one launch per round).
 // bj / bit: the best objective so far and its round, carried in registers across the launch's
-// rounds (the state's copy, read back sc1 every round, put a memory round trip on each
-// round's critical path); stored to the state too, for the next launch.
-__device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* smem, int it, int nl, double& bjv,
-                                             int& bitv) {
+// rounds; stored to the state too, for the next launch.
+__device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* cbase, int it, int nl, double& bjv,
+                                             int& bitv, double* ms, bool last_of_launch) {
 #pragma clang fp contract(off)
   const int tid = threadIdx.x, H = a.H, E = a.elite;
   const int len = nlp_list_len(E);
+  const bool b0 = blockIdx.x == 0;
   NlpState* st = a.st;
-  const NlpCompLds L = nlp_comp_lds(smem, nl, len);
+  const NlpCompLds L = nlp_comp_lds(cbase, nl, len);
   uint64_t* kA = L.kA;
   uint64_t* kB = L.kB;
   uint32_t* iA = L.iA;
@@ -333,10 +355,11 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   }
   NLP_STAMP(5);
   const uint32_t* idx = iA;                                        // the E best, in order
-  // the elite sequences (the sample blocks' rate-clipped candidates)
+  // the elite sequences (the sample blocks' rate-clipped candidates of this round's buffer)
+  const double* cand = nlp_cand(a, it);
   for (int e = tid; e < E * H * 2; e += (int)blockDim.x) {
     const int r = e / (2 * H), q = e - r * 2 * H;
-    eu[e] = ld_wt(&a.cand[2 * (size_t)idx[r] * H + q]);
+    eu[e] = ld_wt(&cand[2 * (size_t)idx[r] * H + q]);
   }
   __syncthreads();
   NLP_STAMP(6);
@@ -344,6 +367,7 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   const double bj0 = bjv;
   const int bit0 = bitv;
   const bool better = c0 < bj0;                     // the best sequence so far (NaN never)
+  double* msn = ms;
   if (tid < 2 * H) {
     // mean / std over the elite in np.mean(axis=0) / np.std(axis=0)'s order: an axis-0
     // reduction adds the rows in sequence (checked against NumPy), std = sqrt(mean((x - m)^2))
@@ -377,29 +401,35 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
       const double d = at(e) - m;
       s += d * d;
     }
-    if (it + 1 < a.iters) {             // the next round's mean / std, tagged halves (low, high)
-      const uint32_t sq1 = nlp_seq(a.host_seq, it + 1);
-      const uint64_t mb = (uint64_t)__double_as_longlong(m);
-      const uint64_t sb = (uint64_t)__double_as_longlong(sqrt(s / E) + a.std_floor);
-      const int im = 2 * k + j, is = 2 * H + 2 * k + j;
-      st_wt(&a.ms_tag[2 * im], tag_word(sq1, (uint32_t)mb));
-      st_wt(&a.ms_tag[2 * im + 1], tag_word(sq1, (uint32_t)(mb >> 32)));
-      st_wt(&a.ms_tag[2 * is], tag_word(sq1, (uint32_t)sb));
-      st_wt(&a.ms_tag[2 * is + 1], tag_word(sq1, (uint32_t)(sb >> 32)));
+    const double sd = sqrt(s / E) + a.std_floor;
+    const int im = 2 * k + j, is = 2 * H + 2 * k + j;
+    if (it + 1 < a.iters) {             // the next round's mean / std
+      if (b0 && last_of_launch) {       // into the next launch: tagged halves (low, high)
+        const uint32_t sq1 = nlp_seq(a.host_seq, it + 1);
+        const uint64_t mb = (uint64_t)__double_as_longlong(m);
+        const uint64_t sb = (uint64_t)__double_as_longlong(sd);
+        st_wt(&a.ms_tag[2 * im], tag_word(sq1, (uint32_t)mb));
+        st_wt(&a.ms_tag[2 * im + 1], tag_word(sq1, (uint32_t)(mb >> 32)));
+        st_wt(&a.ms_tag[2 * is], tag_word(sq1, (uint32_t)sb));
+        st_wt(&a.ms_tag[2 * is + 1], tag_word(sq1, (uint32_t)(sb >> 32)));
+      }
     }
-    if (better) st_wt(&st->best_u[k][j], eu[2 * k + j]);
+    if (b0 && better) st_wt(&st->best_u[k][j], eu[2 * k + j]);
+    msn[im] = m;                        // this block's copy (ms is read again only after a barrier)
+    msn[is] = sd;
   }
   // the result (the last round): best objective and round, before this round's update
   const double bj = better ? c0 : bj0;
   const int bit = better ? it : bit0;
   bjv = bj;
   bitv = bit;
-  if (tid == 0 && better) {
+  if (b0 && tid == 0 && better) {
     st_wt(&st->best_j, c0);
     st_wt(&st->best_it, it);
   }
   NLP_STAMP(8);
-  if (it == a.iters - 1) nlp_trajectory(a, smem, eu, better, bj, bit);
+  if (b0 && it == a.iters - 1) nlp_trajectory(a, eu, better, bj, bit);
+  __syncthreads();                      // ms (the next round's) and the LDS lists (the next poll)
 }
 
 }  // namespace
@@ -413,10 +443,10 @@ constexpr int kNlpStageH = 28;
 // The round's Philox variates z of this block's samples into Ul (value (s H + k) 2 + j; the
 // pair (s H + k) shares one call): independent of the round's mean / std, so a block draws the
 // next round's while the completion block works.
-__device__ __forceinline__ void nlp_draw(const NlpLaunch& a, int blk, int it, double* Ul) {
+__device__ __forceinline__ void nlp_draw(const NlpLaunch& a, int blk, int it, double* Ul, int t0, int stride) {
   constexpr int kPerBlock = 64;
   const int H = a.H;
-  for (int e = threadIdx.x; e < kPerBlock * H; e += (int)blockDim.x) {
+  for (int e = t0; e < kPerBlock * H; e += stride) {
     const int rr = e / H, k = e - rr * H, s = blk * kPerBlock + rr;
     double z0, z1;
     nlp_z2((uint32_t)(s * H + k), a.call, a.seed, (uint32_t)(it + 1), z0, z1);
@@ -425,54 +455,52 @@ __device__ __forceinline__ void nlp_draw(const NlpLaunch& a, int blk, int it, do
   }
 }
 
+// The sample block's LDS after the scratch: xref [H+1][2] | Ul [64][H][2] | x0 [6] | keys [64] |
+// mean / std [2][H][2] | ST: the staged terms [H][64][kStageW] — the completion's region
+// (nlp_comp_bytes) reuses them once the rollouts are done — else the completion's region.
+__host__ __device__ __forceinline__ size_t nlp_su_off(int H) {
+  return kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 48 + 8 * 64 + 32 * (size_t)H;
+}
+
 // NT threads: the rollouts take the first 256 (a quad per sample); the other waves share the
-// sample blocks' per-round loops (bounds, staging, draws), two waves per SIMD
+// blocks' per-round loops (bounds, staging, the completion) and draw the next round's variates
+// while the rollouts run (ST), two waves per SIMD
 template <bool ST, int NT>
 __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int* rflag = reinterpret_cast<int*>(smem + kFlagOff);   // a bounded wait's block verdict
   const int tid = threadIdx.x, H = a.H, blk = (int)blockIdx.x;
-  const int nl = (int)gridDim.x - 1;    // sample blocks; block nl completes every round
-  if (blk == nl) {
-    const NlpCompLds L = nlp_comp_lds(smem, nl, nlp_list_len(a.elite));
-    // the best so far as the launch starts (host-staged, or an earlier launch's rounds): loaded
-    // while the first round's lists are awaited
-    double bjv = ld_wt(&a.st->best_j);
-    int bitv = ld_wt(&a.st->best_it);
-    for (int r = 0; r < a.rounds; ++r) {
-      const int it = a.it + r;
-      NLP_STAMP(7);
-      if (!nlp_poll_lists(a, L, nl, nlp_seq(a.host_seq, it), rflag)) return;
-      NLP_STAMP(4);
-      nlp_complete(a, smem, it, nl, bjv, bitv);
-    }
-    return;
-  }
+  const int nl = (int)gridDim.x;        // every block samples, every block completes every round
   constexpr int LPM = 4, kPerBlock = 64;             // 64 samples per block, a quad each
   double* sx = reinterpret_cast<double*>(smem + kScratchBytes);            // xref [H+1][2]
   double* Ul = sx + 2 * (H + 1);                                            // [64][H][2]
   double* x0 = Ul + 2 * (size_t)kPerBlock * H;                              // [6]
   uint64_t* ks = reinterpret_cast<uint64_t*>(x0 + 6);                       // [64] the samples' keys
   double* ms = reinterpret_cast<double*>(ks + 64);                          // the round's mean, std [2][H][2]
-  double* su = ms + 4 * (size_t)H;                                          // ST: [H][64][kStageW]
-  const NlpState* st = a.st;
+  double* su = reinterpret_cast<double*>(smem + nlp_su_off(H));             // ST: [H][64][kStageW]
+  unsigned char* cbase = smem + nlp_su_off(H);                              // the completion's region
+  NlpState* st = a.st;
   const int len = nlp_list_len(a.elite), nbl = nl * len;
   for (int e = tid; e <= H; e += NT) {   // the solve's inputs (this block's LDS only)
     sx[2 * e] = a.xref[e];
     sx[2 * e + 1] = a.xref[(H + 1) + e];
   }
   if (tid < 6) x0[tid] = a.x0[tid];
-  nlp_draw(a, blk, a.it, Ul);               // the first round's variates
+  nlp_draw(a, blk, a.it, Ul, tid, NT);      // the first round's variates
+  // the best so far as the launch starts (host-staged, or an earlier launch's rounds)
+  double bjv = ld_wt(&st->best_j);
+  int bitv = ld_wt(&st->best_it);
   for (int r = 0; r < a.rounds; ++r) {
     const int it = a.it + r;
     const uint32_t sq = nlp_seq(a.host_seq, it);
     NLP_STAMP(0);
-    // the round's mean / std: the host-staged state (round 0), else the previous round's
-    // completion's tagged halves
+    // the round's mean / std: the host-staged state (round 0), this block's completion of the
+    // previous round (in ms already), or — a launch's first round after round 0 — the previous
+    // launch's block 0's tagged halves
     if (it == 0) {
       for (int e = tid; e < 4 * H; e += NT)
         ms[e] = ld_wt(e < 2 * H ? &st->mean[0][0] + e : &st->std_[0][0] + (e - 2 * H));
-    } else {
+    } else if (r == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       int ok = 1;
       for (int i = tid; i < 4 * H && ok; i += NT) {
@@ -506,9 +534,10 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a) {
     }
     __syncthreads();
     NLP_STAMP(2);
-    // the rate-clipped sequences for the completion block's elite (each wave drains these
-    // stores before its list is published, below)
-    for (int e = tid; e < kPerBlock * H * 2; e += NT) st_wt(&a.cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
+    // the rate-clipped sequences for every block's elite read (each wave drains these stores
+    // before its list is published, below)
+    double* cand = nlp_cand(a, it);
+    for (int e = tid; e < kPerBlock * H * 2; e += NT) st_wt(&cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e]);
     const fm::FmK K = fm::FmK::load();
     if constexpr (ST) {
       const CostK& q0 = a.la.cost;
@@ -574,6 +603,9 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a) {
     }
     NLP_STAMP(3);
     if (sub == 0) ks[c] = nlp_key(J);
+    } else if (ST && r + 1 < a.rounds) {
+      // the helper waves: the next round's variates (Ul is dead: staged above, stored to cand)
+      nlp_draw(a, blk, it + 1, Ul, tid - kPerBlock * LPM, NT - kPerBlock * LPM);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's candidate stores (above)
     __syncthreads();
@@ -582,30 +614,33 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a) {
       uint32_t x = (uint32_t)(blk * kPerBlock + tid);
       nlp_sort64(k, x, tid);
       if (tid < len) {                  // the list as tagged words (nlp.hpp NlpLaunch.list_tag)
+        uint64_t* lt = nlp_lists(a, it);
         const int e = blk * len + tid;
-        st_wt(&a.list_tag[e], tag_word(sq, (uint32_t)(k >> 32)));
-        st_wt(&a.list_tag[nbl + e], tag_word(sq, (uint32_t)k));
-        st_wt(&a.list_tag[2 * nbl + e], tag_word(sq, x));
+        st_wt(&lt[e], tag_word(sq, (uint32_t)(k >> 32)));
+        st_wt(&lt[nbl + e], tag_word(sq, (uint32_t)k));
+        st_wt(&lt[2 * nbl + e], tag_word(sq, x));
       }
     }
-    // the next round's variates while the completion block works (Ul is dead: every wave's
-    // rollout ended before the barrier above)
-    if (r + 1 < a.rounds) nlp_draw(a, blk, it + 1, Ul);
+    // unstaged (H > kNlpStageH): the rollouts read Ul, so the next round's variates now
+    if (!ST && r + 1 < a.rounds) nlp_draw(a, blk, it + 1, Ul, tid, NT);
     NLP_STAMP(11);
+    // the round's completion, in every block
+    const NlpCompLds L = nlp_comp_lds(cbase, nl, len);
+    NLP_STAMP(7);
+    if (!nlp_poll_lists(a, L, nl, it, sq, rflag)) return;
+    NLP_STAMP(4);
+    nlp_complete(a, cbase, it, nl, bjv, bitv, ms, r + 1 == a.rounds);
   }
 }
 
 size_t nlp_lds_bytes(int H, int samples, int elite) {
-  const size_t blocks = kScratchBytes + 16 * (size_t)(H + 1) + 16 * 64 * (size_t)H + 48 + 8 * 64 + 32 * (size_t)H +
-                        (H <= kNlpStageH ? 8 * kStageW * 64 * (size_t)H : 0);
-  const size_t nll = (size_t)(samples / 64) * nlp_list_len(elite);
-  const size_t last = kScratchBytes + 24 * nll + 16 * (size_t)elite * H + 16 * (size_t)(H + 1) + 48;
-  return std::max(blocks, last);
+  const size_t su = H <= kNlpStageH ? 8 * kStageW * 64 * (size_t)H : 0;
+  return nlp_su_off(H) + std::max(su, nlp_comp_bytes(H, samples / 64, elite));
 }
 
 hipError_t launch_nlp(const NlpLaunch& a, hipStream_t s) {
   const size_t lds = std::max<size_t>(nlp_lds_bytes(a.H, a.samples, a.elite), 82 * 1024);
-  const dim3 grid(a.samples / 64 + 1);  // the sample blocks, then the completion block
+  const dim3 grid(a.samples / 64);      // the sample blocks (each completes every round)
   if (a.H <= kNlpStageH) {
     allow_lds(nlp_kernel<true, 2 * kBlock>);
     hipLaunchKernelGGL((nlp_kernel<true, 2 * kBlock>), grid, dim3(2 * kBlock), lds, s, a);

@@ -20,13 +20,13 @@ struct NlpState {
   int32_t pad;
 };
 
-// A launch of CEM rounds [it, it + rounds): samples / 64 sample blocks and ONE completion block
-// (the last in the grid).  Every round of the solve in one launch when the blocks are few
-// enough to be co-resident (nlp_persistent), else one launch per round.  Blocks hand a round
-// over by tagged words (tag nlp_seq(host_seq, round), so no drain, flag or ticket sits between
-// a store and its reader): each sample block's sorted list (list_tag) to the completion block,
-// the next round's mean / std (ms_tag) back to the sample blocks.  Scalars only (no arrays): the
-// kernel never takes the address of its argument (which would copy it to scratch).
+// A launch of CEM rounds [it, it + rounds): samples / 64 sample blocks, each of which also
+// completes every round (nlp.hip).  Every round of the solve in one launch when the blocks are
+// few enough to be co-resident (nlp_persistent), else one launch per round.  Blocks exchange a
+// round by tagged words (tag nlp_seq(host_seq, round), so no drain, flag or ticket sits between
+// a store and its reader): each block's sorted list (list_tag) to every block; across launches
+// the next round's mean / std (ms_tag, block 0).  Scalars only (no arrays): the kernel never
+// takes the address of its argument (which would copy it to scratch).
 // The solve's result as the last round's completion writes it into pinned host memory (then
 // a system-scope fence and the host tag): no D2H copy, no stream synchronisation.
 struct NlpResult {
@@ -43,14 +43,16 @@ struct NlpLaunch {
   const double* xref;            // [2][H+1] device
   uint64_t* top_key;             // [samples / 64][len] each sample block's best (sorted keys),
   uint32_t* top_idx;             //   then their sample indices (len = nlp_list_len(elite))
-  double* cand;                  // [samples][H][2] the round's sequences after the rate clip
+  double* cand;                  // [2][samples][H][2] the round's sequences after the rate clip
+                                 //   (by round parity: nlp.hip nlp_cand)
   NlpResult* res;                // the last round: the result, in pinned host memory (device alias)
   uint64_t* host_tag;            //   then this solve's number (host alias spun on by the caller)
   uint64_t host_seq;
-  uint64_t* list_tag;            // [3][samples / 64 x len]: each sample block's sorted list as
-                                 //   tagged words: key high halves, key low halves, sample indices
-  uint64_t* ms_tag;              // [2][4 H]: round r >= 1's mean [H][2] then std [H][2], each
-                                 //   double as tagged halves (low, high)
+  uint64_t* list_tag;            // [2][3][samples]: by round parity, each sample block's sorted
+                                 //   list (samples / 64 x len entries) as tagged words: key high
+                                 //   halves, key low halves, sample indices
+  uint64_t* ms_tag;              // [2][4 H]: the mean [H][2] then std [H][2] of a launch's first
+                                 //   round r >= 1, each double as tagged halves (low, high)
   uint64_t seed, call;           // Philox key; counter word 1 = the solve call number
   double up0, up1;               // uprev (du_0, nmpc.py:65-66)
   double umin0, umin1, umax0, umax1;
@@ -60,8 +62,8 @@ struct NlpLaunch {
   int32_t H, samples, elite, has_hold;
 };
 
-// every round in one launch: the sample blocks and the completion block (one per CU: the LDS
-// request) must all be resident at once, since each waits for the others' rounds
+// every round in one launch: the sample blocks (one per CU: the LDS request) must all be
+// resident at once, since each waits for the others' rounds
 constexpr int kNlpPersistentBlocks = 64;
 // the round tags' sequence: the solve's number x kNlpMaxIters + the round (llampc_nlp_create
 // bounds iters by it), 32 bits — never a stale word's

@@ -87,6 +87,7 @@ def _worker(rank, world, store, q, n, case, transport):
                                 timeout=datetime.timedelta(seconds=60))
         sb = ShardedBank(_bank(n, case), rank, world, 0, W=W)
         assert sb.exchange and sb.transport == transport, (sb.transport, sb.fallback_reason)
+        sb.bank.set_concurrency(world)     # every rank on this one device: its share of the CUs
         ctl = LLAMPC(sb, ETHZ('optimal', True), H=H, C=C, K=K, mode="device", prelaunch=armed)
         assert ctl._ctl.transport == transport and ctl._ctl.prelaunch == armed
         before = None

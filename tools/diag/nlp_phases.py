@@ -1,8 +1,8 @@
-"""Diagnostic (stamps build): phases of the setupNLP.solve CEM round launches — per block
-(µs from the first sample block's round start, s_memrealtime): mean / std in, samples formed,
-rate-clipped, staged, rolled out, next variates drawn; the completion block: 7 round start,
-4 lists in, 5 merged, 6 elite loaded, 8 next mean / std published — for the last round of a
-few solves.  usage: python tools/diag/nlp_phases.py"""
+"""Diagnostic (stamps build): phases of the setupNLP.solve CEM round — per stamp the earliest
+and latest block (µs from the first block's round start, s_memrealtime): mean / std in, samples
+formed, rate-clipped, staged, rolled out, list published; then every block's completion
+(round 6): lists in, merged, elite loaded, next mean / std — for the last round of a few solves.
+usage: python tools/diag/nlp_phases.py"""
 import ctypes
 import os
 import sys
@@ -22,7 +22,8 @@ from llampc.tracks import ETHZ  # noqa: E402
 lib = nat.load()
 lib.llampc_debug_nlp_stamps.argtypes = [ctypes.c_void_p]
 H = 20
-d = np.load(os.path.join(REPO, "tests", "golden", "dyn_slice.npz"))
+from llampc.tracks import dyn_slice  # noqa: E402
+d = dyn_slice()
 s, u = d["states"], d["inputs"]
 tr = ETHZ('optimal', True)
 p = ORCA(control="pwm")
@@ -37,9 +38,7 @@ for t in range(10, 16):
     nb = nlp.samples // 64
     base = Z[:nb, 0].min()
     us = lambda v: (v - base) / 100.0  # noqa: E731
-    win = nb                                   # the completion block: the grid's last
-    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (10, 1, 2, 9, 3, 11)]
-    comp = [f"{k}: {us(Z[win, k]):.1f}" for k in (7, 4, 5, 6, 8)]
-    print(f"solve {t}: sample blocks ms/formed/clipped/staged/rolled/next-drawn (min/max) {' '.join(row)} | "
-          f"completion block {' '.join(comp)}", flush=True)
+    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (10, 1, 2, 9, 3, 11, 4, 5, 6, 8)]
+    print(f"solve {t}: ms/formed/clipped/staged/rolled/published/lists-in/merged/elite/next-ms (min/max) "
+          f"{' '.join(row)}", flush=True)
 nlp.close()
