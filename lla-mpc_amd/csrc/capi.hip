@@ -644,8 +644,7 @@ int llampc_bank_create(const double* params, int64_t n, int64_t global_offset,
   if (bank_stream(device, b->dedicated, &b->stream) != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "hipStreamCreate failed"));
   b->own_stream = true;
-  // look-back lists (waves); 8 blocks more for the XCD-aligned layout (launch_plan)
-  const int64_t lbl = ((int64_t)lookback_blocks(n) + 8) * (kBlock / 64);
+  const int64_t lbl = (int64_t)lookback_blocks(n) * (kBlock / 64);   // look-back lists (waves)
   const int64_t lab = n;                 // worst case: one model per block (wave-role, G=64)
   if ((rc = dev_alloc(&b->d_params, 6 * (size_t)n)) || (rc = dev_alloc(&b->d_ring, (size_t)W * n)) ||
       (rc = dev_alloc(&b->d_am_val, lbl)) || (rc = dev_alloc(&b->d_am_idx, lbl)) ||

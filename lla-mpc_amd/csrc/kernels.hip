@@ -351,32 +351,6 @@ hipError_t launch_plan(const LookbackLaunch* lb, const LookaheadLaunch* la, Fina
       wq = (stage && (forced ? forced == 8 : units >= 4 * (int64_t)nw * kWaves)) ? 2 : 1;
     }
   }
-  // XCD-aligned look-back (LookbackLaunch.xchunk): with one model per look-back lane and the
-  // block-per-models look-ahead in the same launch, look-back block b takes the models of the
-  // look-ahead blocks dealt to its XCD (grid positions congruent mod 8 share one,
-  // MI355X_MICROARCH.md "Workgroup dispatch"), so each model's Pacejka row is fetched from HBM
-  // once and the second half finds it in that XCD's L2 (verdict r05 #8: the rows were read
-  // twice).  The look-back block count grows to a multiple of 8 covering every XCD's share
-  // (the bank's lists are sized for 8 blocks more).  LLAMPC_LB_XCD=0: contiguous (A/B).
-  if (lb && la && lbv.R == 1 && wq == 0 && la->n == lb->n && la->params == lb->params) {
-    static const bool off = getenv("LLAMPC_LB_XCD") && getenv("LLAMPC_LB_XCD")[0] == '0';
-    const int M = kBlock / (G * lpm);                   // models per look-ahead block
-    if (!off && M >= 1 && kBlock % M == 0) {
-      const int Q = kBlock / M;                         // look-ahead blocks per look-back block
-      const int nb = 8 * (((f.nb_la + 7) / 8 + Q - 1) / Q);
-      if (nb >= f.nb_lb && nb <= lookback_blocks(lb->n) + 8 && nb <= 64 * kListsPerLane / kWaves) {
-        f.nb_lb = nb;
-        lbv.xchunk = M;
-        lbv.xq = Q;
-        lbv.xlb = nb;
-        if (lb->full) {
-          const size_t Mk = (size_t)nb * lb->K, L = nb;   // lb_final (layout there)
-          lds = std::max(lds, kScratchBytes + 8 * (3 * Mk + L) + sizeof(Ent) * L * kWaves +
-                                  4 * (3 * Mk + L + LLAMPC_KMAX + 2) + 8 + 16);
-        }
-      }
-    }
-  }
   if (f.px_G) {                          // fused peer exchange: RK4, given xref, device inputs
     if (pk || integ != LLAMPC_RK4 || (la && la->xref_mode == LLAMPC_XREF_RACELINE) || f.px_G > kPeerFuseMax)
       return hipErrorInvalidValue;

@@ -44,20 +44,8 @@ struct LookbackLaunch {
   double* wm_buf;        // [n] window means (when the window is full: R > 1 or wm_keep)
   double* am_val;  int64_t* am_idx;   // [blocks * kWaves] (one per look-back wave)
   double* tk_val;  int64_t* tk_idx;   // [blocks * kWaves][K]
-  // XCD-aligned models (xchunk > 0, R == 1; launch_plan): look-back block b covers the models
-  // of the look-ahead blocks dealt to its XCD (grid positions b and b + 8 share one), xq chunks
-  // of xchunk models each, so the two halves' Pacejka rows meet in one XCD's L2; else block b
-  // covers models [256 R b, 256 R (b + 1)).  xlb = the launch's look-back block count.
-  int32_t xchunk, xq, xlb;
 };
-// The model of look-back lane (blk, r, tid).
-__host__ __device__ __forceinline__ int64_t lb_model(const LookbackLaunch& a, int blk, int r, int tid) {
-  if (a.xchunk == 0) return (int64_t)blk * kBlock * a.R + (int64_t)r * kBlock + tid;
-  const int x = blk & 7, i = blk >> 3;
-  const int a0 = (x - (a.xlb & 7) + 8) & 7;              // the first look-ahead block of x's XCD
-  const int q = tid / a.xchunk, o = tid - q * a.xchunk;
-  return ((int64_t)a0 + 8 * ((int64_t)i * a.xq + q)) * a.xchunk + o;
-}
+
 
 struct LookaheadLaunch {
   const double* params;  int64_t n;  int64_t goff;

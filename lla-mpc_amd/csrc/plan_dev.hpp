@@ -510,6 +510,7 @@ __device__ __forceinline__ void wave_topk_rank(const LookbackLaunch& a, double w
 template <bool ARMED = false, typename Door = int>
 __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk, const Scratch& sc, Door door = 0) {
   LB_STAMP(blk, 0);
+  const int64_t base = (int64_t)blk * kBlock * a.R;
   const fm::FmK K = fm::FmK::load();
   bool ubad = false;
   const Input uf = make_input_fast(a.u_prev[0], a.u_prev[1], K, ubad);
@@ -524,7 +525,7 @@ __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk,
     bool pvalid = false;
     int64_t pn = 0;
     if (a.R == 1) {                     // launch-uniform
-      const int64_t n = lb_model(a, blk, 0, threadIdx.x);
+      const int64_t n = base + threadIdx.x;
       if (n < a.n) {
         pvalid = true;
         pn = n;
@@ -549,7 +550,7 @@ __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk,
     if (!x_now) return false;
   }
   for (int r = 0; r < a.R; ++r) {
-    const int64_t n = lb_model(a, blk, r, threadIdx.x);
+    const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
     if (n >= a.n) break;
     double x[6];
     Tire t;
@@ -607,7 +608,7 @@ __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk,
   double v = a.nan_first ? __builtin_inf() : __builtin_nan("");
   uint32_t li = kNoLocal;
   for (int r = 0; r < a.R; ++r) {
-    const int64_t n = lb_model(a, blk, r, threadIdx.x);
+    const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
     if (n >= a.n) break;
     const double w = (a.R == 1) ? wm0 : a.wm_buf[n];
     const bool t = a.nan_first ? less_bf<1>(w, (uint32_t)n, v, li) : less_bf<0>(w, (uint32_t)n, v, li);
@@ -625,7 +626,7 @@ __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk,
   BEnt* wl = reinterpret_cast<BEnt*>(rank_lds + kWaves * kRankBytes);   // [kWaves][K]
   BEnt* mine = wl + (threadIdx.x >> 6) * a.K;
   if (a.R == 1) {                       // launch-uniform
-    wave_topk_rank(a, wm0, lb_model(a, blk, 0, threadIdx.x), rank_lds, mine);
+    wave_topk_rank(a, wm0, base + threadIdx.x, rank_lds, mine);
     __syncthreads();
     block_topk_merge(a, blk, wl);
     LB_STAMP(blk, 3);
@@ -638,7 +639,7 @@ __device__ __forceinline__ bool lookback_block(const LookbackLaunch& a, int blk,
     double cv = __builtin_nan("");
     uint32_t cl = kNoLocal;
     for (int r = 0; r < a.R; ++r) {
-      const int64_t n = lb_model(a, blk, r, threadIdx.x);
+      const int64_t n = base + (int64_t)r * kBlock + threadIdx.x;
       if (n >= a.n) break;
       const double w = (a.R == 1) ? wm0 : a.wm_buf[n];
       const uint32_t ln = (uint32_t)n;
@@ -1218,7 +1219,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
         if (a.poll) {
           st_wt(&a.la_tag[nm], tag_word(a.seq, (uint32_t)(__double_as_longlong(mv) >> 32)));
           st_wt(&a.la_tag[a.n + nm], tag_word(a.seq, (uint32_t)__double_as_longlong(mv)));
-          if (C > 1) st_wt(&a.la_tag[2 * a.n + nm], tag_word(a.seq, (uint32_t)(int32_t)mc));
+          st_wt(&a.la_tag[2 * a.n + nm], tag_word(a.seq, (uint32_t)(int32_t)mc));
         } else {
           st_wt(&a.best_cand[nm], (int32_t)mc);
           st_wt(&a.best_cost[nm], mv);
@@ -1337,7 +1338,7 @@ __device__ __forceinline__ void lookahead_block(const LookaheadLaunch& a, int bl
       // candidate is 0, so only the cost's two words (final_poll)
       st_wt(&a.la_tag[n], tag_word(a.seq, (uint32_t)(__double_as_longlong(bv) >> 32)));
       st_wt(&a.la_tag[a.n + n], tag_word(a.seq, (uint32_t)__double_as_longlong(bv)));
-      if (C > 1) st_wt(&a.la_tag[2 * a.n + n], tag_word(a.seq, (uint32_t)(int32_t)bc));
+      st_wt(&a.la_tag[2 * a.n + n], tag_word(a.seq, (uint32_t)(int32_t)bc));
     } else {
       st_wt(&a.best_cand[n], (int32_t)bc);
       st_wt(&a.best_cost[n], bv);
@@ -1731,24 +1732,22 @@ __device__ __forceinline__ void final_poll(const FinalLaunch& f, const Scratch& 
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const uint64_t bound = (uint64_t)(uint32_t)f.poll << 16;
   bool late = false;
-  // C = 1: the look-ahead stores the cost's two words only; the candidate is 0 (the one
-  // candidate wins its model's argmin whatever its cost, NaN included: less_nan_last)
-  const bool one = f.C == 1;
-  auto rec3 = [&](int64_t m, uint64_t* w) {
+  if (mk >= 0) {
     for (;;) {
-      w[0] = ld_wt(&f.la_tag[m]);
-      w[1] = ld_wt(&f.la_tag[f.n + m]);
-      if (!one) w[2] = ld_wt(&f.la_tag[2 * f.n + m]);
-      if ((int)tag_ok(w[0], f.seq) & (int)tag_ok(w[1], f.seq) & ((int)one | (int)tag_ok(w[2], f.seq))) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {
-        late = true;
-        break;
-      }
+#pragma unroll
+      for (int w = 0; w < 3; ++w) kw[w] = ld_wt(&f.la_tag[w * f.n + mk]);
+      if ((int)tag_ok(kw[0], f.seq) & (int)tag_ok(kw[1], f.seq) & (int)tag_ok(kw[2], f.seq)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > bound) { late = true; break; }
     }
-    if (one) w[2] = 0;
-  };
-  if (mk >= 0) rec3(mk, kw);
-  if (ms >= 0) rec3(ms, sw);
+  }
+  if (ms >= 0) {
+    for (;;) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) sw[w] = ld_wt(&f.la_tag[w * f.n + ms]);
+      if ((int)tag_ok(sw[0], f.seq) & (int)tag_ok(sw[1], f.seq) & (int)tag_ok(sw[2], f.seq)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > bound) { late = true; break; }
+    }
+  }
   for (int j = 0; j < nbt; ++j) {
     const int b = tid + j * kBlock;
     if (b < f.nb_la) {
