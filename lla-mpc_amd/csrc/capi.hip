@@ -2228,10 +2228,8 @@ int llampc_ctl_inputs(llampc_ctl* c, double* xref, double* U) {
 struct llampc_nlp {
   llampc_bank* b = nullptr;
   llampc_nlp_cfg cfg{};
-  // device block: NlpState | x0 [6] | xref [2][H+1] | traj [H+1][6] | h [H]  (one H2D, one D2H)
-  unsigned char* d_blk = nullptr;
-  unsigned char* h_blk = nullptr;        // pinned mirror
-  size_t blk_bytes = 0, in_bytes = 0;
+  NlpState* d_st = nullptr;              // the best so far across a solve's launches (device);
+                                         // the inputs travel as kernel arguments (NlpInline)
   double* d_cost = nullptr;              // the sample blocks' sorted lists as tagged words
                                          // [2][3][samples], then the rounds' rate-clipped
                                          // sequences [2][samples][H][2] (NlpLaunch.list_tag, cand;
@@ -2253,10 +2251,9 @@ int llampc_nlp_destroy(llampc_nlp* p) {
   {
     DeviceGuard g(p->b ? p->b->device : 0);
     if (p->b && p->b->stream) (void)hipStreamSynchronize(p->b->stream);
-    if (p->d_blk) (void)hipFree(p->d_blk);
+    if (p->d_st) (void)hipFree(p->d_st);
     if (p->d_cost) (void)hipFree(p->d_cost);
     if (p->d_ms_tag) (void)hipFree(p->d_ms_tag);
-    if (p->h_blk) (void)hipHostFree(p->h_blk);
     if (p->h_res) (void)hipHostFree(p->h_res);
     if (p->h_tag) (void)hipHostFree(p->h_tag);
   }
@@ -2282,15 +2279,13 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
   p->b = b;
   p->cfg = k;
   const size_t H = (size_t)k.H;
-  p->in_bytes = sizeof(NlpState) + 8 * (6 + 2 * (H + 1));
-  p->blk_bytes = p->in_bytes;
   auto cleanup = [&](int code) {
     llampc_nlp_destroy(p);
     return code;
   };
   int rc;
   // the lists: 3 words per entry, samples / 64 x len <= samples entries; both by round parity
-  if ((rc = dev_alloc(&p->d_blk, p->blk_bytes)) || (rc = dev_alloc(&p->d_cost, (size_t)k.samples * (6 + 4 * (size_t)H))) ||
+  if ((rc = dev_alloc(&p->d_st, 1)) || (rc = dev_alloc(&p->d_cost, (size_t)k.samples * (6 + 4 * (size_t)H))) ||
       (rc = dev_alloc(&p->d_ms_tag, 8 * (size_t)LLAMPC_HMAX)))
     return cleanup(rc);
   {
@@ -2303,9 +2298,6 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
     const bool resident = k.samples / 64 <= cus;
     p->per_round = !nlp_persistent(k.samples) || !resident || (e && e[0] == '1');
   }
-  if (hipHostMalloc(reinterpret_cast<void**>(&p->h_blk), p->blk_bytes, hipHostMallocDefault) != hipSuccess)
-    return cleanup(fail(LLAMPC_E_OOM, "hipHostMalloc(NLP staging) failed"));
-  std::memset(p->h_blk, 0, p->blk_bytes);
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_res), sizeof(NlpResult), hipHostMallocCoherent | hipHostMallocMapped) !=
           hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&p->h_tag), 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
@@ -2315,7 +2307,7 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
       hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_tag), p->h_tag, 0) != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "hipHostGetDevicePointer(NLP result) failed"));
   // tagged words start at tag 0, which no solve uses (nlp_seq of a solve number >= 1)
-  if (hipMemcpy(p->d_blk, p->h_blk, p->blk_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+  if (hipMemset(p->d_st, 0, sizeof(NlpState)) != hipSuccess ||
       hipMemset(p->d_cost, 0, (size_t)k.samples * 6 * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(p->d_ms_tag, 0, 8 * LLAMPC_HMAX * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return cleanup(fail(LLAMPC_E_HIP, "NLP solver upload failed"));
@@ -2335,21 +2327,14 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   const llampc_nlp_cfg& k = p->cfg;
   const int H = k.H;
   hipStream_t s = b->stream;
-  // stage: the first mean (base or uprev held), the first std, best = +inf, x0, xref
-  NlpState* hs = reinterpret_cast<NlpState*>(p->h_blk);
+  // the launch's inputs (NlpInline): x0, xref, the first mean (base or uprev held); the first
+  // std is sigma0, the best so far starts at +inf (the kernel's round 0)
+  NlpInline pk;
+  std::memcpy(pk.v, x0, 6 * sizeof(double));
+  std::memcpy(pk.v + 6, xref, 2 * (size_t)(H + 1) * sizeof(double));
+  double* m0 = pk.v + 6 + 2 * (H + 1);
   for (int i = 0; i < H; ++i)
-    for (int j = 0; j < 2; ++j) {
-      hs->mean[i][j] = base ? base[2 * i + j] : uprev[j];
-      hs->std_[i][j] = k.sigma0[j];
-    }
-  hs->best_j = HUGE_VAL;
-  hs->best_it = -1;
-  double* hx = reinterpret_cast<double*>(p->h_blk + sizeof(NlpState));
-  std::memcpy(hx, x0, 6 * sizeof(double));
-  std::memcpy(hx + 6, xref, 2 * (size_t)(H + 1) * sizeof(double));
-  HIP_TRY(hipMemcpyAsync(p->d_blk, p->h_blk, p->in_bytes, hipMemcpyHostToDevice, s));
-  NlpState* ds = reinterpret_cast<NlpState*>(p->d_blk);
-  double* dx = reinterpret_cast<double*>(p->d_blk + sizeof(NlpState));
+    for (int j = 0; j < 2; ++j) m0[2 * i + j] = base ? base[2 * i + j] : uprev[j];
   NlpLaunch a{};
   a.la.params = b->d_params;
   a.la.n = 1;
@@ -2359,15 +2344,14 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.la.integrator = LLAMPC_EULER_NLP;
   a.la.Ts = k.Ts;
   a.la.cost = make_cost(k.cost, k.Ts);
-  a.st = ds;
-  a.x0 = dx;
-  a.xref = dx + 6;
+  a.st = p->d_st;
   a.list_tag = reinterpret_cast<uint64_t*>(p->d_cost);
   a.cand = p->d_cost + 6 * (size_t)k.samples;
   a.res = p->d_res;
   a.host_tag = p->d_tag;
   a.host_seq = p->calls + 1;
   a.ms_tag = p->d_ms_tag;
+  a.ltraj = nlp_ltraj_fits(H, k.samples, k.elite);
   a.seed = k.seed;
   a.call = p->calls;
   a.up0 = uprev[0];
@@ -2381,6 +2365,8 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.rhi0 = k.rate_hi[0];
   a.rhi1 = k.rate_hi[1];
   a.std_floor = k.std_floor;
+  a.sig0 = k.sigma0[0];
+  a.sig1 = k.sigma0[1];
   a.H = H;
   a.samples = k.samples;
   a.elite = k.elite;
@@ -2391,13 +2377,13 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
     for (int it = 0; it < k.iters; ++it) {
       a.it = it;
       TimedLaunch tl(b, 0, s);           // llampc_bank_timing on the solver's bank: per round
-      HIP_TRY(launch_nlp(a, s));
+      HIP_TRY(launch_nlp(a, pk, s));
     }
   } else {                              // every round in one launch (nlp.hpp nlp_persistent)
     a.it = 0;
     a.rounds = k.iters;
     TimedLaunch tl(b, 0, s);             // llampc_bank_timing on the solver's bank: per solve
-    HIP_TRY(launch_nlp(a, s));
+    HIP_TRY(launch_nlp(a, pk, s));
   }
   // the last round's completion writes the result into pinned memory and then the tag
   const uint64_t want = p->calls + 1;

@@ -17,7 +17,7 @@ struct NlpState {
   double best_u[LLAMPC_HMAX][2];
   double best_j;                 // +inf until a finite objective is seen
   int32_t best_it;
-  int32_t pad;
+  int32_t best_s;                // the best sequence's sample index (in round best_it)
 };
 
 // A launch of CEM rounds [it, it + rounds): samples / 64 sample blocks, each of which also
@@ -39,10 +39,6 @@ struct NlpResult {
 struct NlpLaunch {
   LookaheadLaunch la;            // params [6][1], veh (NLP form), cost, H, Ts, integrator EULER_NLP
   NlpState* st;
-  const double* x0;              // [6] device
-  const double* xref;            // [2][H+1] device
-  uint64_t* top_key;             // [samples / 64][len] each sample block's best (sorted keys),
-  uint32_t* top_idx;             //   then their sample indices (len = nlp_list_len(elite))
   double* cand;                  // [2][samples][H][2] the round's sequences after the rate clip
                                  //   (by round parity: nlp.hip nlp_cand)
   NlpResult* res;                // the last round: the result, in pinned host memory (device alias)
@@ -58,8 +54,19 @@ struct NlpLaunch {
   double umin0, umin1, umax0, umax1;
   double rlo0, rlo1, rhi0, rhi1; // per-step rate bounds (x Ts); lo > hi: none
   double std_floor;
+  double sig0, sig1;             // the first round's std (llampc_nlp_cfg.sigma0)
   int32_t it, rounds, iters;     // the launch's first round, its round count, the solve's
   int32_t H, samples, elite, has_hold;
+  int32_t ltraj;                 // the last round's sample rollouts keep their states in LDS and
+                                 //   a best from that round is copied from there (else re-run)
+};
+
+// The solve's inputs in the kernarg segment (the plan kernel's InlinePack idea): x0 [6] | xref
+// [2][H+1] | the first round's mean [H][2] — the launch carries them, so a solve needs no H2D
+// copy (it cost ~8 us of a 212 us solve).  The state (best so far, NlpState) starts in registers.
+constexpr int kNlpInlineDoubles = 6 + 2 * (LLAMPC_HMAX + 1) + 2 * LLAMPC_HMAX;
+struct NlpInline {
+  double v[kNlpInlineDoubles];
 };
 
 // every round in one launch: the sample blocks (one per CU: the LDS request) must all be
@@ -79,7 +86,8 @@ __host__ __device__ __forceinline__ int nlp_list_len(int elite) {
   while (l < elite) l <<= 1;
   return l;
 }
-size_t nlp_lds_bytes(int H, int samples, int elite);
-hipError_t launch_nlp(const NlpLaunch& a, hipStream_t s);
+size_t nlp_lds_bytes(int H, int samples, int elite, bool ltraj = false);
+bool nlp_ltraj_fits(int H, int samples, int elite);
+hipError_t launch_nlp(const NlpLaunch& a, const NlpInline& pk, hipStream_t s);
 
 }  // namespace llampc

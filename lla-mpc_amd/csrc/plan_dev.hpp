@@ -698,8 +698,10 @@ struct DeferOut {
   double xl, act, feas_s;
   bool dok;
 };
+// SW: doubles per staged record (the plan kernel's kStageW; the NLP kernel's compact 6: the
+// Euler record's input-rate term and feasibility then at 4 and 5 instead of 6 and 7).
 template <int INTEG, bool STAGE, int LPM, int XM, bool FAST, bool SPLIT = false, bool ULDS = false, bool TRAJ = false,
-          bool S4 = false, bool DEFER = false>
+          bool S4 = false, bool DEFER = false, int SW = kStageW>
 __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64_t n,
                                           const double* x0, const double* sx, const double* su, const VehK& veh,
                                           const Tire& t, const StageK& sk, const CostK& q,
@@ -737,7 +739,9 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     Input u;
     FusedIn fi{};
     if (STAGE) {                        // staged per block (lookahead_block), layouts there
-      const double* o = su + kStageW * (k * C + c);
+      static_assert(SW == kStageW || (SW == 6 && INTEG != 0), "the compact record: NLP-Euler only");
+      constexpr int kAct = SW == kStageW ? 6 : 4, kFeas = kAct + 1;
+      const double* o = su + SW * (k * C + c);
       if (INTEG == 0 && FAST) {         // the fused stages' input terms
         fi = FusedIn{o[0], o[1], o[2], o[3], o[4]};
         ua = 0.0;
@@ -754,8 +758,8 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
         u.sd = o[2];
         u.cd = o[3];
       }
-      act = act + o[6];                 // the candidate's input-rate term and feasibility
-      feas_s = feas_s * o[7];
+      act = act + o[kAct];              // the candidate's input-rate term and feasibility
+      feas_s = feas_s * o[kFeas];
     } else {
       ua = Ub[2 * ((int64_t)c * H + k)];
       ud = Ub[2 * ((int64_t)c * H + k) + 1];
@@ -797,9 +801,9 @@ __device__ __forceinline__ double rollout(const LookaheadLaunch& a, int c, int64
     if (!STAGE && !S4) act = act + act_term(q, d0, d1);
     p0 = ua;
     p1 = ud;
-    if (TRAJ && traj != nullptr) {      // the state after step k (every lane of a quad holds it)
-#pragma unroll
-      for (int m = 0; m < 6; ++m) traj[6 * (k + 1) + m] = x[m];
+    if (TRAJ && traj != nullptr) {      // the state after step k (every lane of a quad holds it;
+#pragma unroll                          // the caller passes traj to one lane): three 16-B stores
+      for (int m = 0; m < 6; m += 2) *reinterpret_cast<double2*>(traj + 6 * (k + 1) + m) = double2{x[m], x[m + 1]};
     }
   }
   if (S4) {                             // the candidate's summed input-rate cost, feasibility

@@ -163,7 +163,9 @@ _SIGNATURES = {
     "llampc_ctl_merge": (C.c_int, [_dp, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, _dp,
                                    C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "llampc_nlp_create": (C.c_int, [C.c_void_p, C.POINTER(NlpCfg), C.POINTER(C.c_void_p)]),
-    "llampc_nlp_solve": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, C.c_int32, _dp, C.POINTER(C.c_double), _dp]),
+    # pointers as c_void_p: setupNLP.solve passes its persistent buffers' cached addresses
+    "llampc_nlp_solve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                   C.c_void_p, C.c_void_p, C.c_void_p]),
     "llampc_nlp_destroy": (C.c_int, [C.c_void_p]),
     "llampc_dynamics_batch": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                         C.POINTER(Vehicle), C.c_int64, C.c_void_p, C.c_int32,

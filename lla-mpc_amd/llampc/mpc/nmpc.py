@@ -90,23 +90,31 @@ class setupNLP:
         nat.check(nat.load().llampc_nlp_create(self._bank.handle, nat.C.byref(cfg), nat.C.byref(h)))
         self._h = h
         self.cfg = cfg
+        H = self.horizon
+        self._io = {"x0": np.zeros(6), "xref": np.zeros((2, H + 1)), "up": np.zeros(2), "base": np.zeros((H, 2)),
+                    "umpc": np.zeros((H, 2)), "fval": np.zeros(1), "xmpc": np.zeros((H + 1, 6))}
+        self._addr = {k: v.ctypes.data for k, v in self._io.items()}
 
     def solve(self, x0, xref, uprev):
         """-> (umpc [2, H], fval, xmpc [6, H+1], violation in {0, 0.02}) as nmpc.py:161-203."""
         self._ensure()
+        b = self._io
         H = self.horizon
-        x0 = nat.f64(np.asarray(x0, dtype=np.float64).ravel())
-        xref = np.ascontiguousarray(np.asarray(xref, dtype=np.float64)[:2, :H + 1])
-        uprev = nat.f64(np.asarray(uprev, dtype=np.float64).ravel())
-        base = None if self._last is None else np.ascontiguousarray(np.concatenate([self._last[1:], self._last[-1:]]))
-        umpc = np.empty((H, 2))
-        xmpc = np.empty((H + 1, 6))
-        fval = nat.C.c_double()
-        nat.check(nat.load().llampc_nlp_solve(self._h, nat.dptr(x0), nat.dptr(xref), nat.dptr(uprev), nat.dptr(base),
-                                               int(self._last is not None), nat.dptr(umpc), nat.C.byref(fval),
-                                               nat.dptr(xmpc)))
+        # the inputs into the persistent buffers (their addresses cached at the first solve: the
+        # per-call ctypes pointer objects cost more host time than the copies)
+        b["x0"][:] = np.asarray(x0, dtype=np.float64).ravel()
+        b["xref"][:] = np.asarray(xref, dtype=np.float64)[:2, :H + 1]
+        b["up"][:] = np.asarray(uprev, dtype=np.float64).ravel()
+        hold = self._last is not None
+        if hold:                         # the warm start: the last solution shifted one step
+            b["base"][:-1] = self._last[1:]
+            b["base"][-1] = self._last[-1]
+        a = self._addr
+        nat.check(nat.load().llampc_nlp_solve(self._h, a["x0"], a["xref"], a["up"], a["base"] if hold else None,
+                                               int(hold), a["umpc"], a["fval"], a["xmpc"]))
+        umpc = b["umpc"].copy()
         self._last = umpc
-        return umpc.T.copy(), float(fval.value), xmpc.T.copy(), 0.0
+        return umpc.T.copy(), float(b["fval"][0]), b["xmpc"].T.copy(), 0.0
 
     def close(self):
         if self._h is not None:

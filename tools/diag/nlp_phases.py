@@ -1,7 +1,8 @@
 """Diagnostic (stamps build): phases of the setupNLP.solve CEM round — per stamp the earliest
 and latest block (µs from the first block's round start, s_memrealtime): mean / std in, samples
 formed, rate-clipped, staged, rolled out, list published; then every block's completion
-(round 6): lists in, merged, elite loaded, next mean / std — for the last round of a few solves.
+(round 6): wave 0's four lists in, every group in, merged, elite loads issued, elite mean, next
+mean / std — for the last round of a few solves.
 usage: python tools/diag/nlp_phases.py"""
 import ctypes
 import os
@@ -28,17 +29,18 @@ s, u = d["states"], d["inputs"]
 tr = ETHZ('optimal', True)
 p = ORCA(control="pwm")
 nlp = setupNLP(H, 0.02, np.eye(2), np.zeros((2, 2)), np.diag([5e-3, 1]), p, Dynamic(**p, device=0), tr, device=0)
-buf = (ctypes.c_ulonglong * (32 * 12))()
+buf = (ctypes.c_ulonglong * (32 * 16))()
 projidx = 0
 for t in range(10, 16):
     xref, projidx, _ = ConstantSpeed(s[:2, t], s[3, t], tr, H, 0.02, projidx)
     nlp.solve(s[:, t].copy(), xref, u[:, t - 1].copy())
     lib.llampc_debug_nlp_stamps(buf)
-    Z = np.frombuffer(buf, dtype=np.uint64).reshape(32, 12).astype(np.int64)
+    Z = np.frombuffer(buf, dtype=np.uint64).reshape(32, 16).astype(np.int64)
     nb = nlp.samples // 64
     base = Z[:nb, 0].min()
     us = lambda v: (v - base) / 100.0  # noqa: E731
-    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (10, 1, 2, 9, 3, 11, 4, 5, 6, 8)]
-    print(f"solve {t}: ms/formed/clipped/staged/rolled/published/lists-in/merged/elite/next-ms (min/max) "
+    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (10, 1, 2, 9, 3, 12, 11, 4, 13, 5, 6, 14, 8)]
+    print(f"solve {t}: ms/formed/clipped/staged/rolled0/rolled/published/own4/all-in/merged/elite-issued/"
+          f"mean/next-ms (min/max) "
           f"{' '.join(row)}", flush=True)
 nlp.close()
