@@ -245,17 +245,15 @@ __device__ __forceinline__ int nlp_owner(const NlpLaunch& a, int bit, int bs) {
 // trl: the block's LDS states of its samples' rollouts in the solve's last round (NlpLaunch.ltraj)
 // — a best from that round is written by its own block, from there; an earlier round's best by
 // block 0, re-running its rollout.
-__device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, double* ub, bool better, double bj, int bit,
-                                               int bs, int it, const double* trl, const double* sx,
-                                               const double* x0) {
+// bu: the block's LDS copy of the best sequence so far.
+__device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, double* bu, double bj, int bit, int bs, int it,
+                                               const double* trl, const double* sx, const double* x0) {
   const int tid = threadIdx.x, H = a.H;
-  const NlpState* st = a.st;
   NlpResult* res = a.res;
-  __syncthreads();                      // the elite rows are read; best_u is final
+  __syncthreads();                      // bu is final
   for (int e = tid; e < 2 * H; e += (int)blockDim.x) {
-    // an earlier round's completion (none: no finite objective, the result's zeros)
-    const double v = better ? ub[e] : bit < 0 ? 0.0 : ld_wt(&st->best_u[0][0] + e);
-    ub[e] = v;
+    const double v = bit < 0 ? 0.0 : bu[e];   // none: no finite objective, the result's zeros
+    bu[e] = v;
     (&res->best_u[0][0])[e] = v;
   }
   if (tid == 0) {
@@ -267,7 +265,7 @@ __device__ __forceinline__ void nlp_trajectory(const NlpLaunch& a, double* ub, b
     for (int e = tid; e < 6 * (H + 1); e += (int)blockDim.x) (&res->traj[0][0])[e] = e < 6 ? x0[e] : src[e - 6];
   } else {
     __syncthreads();
-    if (tid < 4) nlp_traj_quad(a, sx, ub, x0);
+    if (tid < 4) nlp_traj_quad(a, sx, bu, x0);
   }
   __threadfence_system();               // the result's host-memory stores, then the tag
   __syncthreads();
@@ -380,13 +378,12 @@ __device__ __forceinline__ bool nlp_poll_lists(const NlpLaunch& a, const NlpComp
 // bj / bit: the best objective so far and its round, carried in registers across the launch's
 // rounds; stored to the state too, for the next launch.
 __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* cbase, int it, int nl, double& bjv,
-                                             int& bitv, int& bsv, double* ms, bool last_of_launch,
+                                             int& bitv, int& bsv, double* ms, double* bu, bool last_of_launch,
                                              const double* trl, const double* sx, const double* x0) {
 #pragma clang fp contract(off)
   const int tid = threadIdx.x, H = a.H, E = a.elite;
   const int len = nlp_list_len(E);
   const bool b0 = blockIdx.x == 0;
-  NlpState* st = a.st;
   const NlpCompLds L = nlp_comp_lds(cbase, nl, len);
   uint64_t* kA = L.kA;
   uint64_t* kB = L.kB;
@@ -481,7 +478,7 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
         st_wt(&a.ms_tag[2 * is + 1], tag_word(sq1, (uint32_t)(sb >> 32)));
       }
     }
-    if (b0 && better) st_wt(&st->best_u[k][j], eu[2 * k + j]);
+    if (better) bu[2 * k + j] = eu[2 * k + j];   // this block's copy of the best so far
     msn[im] = m;                        // this block's copy (ms is read again only after a barrier)
     msn[is] = sd;
   }
@@ -492,14 +489,8 @@ __device__ __forceinline__ void nlp_complete(const NlpLaunch& a, unsigned char* 
   bjv = nlp_uni(bj);
   bitv = __builtin_amdgcn_readfirstlane(bit);
   bsv = __builtin_amdgcn_readfirstlane(bs);
-  if (b0 && tid == 0 && (better || it == 0)) {   // round 0: the state's first values
-    st_wt(&st->best_j, bj);
-    st_wt(&st->best_it, bit);
-    st_wt(&st->best_s, bs);
-  }
   NLP_STAMP(8);
-  if (it == a.iters - 1 && (int)blockIdx.x == nlp_owner(a, bit, bs))
-    nlp_trajectory(a, eu, better, bj, bit, bs, it, trl, sx, x0);
+  if (it == a.iters - 1 && (int)blockIdx.x == nlp_owner(a, bit, bs)) nlp_trajectory(a, bu, bj, bit, bs, it, trl, sx, x0);
   __syncthreads();                      // ms (the next round's) and the LDS lists (the next poll)
 }
 
@@ -574,8 +565,8 @@ __device__ __forceinline__ bool nlp_poll2(const uint64_t* lt, int nbl, int ea, i
 // four times the bytes through the one CU, 1.8 us against 1.0 for wave 0's own loads.)
 __device__ __forceinline__ bool nlp_complete32(const NlpLaunch& a, unsigned char* smem, unsigned char* cbase, int it,
                                                int r, int nl, double& bjv, int& bitv, int& bsv, double* ms,
-                                               bool last_of_launch, const double* trl, const double* sx,
-                                               const double* x0) {
+                                               double* bu, bool last_of_launch, const double* trl,
+                                               const double* sx, const double* x0) {
 #pragma clang fp contract(off)
   // an opaque copy of the thread index: the lane arithmetic below stays here instead of being
   // hoisted out of the round loop, where it would live across the rollouts (VGPR spills)
@@ -655,7 +646,8 @@ __device__ __forceinline__ bool nlp_complete32(const NlpLaunch& a, unsigned char
       // that its 32 comparisons stay here instead of being hoisted out of the round loop
       int Eo = E;
       asm volatile("" : "+s"(Eo));
-      const uint32_t fic = lane < Eo ? fi : s0;
+      // each lane its row's offset (one multiply for all 32), then one read-lane per load
+      const uint32_t ro = (lane < Eo ? fi : s0) * (uint32_t)H2;
       for (int q0 = 0; q0 < H2; q0 += 64) {
         const int q = q0 + lane;
         const bool act = q < H2;
@@ -663,10 +655,7 @@ __device__ __forceinline__ bool nlp_complete32(const NlpLaunch& a, unsigned char
         const double* col = cand + (act ? q : H2 - 1);
         double v[32];
 #pragma unroll
-        for (int e = 0; e < 32; ++e) {
-          const uint32_t ix = (uint32_t)__builtin_amdgcn_readlane((int)fic, e);
-          v[e] = ld_wt(col + 2 * (size_t)ix * H);
-        }
+        for (int e = 0; e < 32; ++e) v[e] = ld_wt(col + (uint32_t)__builtin_amdgcn_readlane((int)ro, e));
         NLP_STAMP(6);
         // np.mean / np.std over axis 0: the rows added in sequence, std = sqrt(mean((x - m)^2))
         double acc = 0.0;
@@ -692,8 +681,7 @@ __device__ __forceinline__ bool nlp_complete32(const NlpLaunch& a, unsigned char
             st_wt(&a.ms_tag[2 * is], tag_word(sq1, (uint32_t)sb));
             st_wt(&a.ms_tag[2 * is + 1], tag_word(sq1, (uint32_t)(sb >> 32)));
           }
-          if (b0 && better) st_wt(&a.st->best_u[0][0] + q, v[0]);
-          L.eu[q] = v[0];               // row 0 (the result's, if it is the best)
+          if (better) bu[q] = v[0];     // this block's copy of the best so far
           ms[im] = m;                   // read by the next round after the barrier below
           ms[is] = sd;
         }
@@ -714,14 +702,9 @@ __device__ __forceinline__ bool nlp_complete32(const NlpLaunch& a, unsigned char
   bjv = nlp_uni(better ? c0 : bj0);
   bitv = __builtin_amdgcn_readfirstlane(better ? it : bit0);
   bsv = __builtin_amdgcn_readfirstlane(better ? *bests : bsv);
-  if (b0 && tid == 0 && (better || it == 0)) {   // round 0: the state's first values
-    st_wt(&a.st->best_j, bjv);
-    st_wt(&a.st->best_it, bitv);
-    st_wt(&a.st->best_s, bsv);
-  }
   // the result by the block of the best sample (its states are this block's)
   if (it == a.iters - 1 && (int)blockIdx.x == nlp_owner(a, bitv, bsv))
-    nlp_trajectory(a, L.eu, better, bjv, bitv, bsv, it, trl, sx, x0);
+    nlp_trajectory(a, bu, bjv, bitv, bsv, it, trl, sx, x0);
   return true;
 }
 
@@ -753,11 +736,11 @@ __device__ __forceinline__ void nlp_draw(const NlpLaunch& a, int blk, int it, do
 // The sample block's LDS after the scratch: xref [H+1][2] | Ul [64][us] (us = 2 H + 1 staged,
 // an odd row stride in doubles: the rate chain's and the staging's row-per-lane accesses are
 // then free of bank conflicts; 2 H unstaged, the rollouts' layout) | x0 [6] | keys [64] | mean /
-// std [2][H][2] | ST: the staged terms [H][64][kNlpStageW] — the completion's region
+// std [2][H][2] | the best sequence so far [H][2] | ST: the staged terms [H][64][kNlpStageW] — the completion's region
 // (nlp_comp_bytes) reuses them once the rollouts are done — else the completion's region |
 // ltraj: the samples' rollout states [64][H][6] (nlp_traj_off).
 __host__ __device__ __forceinline__ size_t nlp_su_off(int H) {
-  return kScratchBytes + 16 * (size_t)(H + 1) + 8 * 64 * (2 * (size_t)H + 1) + 48 + 8 * 64 + 32 * (size_t)H;
+  return kScratchBytes + 16 * (size_t)(H + 1) + 8 * 64 * (2 * (size_t)H + 1) + 48 + 8 * 64 + 48 * (size_t)H;
 }
 // ltraj: the samples' rollout states [64][H][6] after the staged terms / the completion's region
 __host__ __device__ __forceinline__ size_t nlp_traj_off(int H, int nl, int elite) {
@@ -781,6 +764,7 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a, NlpInline pk) {
   double* x0 = Ul + (size_t)kPerBlock * us;                                 // [6]
   uint64_t* ks = reinterpret_cast<uint64_t*>(x0 + 6);                       // [64] the samples' keys
   double* ms = reinterpret_cast<double*>(ks + 64);                          // the round's mean, std [2][H][2]
+  double* bu = ms + 4 * H;                                                  // the best sequence so far [H][2]
   double* su = reinterpret_cast<double*>(smem + nlp_su_off(H));             // ST: [H][64][kNlpStageW]
   unsigned char* cbase = smem + nlp_su_off(H);                              // the completion's region
   double* trl = reinterpret_cast<double*>(smem + nlp_traj_off(H, nl, a.elite));   // ltraj: [64][H][6]
@@ -802,6 +786,8 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a, NlpInline pk) {
   double bjv = nlp_uni(a.it == 0 ? HUGE_VAL : ld_wt(&st->best_j));
   int bitv = __builtin_amdgcn_readfirstlane(a.it == 0 ? -1 : ld_wt(&st->best_it));
   int bsv = __builtin_amdgcn_readfirstlane(a.it == 0 ? -1 : ld_wt(&st->best_s));
+  if (a.it > 0)
+    for (int e = tid; e < 2 * H; e += NT) bu[e] = ld_wt(&st->best_u[0][0] + e);
   for (int r = 0; r < a.rounds; ++r) {
     const int it = a.it + r;
     const uint32_t sq = nlp_seq(a.host_seq, it);
@@ -957,12 +943,22 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a, NlpInline pk) {
     // the round's completion, in every block
     NLP_STAMP(7);
     if (len <= 32) {
-      if (!nlp_complete32(a, smem, cbase, it, r, nl, bjv, bitv, bsv, ms, r + 1 == a.rounds, trl, sx, x0)) return;
+      if (!nlp_complete32(a, smem, cbase, it, r, nl, bjv, bitv, bsv, ms, bu, r + 1 == a.rounds, trl, sx, x0)) return;
     } else {
       const NlpCompLds L = nlp_comp_lds(cbase, nl, len);
       if (!nlp_poll_lists(a, L, nl, it, sq, rflag)) return;
       NLP_STAMP(4);
-      nlp_complete(a, cbase, it, nl, bjv, bitv, bsv, ms, r + 1 == a.rounds, trl, sx, x0);
+      nlp_complete(a, cbase, it, nl, bjv, bitv, bsv, ms, bu, r + 1 == a.rounds, trl, sx, x0);
+    }
+    // one launch per round: the best so far into the state for the next launch (block 0; kept in
+    // registers and LDS within a launch — per-round stores here held block 0's next memory wait)
+    if (r + 1 == a.rounds && it + 1 < a.iters && blk == 0) {
+      for (int e = tid; e < 2 * H; e += NT) st_wt(&st->best_u[0][0] + e, bu[e]);
+      if (tid == 0) {
+        st_wt(&st->best_j, bjv);
+        st_wt(&st->best_it, bitv);
+        st_wt(&st->best_s, bsv);
+      }
     }
   }
 }
