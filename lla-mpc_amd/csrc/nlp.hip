@@ -834,12 +834,17 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a, NlpInline pk) {
     __syncthreads();
     NLP_STAMP(2);
     // the rate-clipped sequences for every block's elite read (each wave drains these stores
-    // before its list is published, below)
+    // before its list is published, below): staged, by the helper waves during the rollouts
+    // (stored here, by every wave, they took ~1.5 us of the round); unstaged, here
     double* cand = nlp_cand(a, it);
-    for (int e = tid; e < kPerBlock * H * 2; e += NT) {
-      const int rr = nlp_div(e, 0.5f * rH);
-      st_wt(&cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e + rr * (us - 2 * H)]);
-    }
+    auto store_cand = [&](int t0, int stride) {
+      for (int e = t0; e < kPerBlock * H * 2; e += stride) {
+        const int rr = nlp_div(e, 0.5f * rH);
+        st_wt(&cand[(size_t)blk * kPerBlock * 2 * H + e], Ul[e + rr * (us - 2 * H)]);
+      }
+    };
+    if constexpr (!ST) store_cand(tid, NT);
+    NLP_STAMP(15);
     const fm::FmK K = fm::FmK::load();
     if constexpr (ST) {
       const CostK& q0 = a.la.cost;
@@ -866,6 +871,7 @@ __global__ __launch_bounds__(NT) void nlp_kernel(NlpLaunch a, NlpInline pk) {
       NLP_STAMP(9);
     }
     // rollouts: a quad per sample (the plan kernel's NLP-Euler fast stage + the general re-run)
+    if (ST && tid >= kPerBlock * LPM) store_cand(tid - kPerBlock * LPM, NT - kPerBlock * LPM);
     if (tid < kPerBlock * LPM) {        // whole waves
     const int sub = tid % LPM, c = tid / LPM;
     const Tire t = load_tire(a.la.params, 1, 0);

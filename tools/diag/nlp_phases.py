@@ -39,8 +39,8 @@ for t in range(10, 16):
     nb = nlp.samples // 64
     base = Z[:nb, 0].min()
     us = lambda v: (v - base) / 100.0  # noqa: E731
-    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (10, 1, 2, 9, 3, 12, 11, 4, 13, 5, 6, 14, 8)]
-    print(f"solve {t}: ms/formed/clipped/staged/rolled0/rolled/published/own4/all-in/merged/elite-issued/"
+    row = [f"{k}: {us(Z[:nb, k]).min():.1f}/{us(Z[:nb, k]).max():.1f}" for k in (10, 1, 2, 15, 9, 3, 12, 11, 4, 13, 5, 6, 14, 8)]
+    print(f"solve {t}: ms/formed/clipped/cand-stored/staged/rolled0/rolled/published/own4/all-in/merged/elite-issued/"
           f"mean/next-ms (min/max) "
           f"{' '.join(row)}", flush=True)
 nlp.close()
