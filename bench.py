@@ -1061,11 +1061,11 @@ def lpm_of(n, C):
 
 
 def pmc_issue(kernel: str, kernel_us: float):
-    """Issue fraction of `kernel` from the committed PMC summary (profiles/r05/pmc_kernels.json,
+    """Issue fraction of `kernel` from the committed PMC summary (profiles/r06/pmc_kernels.json,
     tools/pmc_kernels.py): SQ_INSTS_VALU wave-instructions per dispatch x 64 lanes / kernel_us /
     the chip's issue capacity; None when no pass is committed for the kernel."""
     try:
-        d = json.load(open(os.path.join(REPO, "profiles", "r05", "pmc_kernels.json")))
+        d = json.load(open(os.path.join(REPO, "profiles", "r06", "pmc_kernels.json")))
     except (OSError, ValueError):
         return None
     v = d.get(kernel)
@@ -1073,7 +1073,7 @@ def pmc_issue(kernel: str, kernel_us: float):
         return None
     lane = v["SQ_INSTS_VALU"] * 64
     return {"lane_instr_per_launch": lane, "frac": lane / (kernel_us * 1e-6) / ISSUE_PEAK_LANE_INSTR,
-            "source": "profiles/r05/pmc_kernels.json"}
+            "source": "profiles/r06/pmc_kernels.json"}
 
 
 def pmc_traffic(args):
