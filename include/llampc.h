@@ -438,8 +438,9 @@ int llampc_ctl_destroy(llampc_ctl* ctl);
  * noise, clipped to the bounds, rate-clipped in order), the `elite` best setting the next mean
  * and std.  Replaces nlpsol/IPOPT (nmpc.py:146-157, 192), which this platform lacks: the
  * optimum is NOT IPOPT's (parity unpinned).  The bank holds the ONE model (n = 1).  Every
- * round runs in one launch (the sample blocks wait for each round's mean / std on a tagged
- * word; LLAMPC_NLP_ROUND_LAUNCHES=1 in the environment at create: one launch per round). */
+ * round runs in one launch (every block completes every round from the others' tagged lists;
+ * LLAMPC_NLP_ROUND_LAUNCHES=1 in the environment at create: one launch per round).  The solve's
+ * inputs travel as kernel arguments (no host-to-device copy). */
 typedef struct llampc_nlp_cfg {
   int32_t H, samples, iters, elite;  /* samples: power of two in [64, 4096]; 1 <= elite <= 64      */
   double Ts;
