@@ -83,7 +83,8 @@ for mode in ("paced", "back-to-back"):
             parts.append("|")
         for slot in ((16, 0, 14, 15, 1, 17, 18, 10, 2, 3, 4, 5) if PRE else (0, 14, 15, 1, 17, 18, 10, 2, 3, 4, 5)):
             v = np.array([us(Z[k, slot]) for k in la])
-            parts.append(f"{NAMES[slot]} {v.min():.1f}/{v.max():.1f}")
+            if v.size:                   # armed ticks whose selection the spec blocks covered
+                parts.append(f"{NAMES[slot]} {v.min():.1f}/{v.max():.1f}")   # roll nothing more
         print(" ".join(parts), flush=True)
 ctl.close()
 b.close()
