@@ -2236,6 +2236,8 @@ struct llampc_nlp {
                                          // by round parity)
   uint64_t* d_ms_tag = nullptr;          // [2][4 HMAX]: a round's mean / std (NlpLaunch.ms_tag)
   bool per_round = false;                // one launch per round (LLAMPC_NLP_ROUND_LAUNCHES=1: A/B)
+  bool ltraj = false;                    // the last round keeps its states in LDS (NlpLaunch.ltraj;
+                                         // LLAMPC_NLP_RERUN_TRAJ=1 at create: always re-run, tests)
   NlpResult* h_res = nullptr;            // pinned, coherent, mapped: the last round writes it
   NlpResult* d_res = nullptr;            //   (device alias), then the solve's number into h_tag
   uint64_t* h_tag = nullptr;
@@ -2297,6 +2299,8 @@ int llampc_nlp_create(llampc_bank* b, const llampc_nlp_cfg* cfg, llampc_nlp** ou
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device) != hipSuccess) cus = 0;
     const bool resident = k.samples / 64 <= cus;
     p->per_round = !nlp_persistent(k.samples) || !resident || (e && e[0] == '1');
+    const char* rt = std::getenv("LLAMPC_NLP_RERUN_TRAJ");
+    p->ltraj = nlp_ltraj_fits(k.H, k.samples, k.elite) && !(rt && rt[0] == '1');
   }
   if (hipHostMalloc(reinterpret_cast<void**>(&p->h_res), sizeof(NlpResult), hipHostMallocCoherent | hipHostMallocMapped) !=
           hipSuccess ||
@@ -2351,7 +2355,7 @@ int llampc_nlp_solve(llampc_nlp* p, const double* x0, const double* xref, const 
   a.host_tag = p->d_tag;
   a.host_seq = p->calls + 1;
   a.ms_tag = p->d_ms_tag;
-  a.ltraj = nlp_ltraj_fits(H, k.samples, k.elite);
+  a.ltraj = p->ltraj;
   a.seed = k.seed;
   a.call = p->calls;
   a.up0 = uprev[0];

@@ -1282,6 +1282,36 @@ def test_setupnlp_one_launch_equals_round_launches(nat, monkeypatch):
         np.testing.assert_array_equal(a[2], b[2])
 
 
+def test_setupnlp_kept_states_equal_rerun(nat, monkeypatch):
+    """The result's trajectory copied from the last round's rollout states kept in LDS (nlp.hip
+    NlpLaunch.ltraj, the best sample's own block) against the best sequence's rollout re-run
+    by block 0 (LLAMPC_NLP_RERUN_TRAJ=1 at create): umpc and fval bitwise, xmpc to 1e-12 (the
+    staged and the unstaged rollout of the same inputs), over six successive solves."""
+    from llampc.mpc.planner import ConstantSpeed
+    from llampc.tracks import ETHZ
+    d = golden("dyn_slice.npz")
+    s, u = d["states"], d["inputs"]
+    tr = ETHZ('optimal', True)
+    outs = []
+    for rerun in ("0", "1"):
+        monkeypatch.setenv("LLAMPC_NLP_RERUN_TRAJ", rerun)
+        nlp, _ = _nlp()
+        try:
+            got = []
+            for t in range(20, 26):
+                x0, up = s[:, t].copy(), u[:, t - 1].copy()
+                xref, _, _ = ConstantSpeed(x0[:2], x0[3], tr, 20, TS, 0)
+                umpc, fval, xmpc, _ = nlp.solve(x0, xref, up)
+                got.append((np.array(umpc, copy=True), float(fval), np.array(xmpc, copy=True)))
+        finally:
+            nlp.close()
+        outs.append(got)
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a[0], b[0])
+        assert a[1] == b[1]
+        np.testing.assert_allclose(a[2], b[2], rtol=1e-12, atol=1e-14)
+
+
 @pytest.mark.parametrize("samples,elite,iters,H", [(64, 5, 3, 20), (256, 17, 3, 20), (4096, 64, 2, 20), (1024, 1, 2, 20),
                                                    (512, 32, 3, 40)])
 def test_setupnlp_cem_shapes_equal_oracle(nat, samples, elite, iters, H):
